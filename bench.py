@@ -1,0 +1,286 @@
+#!/usr/bin/env python3
+"""Benchmark: MossTTSDelay generate() throughput (audio-seconds/sec) on MI355X.
+
+Workload (BASELINE.json configs[1]): MossTTSDelay-8B shape (Qwen3-8B backbone, 36 layers,
+h 4096, 32/8 heads, I 12288, V 151936, n_vq 32), bf16, random-init weights (no checkpoint
+is available offline), batch 1 per GPU, a synthetic zero-shot-clone prompt (3 s of
+reference audio = 38 frames in a user audio block + a 200-character text, T = 180 tokens),
+greedy decoding with a forced text schedule of 208 steps (audio_start, 173 gen slots,
+the delay tail, audio_end, im_end) so every run does the same work.
+
+One "step" = one complete generate() call (prefill + 208 hipGraph decode steps) for the
+batch resident in HBM.  value = audio seconds produced by all ranks / max-over-ranks wall
+time.  Run N GPUs with torch.distributed.run (one process per GPU, no collective in the
+data path: utterances are independent, weak scaling).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "audio-seconds/sec/GPU (RTF) + p50 first-chunk latency, MossTTSDelay b=1/32"
+FRAME_RATE = 12.5
+HBM_PEAK_GBS = 8000.0
+
+
+def synthetic_prompt(cfg, rng, text_tokens=48, ref_frames=38, template_tokens=56):
+    """Clone prompt laid out like processing_moss_tts.py:539-641 (user turn with an audio
+    block of ref_frames delayed frames, assistant header); random ids stand in for text."""
+    n_vq, pad = cfg["n_vq"], 1024
+    rows = []
+
+    def text(t):
+        rows.append([int(t)] + [pad] * n_vq)
+
+    text(151644)
+    for t in rng.integers(200, 20000, template_tokens):
+        text(t)
+    codes = rng.integers(0, 1024, (ref_frames, n_vq))
+    dl = np.full((ref_frames + n_vq - 1, n_vq), pad, np.int64)
+    for i in range(n_vq):
+        dl[i:i + ref_frames, i] = codes[:, i]
+    text(151652)
+    for r in dl:
+        rows.append([151654] + [int(v) for v in r])
+    text(151653)
+    for t in rng.integers(200, 20000, text_tokens):
+        text(t)
+    for t in (151645, 198, 151644, 77091, 198):
+        text(t)
+    return np.array(rows, np.int64)
+
+
+def forced_schedule(n_steps, n_vq, gen_frames):
+    """text decisions for rows that sample: audio_start, gen slots, delay slot, ..., im_end"""
+    f = np.full(n_steps, -1, np.int32)
+    f[0] = 151652
+    f[1:1 + gen_frames] = 151656
+    f[1 + gen_frames] = 151662
+    f[n_steps - 1] = 151645
+    return f
+
+
+def count_audio_frames(gen_row, start, n_vq):
+    import torch
+    from moss_tts_amd.processing_moss_tts import split_audio_segments
+    a = torch.from_numpy(gen_row[start:, 1:])
+    segs = split_audio_segments(a, 1024) if a.shape[0] >= n_vq else []
+    return sum(int(s.shape[0]) for s in segs)
+
+
+def cpu_baseline(args, T, n_steps, frames):
+    """The oracle (numpy fp32 restatement, pinned to the reference) at the full 8B shape on
+    this host's cores, on a bounded sample: one prefill layer over T tokens, 3 decode
+    layer-steps and one pass of the 1+32 heads; composed into one utterance
+    (36 layers x (prefill + n_steps decode) + heads per step)."""
+    from oracle import moss_delay as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [os.cpu_count() or 1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    cfg = O.Cfg()
+    ctx = O._Ctx("fp32")
+    rng = np.random.default_rng(0)
+    H, I, D = cfg.hidden, cfg.inter, cfg.head_dim
+    W = {}
+    p = "language_model.layers.0."
+
+    def rnd(shape, s):
+        return (rng.standard_normal(shape, dtype=np.float32) * np.float32(s))
+
+    W[p + "self_attn.q_proj.weight"] = rnd((cfg.n_heads * D, H), H ** -0.5)
+    W[p + "self_attn.k_proj.weight"] = rnd((cfg.n_kv * D, H), H ** -0.5)
+    W[p + "self_attn.v_proj.weight"] = rnd((cfg.n_kv * D, H), H ** -0.5)
+    W[p + "self_attn.o_proj.weight"] = rnd((H, cfg.n_heads * D), H ** -0.5)
+    W[p + "self_attn.q_norm.weight"] = np.ones(D, np.float32)
+    W[p + "self_attn.k_norm.weight"] = np.ones(D, np.float32)
+    W[p + "mlp.gate_proj.weight"] = rnd((I, H), H ** -0.5)
+    W[p + "mlp.up_proj.weight"] = rnd((I, H), H ** -0.5)
+    W[p + "mlp.down_proj.weight"] = rnd((H, I), I ** -0.5)
+    W[p + "input_layernorm.weight"] = np.ones(H, np.float32)
+    W[p + "post_attention_layernorm.weight"] = np.ones(H, np.float32)
+    cos, sin = O.rope_cos_sin(ctx, cfg, np.arange(T + 8))
+    cache = O.KVCache(1)
+    h = rnd((1, T, H), 1.0)
+    t0 = time.perf_counter()
+    O.decoder_layer(ctx, W, cfg, 0, h, cos[:T], sin[:T], cache, np.ones((1, T), bool), np.arange(T))
+    t_prefill_layer = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    nd = 3
+    for s in range(nd):
+        x = rnd((1, 1, H), 1.0)
+        O.decoder_layer(ctx, W, cfg, 0, x, cos[T + s:T + s + 1], sin[T + s:T + s + 1], cache,
+                        np.ones((1, T + s + 1), bool), np.array([T + s]))
+    t_dec_layer = (time.perf_counter() - t0) / nd
+    del W
+    heads = rnd((cfg.heads_rows, H), H ** -0.5)
+    x = rnd((1, H), 1.0)
+    t0 = time.perf_counter()
+    _ = x @ heads.T
+    t_heads = time.perf_counter() - t0
+    del heads
+    utt = cfg.layers * (t_prefill_layer + n_steps * t_dec_layer) + (n_steps + 1) * t_heads
+    return {"value": round(frames / FRAME_RATE / utt, 5), "unit": "audio-s/s", "cores": int(cores), "kind": "port",
+            "sample": (f"oracle fp32 at the 8B shape, batch 1: 1 prefill layer (T={T}) + {nd} decode layer-steps + "
+                       f"1 heads GEMV timed ({t_prefill_layer:.2f}s, {t_dec_layer * 1e3:.1f}ms/layer-step, "
+                       f"{t_heads * 1e3:.0f}ms), composed to one utterance of {n_steps} steps = {utt:.1f}s")}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
+    ap.add_argument("--layers", type=int, default=36)
+    ap.add_argument("--decode-steps", type=int, default=208)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-roofline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from moss_tts_amd.engine import Engine, EngineConfig, sampling_params
+    n_steps = args.decode_steps
+    gen_frames = n_steps - 35
+    cfgd = dict(n_vq=32)
+    rng = np.random.default_rng(1 + rank)
+    prompts = [synthetic_prompt(cfgd, rng) for _ in range(args.batch)]
+    T = max(p.shape[0] for p in prompts)
+    from moss_tts_amd.processing_moss_tts import left_pad
+    padded = left_pad([torch.from_numpy(p) for p in prompts], 151643, 1024)
+    ids, mask = padded["input_ids"].numpy(), padded["attention_mask"].numpy()
+    ecfg = EngineConfig(layers=args.layers, max_batch=max(args.batch, 1), max_ctx=T + n_steps + 16,
+                        max_prefill_tokens=max(T * args.batch, 256))
+    eng = Engine(ecfg, local)
+    eng.init_random(seed=0)
+    ids_d = torch.from_numpy(ids).cuda()
+    mask_d = torch.from_numpy(mask.astype(np.uint8)).cuda()
+    forced = torch.from_numpy(forced_schedule(n_steps, 32, gen_frames)).cuda()
+    sp = sampling_params(text_temperature=0, audio_temperature=0)
+
+    def one():
+        return eng.generate_ids(ids_d, mask_d, n_steps, sp, forced_text=forced, chunk=16)
+
+    for _ in range(args.warmup):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    # frames actually produced (de-delayed, non-pad rows after the assistant start)
+    g = out.cpu().numpy()
+    start = T  # generation starts after the trailing "<|im_start|>assistant\n" (im_start + 3)
+    frames = [count_audio_frames(g[b], start, 32) for b in range(args.batch)]
+    audio_s = sum(frames) / FRAME_RATE * args.steps
+    t = torch.tensor([dt, audio_s], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        t[0] = tmax[0]
+    dt_max, audio_total = float(t[0]), float(t[1])
+
+    # first-chunk latency: prefill + decode until the first 1 s of audio (13 frames) has all
+    # n_vq codebooks (frame f is complete n_vq steps after its first codebook), codec excluded
+    lat = []
+    from moss_tts_amd import _native as Nn
+    import ctypes
+    first_steps = 1 + 13 + 32
+    t_begin = []
+    for _ in range(3):  # prefill + step 0 alone
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        Nn.check(Nn.load().mtts_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()),
+                                               ctypes.c_void_p(mask_d.data_ptr()), args.batch, T, n_steps,
+                                               ctypes.byref(sp), ctypes.c_void_p(forced.data_ptr()), None), "begin")
+        Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
+        t_begin.append((time.perf_counter() - a) * 1e3)
+    t_begin = float(np.median(t_begin))
+    for _ in range(5):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        Nn.check(Nn.load().mtts_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()),
+                                               ctypes.c_void_p(mask_d.data_ptr()), args.batch, T, n_steps,
+                                               ctypes.byref(sp), ctypes.c_void_p(forced.data_ptr()), None), "begin")
+        Nn.check(Nn.load().mtts_generate_decode(eng._h, first_steps - 1, None), "decode")
+        Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
+        lat.append((time.perf_counter() - a) * 1e3)
+    p50 = float(np.median(lat))
+
+    res = None
+    if rank == 0:
+        wb = eng.weight_bytes()
+        step_ms = None
+        roof = None
+        if not args.no_roofline:
+            # dominant kernel: the gate|up GEMV with the fused SwiGLU (201 MB of weights per launch)
+            ms = ctypes.c_float()
+            nb = ctypes.c_uint64()
+            Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 2, 0, args.batch, 50, ctypes.byref(ms), ctypes.byref(nb)),
+                     "time_gemv")
+            ach = nb.value / (ms.value * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": "gemv_kernel<1,2,EPI_SWIGLU> (gate|up + SwiGLU, layer 0)",
+                    "alg_bytes_per_launch": int(nb.value), "avg_launch_us": round(ms.value * 1e3, 2)}
+        # whole decode step against the weight-stream roofline
+        per_utt_ms = dt_max / args.steps * 1e3
+        res = {
+            "metric": METRIC, "value": round(audio_total / dt_max, 4), "unit": "audio-s/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(per_utt_ms, 3), "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init bf16 weights at the MossTTSDelay-8B shape; synthetic clone prompts)",
+            "config": {"workload": "MossTTSDelay bf16 batch=1 zero-shot clone (3s prompt audio) on 1xMI355X, hipGraph "
+                                   "decode" if args.batch == 1 else f"MossTTSDelay bf16 batch={args.batch}/GPU",
+                       "batch_per_gpu": args.batch, "prompt_tokens": int(T), "decode_steps": n_steps,
+                       "layers": args.layers, "parallelism": f"dp{world}", "sampling": "greedy, forced text schedule"},
+            "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
+            "audio_frames_per_utt": frames[0],
+            "p50_first_chunk_ms": round(p50, 2),
+            "first_chunk_def": "prefill + 46 decode steps (first 1 s of audio codes complete), codec excluded",
+            "decode_weight_bytes": wb,
+            "roofline": roof,
+        }
+        step_ms = (per_utt_ms - t_begin) / (n_steps - 1)
+        res["prefill_ms"] = round(t_begin, 3)
+        res["ms_per_decode_step"] = round(step_ms, 4)
+        res["decode_step_hbm_frac"] = round(wb / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline(args, int(T), n_steps, frames[0])
+        elif not args.no_cpu_baseline:
+            res["cpu_baseline"] = None
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

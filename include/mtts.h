@@ -1,0 +1,136 @@
+/* mtts.h -- C ABI of libmtts.so, the MI355X (gfx950) MossTTSDelay decode engine.
+ *
+ * Drop-in boundary.  The Python package `moss_tts_amd` binds these
+ * entry points with ctypes; any other host (cgo, JNI, N-API) can bind them the same
+ * way.  No torch types cross this boundary: plain pointers, sizes
+ * and a hipStream_t (passed as void*).  All `*_dev` pointers are device memory owned
+ * by the caller; the engine owns weights, KV cache and workspaces.
+ *
+ * Errors: every function returns 0 on success or a negative MTTS_E_* code;
+ * mtts_last_error() returns a thread-local message.  Threading: one engine = one
+ * device = one stream at a time (not re-entrant per engine); engines on different
+ * devices may run concurrently (one process per GPU for data parallelism).
+ */
+#ifndef MTTS_H
+#define MTTS_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTTS_OK 0
+#define MTTS_E_INVALID -1     /* bad shape / argument (reference raises ValueError) */
+#define MTTS_E_OOM -2
+#define MTTS_E_HIP -3         /* HIP runtime error */
+#define MTTS_E_UNSUPPORTED -4 /* config the kernels do not cover */
+
+typedef struct mtts_engine mtts_engine;
+
+/* Model + capacity configuration.  Model fields restate MossTTSDelayConfig
+ * (moss_tts_delay/configuration_moss_tts.py:62-103) and the nested Qwen3Config. */
+typedef struct mtts_config {
+  int hidden, layers, n_heads, n_kv, head_dim, inter, vocab;
+  int n_vq, audio_vocab; /* audio heads/embeddings have audio_vocab + 1 rows */
+  float rope_theta, rms_eps;
+  int pad_token_id, im_start_token_id, im_end_token_id, audio_start_token_id, audio_end_token_id;
+  int audio_user_slot_token_id, audio_assistant_gen_slot_token_id, audio_assistant_delay_slot_token_id;
+  int audio_pad_code;
+  /* capacity */
+  int max_batch;          /* rows per generate() call */
+  int max_ctx;            /* prompt + max_new_tokens */
+  int max_prefill_tokens; /* rows x prompt tokens processed per prefill chunk */
+} mtts_config;
+
+/* generate() keyword arguments (modeling_moss_tts.py:393-405); temperature <= 0 = greedy */
+typedef struct mtts_sampling {
+  float text_temperature, text_top_p;
+  int text_top_k;
+  float audio_temperature, audio_top_p;
+  int audio_top_k;
+  float audio_repetition_penalty;
+  uint64_t seed; /* Philox key for the multinomial draws */
+} mtts_sampling;
+
+const char* mtts_last_error(void);
+int mtts_version(void);
+
+/* ---- engine lifecycle --------------------------------------------------- */
+/* replaces AutoModel.from_pretrained(...).to(device) (clis/moss_tts_app.py:95-107) */
+int mtts_engine_create(const mtts_config* cfg, int device, mtts_engine** out);
+int mtts_engine_destroy(mtts_engine* eng);
+/* Re-size the capacity buffers (KV cache, workspaces, generate state); weights are kept. */
+int mtts_engine_reserve(mtts_engine* eng, int max_batch, int max_ctx, int max_prefill_tokens);
+/* Load one tensor by its reference state_dict name (modeling_moss_tts.py:170-191,
+ * e.g. "language_model.layers.3.mlp.gate_proj.weight"); src is bf16 row-major in the
+ * reference shape, on the host (src_on_device = 0) or the device (1).  The engine
+ * repacks matrices into its MFMA-tile layout. */
+int mtts_engine_load_weight(mtts_engine* eng, const char* name, const void* src, size_t bytes, int src_on_device);
+/* Fill every weight with the portable splitmix64 init of oracle/prng.py (benchmarks). */
+int mtts_engine_init_random(mtts_engine* eng, uint64_t seed);
+/* Total bytes of weights streamed per decode step (for roofline accounting). */
+int mtts_engine_weight_bytes(const mtts_engine* eng, uint64_t* bytes);
+/* Roofline probe: average duration (HIP events, engine stream) of one GEMV of the loaded
+ * model -- which: 0 q|k|v, 1 o_proj, 2 gate|up+SwiGLU, 3 down, 4 heads -- and its
+ * algorithmic bytes per launch (weights once + activations + outputs). */
+int mtts_engine_time_gemv(mtts_engine* eng, int which, int layer, int B, int iters, float* avg_ms,
+                          uint64_t* alg_bytes);
+
+/* ---- forward (teacher-forced; MossTTSDelayModel.forward, modeling_moss_tts.py:225-300) ----
+ * Appends S tokens per row at positions past..past+S-1 (left pads included, like
+ * TF/.../modeling_qwen3.py:386-389).  ids_dev int64 [B,S,1+n_vq]; mask_dev uint8
+ * [B, past+S] (1 = attend); logits_dev bf16 [B, heads_ld] receives the last position's
+ * logits of all 1+n_vq heads concatenated (text | audio_0 | ...), audio pad column = -inf. */
+int mtts_forward(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int S, int past,
+                 uint16_t* logits_dev, void* stream);
+int mtts_heads_ld(const mtts_engine* eng);
+
+/* ---- generate (MossTTSDelayModel.generate, modeling_moss_tts.py:392-525) ----
+ * begin: state init + prefill + the step-0 sampling.  decode: n more steps (hipGraph).
+ * forced_text_dev (int32 [max_new_tokens], -1 = free) optionally overrides the text token
+ * of rows that sample the text channel (benchmark schedule); pass NULL normally. */
+int mtts_generate_begin(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int T,
+                        int max_new_tokens, const mtts_sampling* sp, const int32_t* forced_text_dev, void* stream);
+int mtts_generate_decode(mtts_engine* eng, int n_steps, void* stream);
+/* synchronises the stream; *steps = sampled steps so far, *done_step = step at which
+ * every row had emitted im_end (-1 if none) */
+int mtts_generate_poll(mtts_engine* eng, int* steps, int* done_step, void* stream);
+/* whole loop: begin + decode in chunks until every row stopped or max_new_tokens;
+ * *n_rows = generated rows per sequence (reference generation_ids width - T) */
+int mtts_generate(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int T,
+                  int max_new_tokens, const mtts_sampling* sp, const int32_t* forced_text_dev, int chunk,
+                  int* n_rows, void* stream);
+/* copy generation_ids [B, T + n_rows, 1+n_vq] (prompt included) to out_dev */
+int mtts_generate_fetch(mtts_engine* eng, int64_t* out_dev, int n_rows, void* stream);
+
+/* ---- kernel-level entry points (unit parity; device pointers, explicit shapes) ---- */
+/* pack W [rows,K] bf16 into MFMA tiles; interleave=1 places gate/up tile pairs */
+int mtts_k_pack(const uint16_t* src, uint16_t* dst, int rows, int K, int row_offset, int interleave, int which,
+                void* stream);
+size_t mtts_k_packed_bytes(int rows, int K);
+/* y[B,N] = epi(x[B,K] . W^T); epi 0 store, 1 residual add (res), 2 swiglu (N = I), 3 logits */
+int mtts_k_gemv(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                int ldres, int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, void* stream);
+int mtts_k_rmsnorm(const uint16_t* x, size_t x_off, size_t x_stride, const uint16_t* w, uint16_t* y, int M, int H,
+                   float eps, void* stream);
+int mtts_k_embed(const int64_t* ids, int C, const uint16_t* emb_text, const uint16_t* emb_audio, int audio_rows,
+                 int H, uint16_t* h, int M, void* stream);
+/* q/k RMSNorm + RoPE (cos/sin bf16 [max_pos, D]) + cache append; pos_base_dev int32 */
+int mtts_k_qk_norm_rope(const uint16_t* qkv, uint16_t* q_out, uint16_t* kc, uint16_t* vc, const uint16_t* qn_w,
+                        const uint16_t* kn_w, const uint16_t* cos_t, const uint16_t* sin_t, const int32_t* pos_base_dev,
+                        int M, int S, int Hq, int Hkv, int D, int Cmax, float eps, void* stream);
+/* attention over the cache; q [M, Hq*D]; workspace_dev >= mtts_k_attention_ws_bytes */
+size_t mtts_k_attention_ws_bytes(int M, int Hq, int D, int n_split);
+int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
+                     const int32_t* pos_base_dev, uint16_t* out, void* workspace_dev, int M, int S, int Hq, int Hkv,
+                     int D, int Cmax, int CH, int n_split, void* stream);
+/* RoPE table exactly as the engine builds it: bf16 cos/sin [n_pos, D] on the host */
+int mtts_rope_table(float theta, int D, int n_pos, uint16_t* cos_host, uint16_t* sin_host);
+int mtts_k_fill_uniform(uint16_t* dst, size_t n, uint64_t seed, uint64_t tensor_id, float scale, float offset,
+                        void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,111 @@
+"""ctypes binding of libmtts.so (the C ABI in include/mtts.h).
+
+There is no fallback: if the HIP library is missing or fails to load, every
+entry point raises.  Error codes map to the exceptions the reference raises
+(ValueError for bad shapes, `modeling_moss_tts.py:253-254`; RuntimeError for
+runtime failures).
+"""
+import ctypes
+import os
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmtts.so")
+
+MTTS_OK = 0
+MTTS_E_INVALID = -1
+MTTS_E_OOM = -2
+MTTS_E_HIP = -3
+MTTS_E_UNSUPPORTED = -4
+
+
+class MttsConfig(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("hidden", "layers", "n_heads", "n_kv", "head_dim", "inter", "vocab",
+                                            "n_vq", "audio_vocab")] + \
+               [("rope_theta", ctypes.c_float), ("rms_eps", ctypes.c_float)] + \
+               [(n, ctypes.c_int) for n in ("pad_token_id", "im_start_token_id", "im_end_token_id",
+                                            "audio_start_token_id", "audio_end_token_id",
+                                            "audio_user_slot_token_id", "audio_assistant_gen_slot_token_id",
+                                            "audio_assistant_delay_slot_token_id", "audio_pad_code",
+                                            "max_batch", "max_ctx", "max_prefill_tokens")]
+
+
+class MttsSampling(ctypes.Structure):
+    _fields_ = [("text_temperature", ctypes.c_float), ("text_top_p", ctypes.c_float), ("text_top_k", ctypes.c_int),
+                ("audio_temperature", ctypes.c_float), ("audio_top_p", ctypes.c_float), ("audio_top_k", ctypes.c_int),
+                ("audio_repetition_penalty", ctypes.c_float), ("seed", ctypes.c_uint64)]
+
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+SZ = ctypes.c_size_t
+U64 = ctypes.c_uint64
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "mtts_last_error": (ctypes.c_char_p, []),
+    "mtts_version": (I, []),
+    "mtts_engine_create": (I, [ctypes.POINTER(MttsConfig), I, ctypes.POINTER(P)]),
+    "mtts_engine_destroy": (I, [P]),
+    "mtts_engine_reserve": (I, [P, I, I, I]),
+    "mtts_engine_load_weight": (I, [P, ctypes.c_char_p, P, SZ, I]),
+    "mtts_engine_init_random": (I, [P, U64]),
+    "mtts_engine_weight_bytes": (I, [P, ctypes.POINTER(U64)]),
+    "mtts_engine_time_gemv": (I, [P, I, I, I, I, ctypes.POINTER(F), ctypes.POINTER(U64)]),
+    "mtts_forward": (I, [P, P, P, I, I, I, P, P]),
+    "mtts_heads_ld": (I, [P]),
+    "mtts_generate_begin": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, P]),
+    "mtts_generate_decode": (I, [P, I, P]),
+    "mtts_generate_poll": (I, [P, ctypes.POINTER(I), ctypes.POINTER(I), P]),
+    "mtts_generate": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, I, ctypes.POINTER(I), P]),
+    "mtts_generate_fetch": (I, [P, P, I, P]),
+    "mtts_k_pack": (I, [P, P, I, I, I, I, I, P]),
+    "mtts_k_packed_bytes": (SZ, [I, I]),
+    "mtts_k_gemv": (I, [P, P, I, P, I, P, I, I, I, I, I, I, I, I, P]),
+    "mtts_k_rmsnorm": (I, [P, SZ, SZ, P, P, I, I, F, P]),
+    "mtts_k_embed": (I, [P, I, P, P, I, I, P, I, P]),
+    "mtts_k_qk_norm_rope": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P]),
+    "mtts_k_attention_ws_bytes": (SZ, [I, I, I, I]),
+    "mtts_k_attention": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
+    "mtts_rope_table": (I, [F, I, I, P, P]),
+    "mtts_k_fill_uniform": (I, [P, SZ, U64, U64, F, F, P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+_lib = None
+
+
+def lib_path():
+    return _LIB_PATH
+
+
+def load():
+    """Load libmtts.so (raises if it is missing: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise RuntimeError(f"libmtts.so not found at {_LIB_PATH}; build it with "
+                           "`python -c 'import __graft_entry__ as g; g.build()'` or `make -C moss_tts_amd/csrc`")
+    lib = ctypes.CDLL(_LIB_PATH)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc, what=""):
+    if rc == MTTS_OK:
+        return
+    msg = load().mtts_last_error().decode(errors="replace")
+    if rc == MTTS_E_INVALID:
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what} failed ({rc}): {msg}")
+
+
+def call(name, *args):
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+    return rc

@@ -1,0 +1,705 @@
+// libmtts engine: weights, KV cache, workspaces, prefill, hipGraph-captured decode steps,
+// and the C ABI declared in include/mtts.h.
+//
+// Reference behaviour restated here (everything device-side lives in the .hip files):
+//   MossTTSDelayModel.forward   moss_tts_delay/modeling_moss_tts.py:225-300
+//   MossTTSDelayModel.generate  moss_tts_delay/modeling_moss_tts.py:392-525
+//   Qwen3Model.forward          transformers/models/qwen3/modeling_qwen3.py:367-427
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mtts.h"
+#include "kernels.h"
+
+using namespace mtts;
+
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return fail(MTTS_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+constexpr int CH_DECODE = 64;
+constexpr int CH_PREFILL = 256;
+constexpr int TEXT_PARTS = 64;
+
+struct LayerW {
+  bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
+};
+
+size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
+
+}  // namespace
+
+struct mtts_engine {
+  mtts_config c{};
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  int qkv_rows = 0, audio_rows = 0, heads_rows = 0, heads_ld = 0;
+  std::vector<LayerW> L;
+  bf16_t *emb_text = nullptr, *emb_audio = nullptr, *final_norm = nullptr, *heads = nullptr;
+  bf16_t *kc = nullptr, *vc = nullptr;
+  size_t layer_kv = 0;  // elements per layer in kc / vc
+  bf16_t *cos_t = nullptr, *sin_t = nullptr;
+  uint8_t* mask = nullptr;
+  // workspace
+  int Mmax = 0;
+  bf16_t *h = nullptr, *xn = nullptr, *qkvb = nullptr, *qb = nullptr, *attnb = nullptr, *act = nullptr;
+  float* part = nullptr;
+  size_t part_floats = 0;
+  bf16_t* logits = nullptr;
+  int* d_pos = nullptr;  // pos_base for teacher-forced forwards / prefill
+  // generate state
+  GenDev* st = nullptr;
+  GenDev hst{};
+  int *is_stopping = nullptr, *is_audio = nullptr, *text_cand = nullptr, *audio_cand = nullptr, *part_idx = nullptr;
+  int64_t *audio_len = nullptr, *delayed = nullptr, *cur_ids = nullptr, *gen_ids = nullptr;
+  uint8_t* seen = nullptr;
+  float* part_val = nullptr;
+  const int* forced = nullptr;
+  int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
+  struct Graph { hipGraphExec_t exec; const int* forced; };
+  std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
+  std::vector<void*> allocs;      // weights
+  std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)
+  bool cap_mode = false;
+  bf16_t* staging = nullptr;
+  size_t staging_bytes = 0;
+  uint64_t step_weight_bytes = 0;
+
+  template <class T>
+  int alloc(T** p, size_t n) {
+    void* q = nullptr;
+    if (n == 0) n = 1;
+    if (hipMalloc(&q, n * sizeof(T)) != hipSuccess) return fail(MTTS_E_OOM, "hipMalloc failed (" + std::to_string(n * sizeof(T)) + " B)");
+    (cap_mode ? cap_allocs : allocs).push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+  GenBufs bufs() const {
+    GenBufs g;
+    g.st = st; g.logits = logits; g.is_stopping = is_stopping; g.is_audio = is_audio;
+    g.audio_len = audio_len; g.delayed = delayed; g.cur_ids = cur_ids; g.gen_ids = gen_ids; g.mask = mask;
+    g.seen = seen; g.part_val = part_val; g.part_idx = part_idx; g.text_cand = text_cand; g.audio_cand = audio_cand;
+    g.forced = forced;
+    return g;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// RoPE table (TF/.../modeling_qwen3.py:106-137): inv_freq = 1/theta^(2i/D) with the power
+// correctly rounded to fp32 and an fp32 division; freqs = fp32(inv_freq * pos); cos/sin
+// evaluated in double, rounded to fp32, then to bf16 (RNE).
+static uint16_t host_f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+extern "C" int mtts_rope_table(float theta, int D, int n_pos, uint16_t* cos_h, uint16_t* sin_h) {
+  if (D <= 0 || D % 2 || n_pos <= 0 || !cos_h || !sin_h) return fail(MTTS_E_INVALID, "bad rope table args");
+  std::vector<float> inv(D / 2);
+  for (int i = 0; i < D / 2; ++i) {
+    const float e = (float)(2 * i) / (float)D;
+    const float p = (float)std::pow((double)theta, (double)e);
+    inv[i] = 1.0f / p;
+  }
+  for (int pos = 0; pos < n_pos; ++pos)
+    for (int d = 0; d < D; ++d) {
+      const float f = inv[d % (D / 2)] * (float)pos;
+      cos_h[(size_t)pos * D + d] = host_f2bf((float)std::cos((double)f));
+      sin_h[(size_t)pos * D + d] = host_f2bf((float)std::sin((double)f));
+    }
+  return 0;
+}
+
+extern "C" const char* mtts_last_error(void) { return g_err.c_str(); }
+extern "C" int mtts_version(void) { return 1; }
+
+extern "C" int mtts_engine_destroy(mtts_engine* e) {
+  if (!e) return 0;
+  hipSetDevice(e->device);
+  for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second.exec);
+  for (void* p : e->allocs) hipFree(p);
+  for (void* p : e->cap_allocs) hipFree(p);
+  if (e->staging) hipFree(e->staging);
+  if (e->ev_in) hipEventDestroy(e->ev_in);
+  if (e->ev_out) hipEventDestroy(e->ev_out);
+  if (e->stream) hipStreamDestroy(e->stream);
+  delete e;
+  return 0;
+}
+
+// capacity-dependent buffers (KV cache, RoPE table, mask, workspaces, generate state);
+// weights are untouched, so mtts_engine_reserve can grow these without a reload
+static int alloc_capacity(mtts_engine* e) {
+  const mtts_config& c = e->c;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
+  int rc = 0;
+  e->cap_mode = true;
+  // KV cache [layer][Bmax][Hkv][Cmax][D]
+  e->layer_kv = (size_t)c.max_batch * Hkv * c.max_ctx * D;
+  if ((rc = e->alloc(&e->kc, e->layer_kv * c.layers)) || (rc = e->alloc(&e->vc, e->layer_kv * c.layers))) return rc;
+  if ((rc = e->alloc(&e->cos_t, (size_t)c.max_ctx * D)) || (rc = e->alloc(&e->sin_t, (size_t)c.max_ctx * D))) return rc;
+  {
+    std::vector<uint16_t> cs((size_t)c.max_ctx * D), sn((size_t)c.max_ctx * D);
+    mtts_rope_table(c.rope_theta, D, c.max_ctx, cs.data(), sn.data());
+    hipMemcpy(e->cos_t, cs.data(), cs.size() * 2, hipMemcpyHostToDevice);
+    hipMemcpy(e->sin_t, sn.data(), sn.size() * 2, hipMemcpyHostToDevice);
+  }
+  if ((rc = e->alloc(&e->mask, (size_t)c.max_batch * c.max_ctx))) return rc;
+  // workspaces
+  e->Mmax = std::max(c.max_batch, c.max_prefill_tokens);
+  const size_t M = e->Mmax;
+  if ((rc = e->alloc(&e->h, M * H)) || (rc = e->alloc(&e->xn, M * H)) || (rc = e->alloc(&e->qkvb, M * e->qkv_rows)) ||
+      (rc = e->alloc(&e->qb, M * Hq * D)) || (rc = e->alloc(&e->attnb, M * Hq * D)) || (rc = e->alloc(&e->act, M * I)))
+    return rc;
+  const size_t ns_dec = (c.max_ctx + CH_DECODE - 1) / CH_DECODE;
+  const size_t ns_pf = (c.max_ctx + CH_PREFILL - 1) / CH_PREFILL;
+  e->part_floats = std::max((size_t)c.max_batch * ns_dec, M * ns_pf) * Hq * (D + 2);
+  if ((rc = e->alloc(&e->part, e->part_floats))) return rc;
+  if ((rc = e->alloc(&e->logits, (size_t)c.max_batch * e->heads_ld))) return rc;
+  if ((rc = e->alloc(&e->d_pos, 4))) return rc;
+  // generate state
+  const int B = c.max_batch;
+  if ((rc = e->alloc(&e->st, 1)) || (rc = e->alloc(&e->is_stopping, B)) || (rc = e->alloc(&e->is_audio, B)) ||
+      (rc = e->alloc(&e->text_cand, B)) || (rc = e->alloc(&e->audio_cand, (size_t)B * c.n_vq)) ||
+      (rc = e->alloc(&e->part_idx, (size_t)B * TEXT_PARTS * MAXK)) || (rc = e->alloc(&e->part_val, (size_t)B * TEXT_PARTS * MAXK)) ||
+      (rc = e->alloc(&e->audio_len, B)) || (rc = e->alloc(&e->delayed, B)) || (rc = e->alloc(&e->cur_ids, (size_t)B * (c.n_vq + 1))) ||
+      (rc = e->alloc(&e->gen_ids, (size_t)B * c.max_ctx * (c.n_vq + 1))) || (rc = e->alloc(&e->seen, 2 * e->audio_rows)))
+    return rc;
+  e->cap_mode = false;
+  return 0;
+}
+
+extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engine** out) {
+  if (!cfg || !out) return fail(MTTS_E_INVALID, "null argument");
+  const mtts_config& c = *cfg;
+  if (c.hidden % 32 || c.inter % 32 || c.head_dim % 8 || c.head_dim > 128 || c.n_heads % c.n_kv ||
+      (c.n_heads * c.head_dim) % 32 || c.max_batch <= 0 || c.max_batch > 256 || c.max_ctx <= 0 || c.n_vq < 1)
+    return fail(MTTS_E_UNSUPPORTED, "unsupported model shape");
+  const int G = c.n_heads / c.n_kv;
+  if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MTTS_E_UNSUPPORTED, "GQA group must be 1/2/4/8");
+  if ((c.vocab + TEXT_PARTS - 1) / TEXT_PARTS > 4096) return fail(MTTS_E_UNSUPPORTED, "text vocab too large");
+  if (c.audio_vocab + 1 > 1040) return fail(MTTS_E_UNSUPPORTED, "audio vocab too large");
+  if (hipSetDevice(device) != hipSuccess) return fail(MTTS_E_HIP, "hipSetDevice failed");
+  mtts_engine* e = new mtts_engine();
+  e->c = c;
+  if (e->c.max_prefill_tokens <= 0) e->c.max_prefill_tokens = 8192;
+  e->device = device;
+  auto bail = [&](int rc) {
+    mtts_engine_destroy(e);
+    return rc;
+  };
+  if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(MTTS_E_HIP, "stream"));
+  hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming);
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
+  e->qkv_rows = (Hq + 2 * Hkv) * D;
+  e->audio_rows = c.audio_vocab + 1;
+  e->heads_rows = c.vocab + c.n_vq * e->audio_rows;
+  e->heads_ld = e->heads_rows;
+  int rc = 0;
+  e->L.resize(c.layers);
+  uint64_t wb = 0;
+  for (int l = 0; l < c.layers; ++l) {
+    LayerW& w = e->L[l];
+    if ((rc = e->alloc(&w.qkv, packed_bytes(e->qkv_rows, H) / 2))) return bail(rc);
+    if ((rc = e->alloc(&w.o, packed_bytes(H, Hq * D) / 2))) return bail(rc);
+    if ((rc = e->alloc(&w.gu, packed_bytes(2 * I, H) / 2))) return bail(rc);
+    if ((rc = e->alloc(&w.down, packed_bytes(H, I) / 2))) return bail(rc);
+    if ((rc = e->alloc(&w.in_norm, H)) || (rc = e->alloc(&w.post_norm, H)) || (rc = e->alloc(&w.q_norm, D)) ||
+        (rc = e->alloc(&w.k_norm, D)))
+      return bail(rc);
+    hipMemset(w.qkv, 0, packed_bytes(e->qkv_rows, H));
+    hipMemset(w.o, 0, packed_bytes(H, Hq * D));
+    wb += 2ull * ((uint64_t)e->qkv_rows * H + (uint64_t)H * Hq * D + 2ull * I * H + (uint64_t)H * I) + 2ull * 2 * H + 2ull * 2 * D;
+  }
+  if ((rc = e->alloc(&e->emb_text, (size_t)c.vocab * H)) || (rc = e->alloc(&e->emb_audio, (size_t)c.n_vq * e->audio_rows * H)) ||
+      (rc = e->alloc(&e->final_norm, H)) || (rc = e->alloc(&e->heads, packed_bytes(e->heads_rows, H) / 2)))
+    return bail(rc);
+  hipMemset(e->heads, 0, packed_bytes(e->heads_rows, H));
+  wb += 2ull * (uint64_t)e->heads_rows * H + 2ull * H;
+  e->step_weight_bytes = wb;
+  if ((rc = alloc_capacity(e))) return bail(rc);
+  if (hipDeviceSynchronize() != hipSuccess) return bail(fail(MTTS_E_HIP, "init sync failed"));
+  *out = e;
+  return 0;
+}
+
+extern "C" int mtts_engine_reserve(mtts_engine* e, int max_batch, int max_ctx, int max_prefill_tokens) {
+  if (!e || max_batch <= 0 || max_batch > 256 || max_ctx <= 0) return fail(MTTS_E_INVALID, "bad capacity");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second.exec);
+  e->graphs.clear();
+  for (void* p : e->cap_allocs) hipFree(p);
+  e->cap_allocs.clear();
+  e->c.max_batch = max_batch;
+  e->c.max_ctx = max_ctx;
+  e->c.max_prefill_tokens = max_prefill_tokens > 0 ? max_prefill_tokens : 8192;
+  e->gen_B = 0;
+  int rc = alloc_capacity(e);
+  if (rc) return rc;
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
+}
+
+extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
+  if (!e || !bytes) return fail(MTTS_E_INVALID, "null argument");
+  *bytes = e->step_weight_bytes;
+  return 0;
+}
+extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
+
+// ---------------------------------------------------------------------------
+// weight loading by reference state_dict name
+static int ensure_staging(mtts_engine* e, size_t bytes) {
+  if (e->staging_bytes >= bytes) return 0;
+  if (e->staging) hipFree(e->staging);
+  e->staging = nullptr;
+  e->staging_bytes = 0;
+  if (hipMalloc(&e->staging, bytes) != hipSuccess) return fail(MTTS_E_OOM, "staging alloc");
+  e->staging_bytes = bytes;
+  return 0;
+}
+
+static bool parse_layer(const char* name, int* layer, std::string* rest) {
+  const char* p = "language_model.layers.";
+  if (std::strncmp(name, p, std::strlen(p)) != 0) return false;
+  const char* q = name + std::strlen(p);
+  char* end = nullptr;
+  long l = std::strtol(q, &end, 10);
+  if (end == q || *end != '.') return false;
+  *layer = (int)l;
+  *rest = std::string(end + 1);
+  return true;
+}
+
+extern "C" int mtts_engine_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev) {
+  if (!e || !name || !src) return fail(MTTS_E_INVALID, "null argument");
+  hipSetDevice(e->device);
+  const mtts_config& c = e->c;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
+  hipStream_t s = e->stream;
+  // resolve target
+  enum Kind { RAW, PACK };
+  Kind kind = RAW;
+  bf16_t* dst = nullptr;
+  size_t expect = 0;
+  int rows = 0, K = 0, row_off = 0, inter = 0, which = 0;
+  int layer = -1;
+  std::string rest;
+  if (!std::strcmp(name, "language_model.embed_tokens.weight")) {
+    dst = e->emb_text; expect = (size_t)c.vocab * H;
+  } else if (!std::strcmp(name, "language_model.norm.weight")) {
+    dst = e->final_norm; expect = H;
+  } else if (!std::strncmp(name, "emb_ext.", 8)) {
+    const int j = std::atoi(name + 8);
+    if (j < 0 || j >= c.n_vq) return fail(MTTS_E_INVALID, std::string("bad name ") + name);
+    dst = e->emb_audio + (size_t)j * e->audio_rows * H; expect = (size_t)e->audio_rows * H;
+  } else if (!std::strncmp(name, "lm_heads.", 9)) {
+    const int j = std::atoi(name + 9);
+    if (j < 0 || j > c.n_vq) return fail(MTTS_E_INVALID, std::string("bad name ") + name);
+    kind = PACK; dst = e->heads; K = H;
+    rows = j == 0 ? c.vocab : e->audio_rows;
+    row_off = j == 0 ? 0 : c.vocab + (j - 1) * e->audio_rows;
+    expect = (size_t)rows * H;
+  } else if (parse_layer(name, &layer, &rest)) {
+    if (layer < 0 || layer >= c.layers) return fail(MTTS_E_INVALID, std::string("bad layer in ") + name);
+    LayerW& w = e->L[layer];
+    if (rest == "self_attn.q_proj.weight") { kind = PACK; dst = w.qkv; rows = Hq * D; K = H; row_off = 0; }
+    else if (rest == "self_attn.k_proj.weight") { kind = PACK; dst = w.qkv; rows = Hkv * D; K = H; row_off = Hq * D; }
+    else if (rest == "self_attn.v_proj.weight") { kind = PACK; dst = w.qkv; rows = Hkv * D; K = H; row_off = (Hq + Hkv) * D; }
+    else if (rest == "self_attn.o_proj.weight") { kind = PACK; dst = w.o; rows = H; K = Hq * D; }
+    else if (rest == "mlp.gate_proj.weight") { kind = PACK; dst = w.gu; rows = I; K = H; inter = 1; which = 0; }
+    else if (rest == "mlp.up_proj.weight") { kind = PACK; dst = w.gu; rows = I; K = H; inter = 1; which = 1; }
+    else if (rest == "mlp.down_proj.weight") { kind = PACK; dst = w.down; rows = H; K = I; }
+    else if (rest == "self_attn.q_norm.weight") { dst = w.q_norm; expect = D; }
+    else if (rest == "self_attn.k_norm.weight") { dst = w.k_norm; expect = D; }
+    else if (rest == "input_layernorm.weight") { dst = w.in_norm; expect = H; }
+    else if (rest == "post_attention_layernorm.weight") { dst = w.post_norm; expect = H; }
+    else return fail(MTTS_E_INVALID, std::string("unknown weight ") + name);
+    if (kind == PACK) expect = (size_t)rows * K;
+  } else {
+    return fail(MTTS_E_INVALID, std::string("unknown weight ") + name);
+  }
+  if (bytes != expect * 2) return fail(MTTS_E_INVALID, std::string("size mismatch for ") + name);
+  if (kind == RAW) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  } else {
+    const bf16_t* from = reinterpret_cast<const bf16_t*>(src);
+    if (!on_dev) {
+      int rc = ensure_staging(e, bytes);
+      if (rc) return rc;
+      HIPCHK(hipMemcpyAsync(e->staging, src, bytes, hipMemcpyHostToDevice, s));
+      from = e->staging;
+    }
+    HIPCHK(pack_weight(from, dst, rows, K, row_off, inter, which, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  return 0;
+}
+
+// same tensor order / init as oracle.moss_delay.weight_specs + scale_for (no text boost)
+extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
+  if (!e) return fail(MTTS_E_INVALID, "null engine");
+  hipSetDevice(e->device);
+  const mtts_config& c = e->c;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
+  struct Spec { std::string name; size_t rows, cols; int kind; };  // 0 lin 1 norm 2 emb 3 head
+  std::vector<Spec> sp;
+  sp.push_back({"language_model.embed_tokens.weight", (size_t)c.vocab, (size_t)H, 2});
+  for (int l = 0; l < c.layers; ++l) {
+    const std::string p = "language_model.layers." + std::to_string(l) + ".";
+    sp.push_back({p + "self_attn.q_proj.weight", (size_t)Hq * D, (size_t)H, 0});
+    sp.push_back({p + "self_attn.k_proj.weight", (size_t)Hkv * D, (size_t)H, 0});
+    sp.push_back({p + "self_attn.v_proj.weight", (size_t)Hkv * D, (size_t)H, 0});
+    sp.push_back({p + "self_attn.o_proj.weight", (size_t)H, (size_t)Hq * D, 0});
+    sp.push_back({p + "self_attn.q_norm.weight", 1, (size_t)D, 1});
+    sp.push_back({p + "self_attn.k_norm.weight", 1, (size_t)D, 1});
+    sp.push_back({p + "mlp.gate_proj.weight", (size_t)I, (size_t)H, 0});
+    sp.push_back({p + "mlp.up_proj.weight", (size_t)I, (size_t)H, 0});
+    sp.push_back({p + "mlp.down_proj.weight", (size_t)H, (size_t)I, 0});
+    sp.push_back({p + "input_layernorm.weight", 1, (size_t)H, 1});
+    sp.push_back({p + "post_attention_layernorm.weight", 1, (size_t)H, 1});
+  }
+  sp.push_back({"language_model.norm.weight", 1, (size_t)H, 1});
+  for (int j = 0; j < c.n_vq; ++j) sp.push_back({"emb_ext." + std::to_string(j) + ".weight", (size_t)e->audio_rows, (size_t)H, 2});
+  sp.push_back({"lm_heads.0.weight", (size_t)c.vocab, (size_t)H, 3});
+  for (int j = 0; j < c.n_vq; ++j) sp.push_back({"lm_heads." + std::to_string(j + 1) + ".weight", (size_t)e->audio_rows, (size_t)H, 3});
+  size_t mx = 0;
+  for (auto& s : sp) mx = std::max(mx, s.rows * s.cols);
+  int rc = ensure_staging(e, mx * 2);
+  if (rc) return rc;
+  for (size_t tid = 0; tid < sp.size(); ++tid) {
+    const Spec& s = sp[tid];
+    float scale = 1.f, offset = 0.f;
+    if (s.kind == 0 || s.kind == 3) scale = (float)std::sqrt(3.0 / (double)s.cols);
+    else if (s.kind == 1) { scale = 0.25f; offset = 1.0f; }
+    HIPCHK(fill_uniform_bf16(e->staging, s.rows * s.cols, seed, tid, scale, offset, e->stream));
+    rc = mtts_engine_load_weight(e, s.name.c_str(), e->staging, s.rows * s.cols * 2, 1);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// forward over rows [b0, b0+B) with S tokens each; pos_base device pointer
+static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
+                        int n_split, bf16_t* logits_out, hipStream_t s) {
+  const mtts_config& c = e->c;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter, C = c.n_vq + 1;
+  const int M = B * S;
+  HIPCHK(embed(ids, C, e->emb_text, e->emb_audio, e->audio_rows, H, e->h, M, s));
+  const float eps = c.rms_eps;
+  for (int l = 0; l < c.layers; ++l) {
+    const LayerW& w = e->L[l];
+    HIPCHK(rmsnorm(e->h, 0, H, w.in_norm, e->xn, M, H, eps, s));
+    HIPCHK(gemv(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, nullptr, 0, M, e->qkv_rows, H, EPI_STORE, 0, 1, 0, s));
+    QKRopeArgs qa;
+    qa.qkv = e->qkvb; qa.q_out = e->qb;
+    qa.kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
+    qa.vc = e->vc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
+    qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = e->cos_t; qa.sin_t = e->sin_t;
+    qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = c.max_ctx; qa.eps = eps; qa.M = M;
+    HIPCHK(qk_norm_rope(qa, s));
+    AttnArgs aa;
+    aa.q = e->qb; aa.kc = qa.kc; aa.vc = qa.vc; aa.mask = e->mask + (size_t)b0 * c.max_ctx; aa.pos_base = pos_base;
+    aa.part_o = e->part; aa.part_ml = e->part + (size_t)M * n_split * Hq * D; aa.out = e->attnb;
+    aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = c.max_ctx; aa.CH = CH; aa.n_split = n_split; aa.M = M;
+    aa.scale = 1.0f / std::sqrt((float)D);
+    HIPCHK(attention(aa, s));
+    HIPCHK(gemv(w.o, e->attnb, Hq * D, e->h, H, e->h, H, M, H, Hq * D, EPI_RESADD, 0, 1, 0, s));
+    HIPCHK(rmsnorm(e->h, 0, H, w.post_norm, e->xn, M, H, eps, s));
+    HIPCHK(gemv(w.gu, e->xn, H, e->act, I, nullptr, 0, M, I, H, EPI_SWIGLU, 0, 1, 0, s));
+    HIPCHK(gemv(w.down, e->act, I, e->h, H, e->h, H, M, H, I, EPI_RESADD, 0, 1, 0, s));
+  }
+  // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
+  HIPCHK(rmsnorm(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->final_norm, e->xn, B, H, eps, s));
+  HIPCHK(gemv(e->heads, e->xn, H, logits_out, e->heads_ld, nullptr, 0, B, e->heads_rows, H, EPI_LOGITS, c.vocab,
+              e->audio_rows, e->audio_rows - 1, s));
+  return 0;
+}
+
+// prefill / teacher-forced forward of S tokens at position `past` (host int), rows chunked
+static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s) {
+  const mtts_config& c = e->c;
+  if (S > e->Mmax) return fail(MTTS_E_UNSUPPORTED, "prompt longer than max_prefill_tokens");
+  HIPCHK(hipMemcpyAsync(e->d_pos, &past, sizeof(int), hipMemcpyHostToDevice, s));
+  const int rows_per = std::max(1, e->Mmax / S);
+  const int CH = S == 1 ? CH_DECODE : CH_PREFILL;
+  const int n_split = (past + S + CH - 1) / CH;
+  for (int b0 = 0; b0 < B; b0 += rows_per) {
+    const int nb = std::min(rows_per, B - b0);
+    int rc = forward_rows(e, ids + (size_t)b0 * S * (c.n_vq + 1), b0, nb, S, e->d_pos, CH, n_split,
+                          logits_out + (size_t)b0 * e->heads_ld, s);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+static hipStream_t enter(mtts_engine* e, void* user) {
+  hipSetDevice(e->device);
+  if (user) {
+    hipEventRecord(e->ev_in, (hipStream_t)user);
+    hipStreamWaitEvent(e->stream, e->ev_in, 0);
+  }
+  return e->stream;
+}
+static void leave(mtts_engine* e, void* user) {
+  if (user) {
+    hipEventRecord(e->ev_out, e->stream);
+    hipStreamWaitEvent((hipStream_t)user, e->ev_out, 0);
+  }
+}
+
+extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
+                            uint16_t* logits, void* stream) {
+  if (!e || !ids || !mask || !logits) return fail(MTTS_E_INVALID, "null argument");
+  const mtts_config& c = e->c;
+  if (B <= 0 || B > c.max_batch || S <= 0 || past < 0 || past + S > c.max_ctx) return fail(MTTS_E_INVALID, "bad B/S/past");
+  hipStream_t s = enter(e, stream);
+  HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
+  int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
+  leave(e, stream);
+  return rc;
+}
+
+// ---------------------------------------------------------------------------
+static int decode_step_launch(mtts_engine* e, hipStream_t s) {
+  const int B = e->gen_B;
+  const int n_split = (e->c.max_ctx + CH_DECODE - 1) / CH_DECODE;
+  int rc = forward_rows(e, e->cur_ids, 0, B, 1, &e->st->fwd_pos, CH_DECODE, n_split, e->logits, s);
+  if (rc) return rc;
+  HIPCHK(sample_step(e->bufs(), B, e->c.n_vq, TEXT_PARTS, s));
+  return 0;
+}
+
+extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T, int max_new,
+                                   const mtts_sampling* sp, const int32_t* forced, void* stream) {
+  if (!e || !ids || !sp) return fail(MTTS_E_INVALID, "null argument");
+  const mtts_config& c = e->c;
+  if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
+    return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
+  hipStream_t s = enter(e, stream);
+  GenDev& g = e->hst;
+  std::memset(&g, 0, sizeof(g));
+  g.T0 = T; g.step = 0; g.fwd_pos = 0; g.done_step = -1;
+  g.B = B; g.n_vq = c.n_vq; g.C = c.n_vq + 1; g.Ltot = c.max_ctx; g.Cmax = c.max_ctx;
+  g.vocab = c.vocab; g.audio_rows = e->audio_rows; g.heads_ld = e->heads_ld;
+  g.P = TEXT_PARTS; g.part_len = (c.vocab + TEXT_PARTS - 1) / TEXT_PARTS;
+  g.text_sample = sp->text_temperature > 0.f;
+  g.audio_sample = sp->audio_temperature > 0.f;
+  g.text_temp = g.text_sample ? sp->text_temperature : 1.f;
+  g.audio_temp = g.audio_sample ? sp->audio_temperature : 1.f;
+  g.text_top_p = sp->text_top_p; g.audio_top_p = sp->audio_top_p;
+  g.text_top_k = sp->text_top_k; g.audio_top_k = sp->audio_top_k;
+  g.rep_penalty = sp->audio_repetition_penalty;
+  g.seed = sp->seed;
+  g.ids.pad = c.pad_token_id; g.ids.im_start = c.im_start_token_id; g.ids.im_end = c.im_end_token_id;
+  g.ids.audio_start = c.audio_start_token_id; g.ids.audio_end = c.audio_end_token_id;
+  g.ids.user_slot = c.audio_user_slot_token_id; g.ids.gen_slot = c.audio_assistant_gen_slot_token_id;
+  g.ids.delay_slot = c.audio_assistant_delay_slot_token_id; g.ids.audio_pad = c.audio_pad_code;
+  if ((g.text_sample && (sp->text_top_k > MAXK || sp->text_top_k <= 0)) ||
+      (g.audio_sample && (sp->audio_top_k > MAXK || sp->audio_top_k <= 0)))
+    return fail(MTTS_E_UNSUPPORTED, "top_k must be in [1, 64] when sampling");
+  e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = forced;
+  HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetAsync(e->seen, 0, 2 * e->audio_rows, s));
+  HIPCHK(gen_init(e->bufs(), ids, mask, s));
+  int rc = forward_chunked(e, ids, B, T, 0, e->logits, s);
+  if (rc) return rc;
+  HIPCHK(sample_step(e->bufs(), B, c.n_vq, TEXT_PARTS, s));
+  e->steps_issued = 1;
+  leave(e, stream);
+  return 0;
+}
+
+extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
+  if (!e) return fail(MTTS_E_INVALID, "null engine");
+  if (e->gen_B <= 0) return fail(MTTS_E_INVALID, "generate_begin not called");
+  hipStream_t s = enter(e, stream);
+  // the graph bakes the kernel arguments (buffers, B, the forced-schedule pointer);
+  // every step-dependent value is read from device state, so one graph serves all steps
+  auto it = e->graphs.find(e->gen_B);
+  hipGraphExec_t exec = nullptr;
+  if (it != e->graphs.end() && it->second.forced == e->forced) {
+    exec = it->second.exec;
+  } else {
+    if (it != e->graphs.end()) {
+      hipGraphExecDestroy(it->second.exec);
+      e->graphs.erase(it);
+    }
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = decode_step_launch(e, s);
+    hipError_t ce = hipStreamEndCapture(s, &graph);
+    if (rc) return rc;
+    if (ce != hipSuccess) return fail(MTTS_E_HIP, std::string("capture: ") + hipGetErrorString(ce));
+    HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    hipGraphDestroy(graph);
+    e->graphs[e->gen_B] = mtts_engine::Graph{exec, e->forced};
+  }
+  for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
+    HIPCHK(hipGraphLaunch(exec, s));
+    ++e->steps_issued;
+  }
+  leave(e, stream);
+  return 0;
+}
+
+extern "C" int mtts_generate_poll(mtts_engine* e, int* steps, int* done_step, void* stream) {
+  if (!e) return fail(MTTS_E_INVALID, "null engine");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  GenDev g;
+  HIPCHK(hipMemcpy(&g, e->st, sizeof(g), hipMemcpyDeviceToHost));
+  if (steps) *steps = g.step;
+  if (done_step) *done_step = g.done_step;
+  (void)stream;
+  return 0;
+}
+
+extern "C" int mtts_generate(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T, int max_new,
+                             const mtts_sampling* sp, const int32_t* forced, int chunk, int* n_rows, void* stream) {
+  int rc = mtts_generate_begin(e, ids, mask, B, T, max_new, sp, forced, stream);
+  if (rc) return rc;
+  if (chunk <= 0) chunk = 16;
+  int steps = 1, done = -1;
+  while (true) {
+    rc = mtts_generate_poll(e, &steps, &done, stream);
+    if (rc) return rc;
+    if (done >= 0 || steps >= max_new) break;
+    rc = mtts_generate_decode(e, std::min(chunk, max_new - steps), stream);
+    if (rc) return rc;
+  }
+  if (n_rows) *n_rows = done >= 0 ? done + 1 : steps;
+  return 0;
+}
+
+extern "C" int mtts_generate_fetch(mtts_engine* e, int64_t* out, int n_rows, void* stream) {
+  if (!e || !out) return fail(MTTS_E_INVALID, "null argument");
+  const int C = e->c.n_vq + 1;
+  if (n_rows < 0 || e->gen_T + n_rows > e->c.max_ctx) return fail(MTTS_E_INVALID, "bad n_rows");
+  hipStream_t s = enter(e, stream);
+  const size_t w = (size_t)(e->gen_T + n_rows) * C * sizeof(int64_t);
+  HIPCHK(hipMemcpy2DAsync(out, w, e->gen_ids, (size_t)e->c.max_ctx * C * sizeof(int64_t), w, e->gen_B,
+                          hipMemcpyDeviceToDevice, s));
+  leave(e, stream);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// kernel-level entry points
+extern "C" size_t mtts_k_packed_bytes(int rows, int K) { return packed_bytes(rows, K); }
+extern "C" int mtts_k_pack(const uint16_t* src, uint16_t* dst, int rows, int K, int row_offset, int interleave, int which,
+                           void* stream) {
+  HIPCHK(pack_weight(src, dst, rows, K, row_offset, interleave, which, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_gemv(const uint16_t* w, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                           int ldres, int B, int N, int K, int epi, int ps, int pp, int po, void* stream) {
+  if (K % 32) return fail(MTTS_E_INVALID, "K must be a multiple of 32");
+  HIPCHK(gemv(w, x, ldx, y, ldy, res, ldres, B, N, K, epi, ps, pp, po, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_rmsnorm(const uint16_t* x, size_t xo, size_t xs, const uint16_t* w, uint16_t* y, int M, int H,
+                              float eps, void* stream) {
+  HIPCHK(rmsnorm(x, xo, xs, w, y, M, H, eps, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_embed(const int64_t* ids, int C, const uint16_t* et, const uint16_t* ea, int ar, int H, uint16_t* h,
+                            int M, void* stream) {
+  HIPCHK(embed(ids, C, et, ea, ar, H, h, M, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_qk_norm_rope(const uint16_t* qkv, uint16_t* q_out, uint16_t* kc, uint16_t* vc, const uint16_t* qn,
+                                   const uint16_t* kn, const uint16_t* cs, const uint16_t* sn, const int32_t* pos, int M,
+                                   int S, int Hq, int Hkv, int D, int Cmax, float eps, void* stream) {
+  QKRopeArgs a;
+  a.qkv = qkv; a.q_out = q_out; a.kc = kc; a.vc = vc; a.qn_w = qn; a.kn_w = kn; a.cos_t = cs; a.sin_t = sn;
+  a.pos_base = pos; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.eps = eps; a.M = M;
+  HIPCHK(qk_norm_rope(a, (hipStream_t)stream));
+  return 0;
+}
+extern "C" size_t mtts_k_attention_ws_bytes(int M, int Hq, int D, int n_split) {
+  return (size_t)M * n_split * Hq * (D + 2) * sizeof(float);
+}
+extern "C" int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
+                                const int32_t* pos, uint16_t* out, void* ws, int M, int S, int Hq, int Hkv, int D,
+                                int Cmax, int CH, int n_split, void* stream) {
+  AttnArgs a;
+  a.q = q; a.kc = kc; a.vc = vc; a.mask = mask; a.pos_base = pos;
+  a.part_o = reinterpret_cast<float*>(ws);
+  a.part_ml = a.part_o + (size_t)M * n_split * Hq * D;
+  a.out = out; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.CH = CH; a.n_split = n_split; a.M = M;
+  a.scale = 1.0f / std::sqrt((float)D);
+  HIPCHK(attention(a, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_fill_uniform(uint16_t* dst, size_t n, uint64_t seed, uint64_t tid, float scale, float offset,
+                                   void* stream) {
+  HIPCHK(fill_uniform_bf16(dst, n, seed, tid, scale, offset, (hipStream_t)stream));
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// roofline probe: time one weight-streaming GEMV of the loaded model on the engine
+// stream with HIP events (which: 0 q|k|v, 1 o_proj, 2 gate|up (SwiGLU), 3 down, 4 heads)
+extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B, int iters, float* avg_ms,
+                                     uint64_t* alg_bytes) {
+  if (!e || !avg_ms || !alg_bytes || iters <= 0) return fail(MTTS_E_INVALID, "null argument");
+  const mtts_config& c = e->c;
+  if (layer < 0 || layer >= c.layers || B <= 0 || B > c.max_batch) return fail(MTTS_E_INVALID, "bad layer/B");
+  hipSetDevice(e->device);
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, I = c.inter;
+  const LayerW& w = e->L[layer];
+  hipStream_t s = e->stream;
+  const bf16_t* W = nullptr;
+  const bf16_t* x = e->xn;
+  bf16_t* y = e->qkvb;
+  const bf16_t* res = nullptr;
+  int N = 0, K = H, epi = EPI_STORE, ps = 0, pp = 1, po = 0, ldx = H, ldy = 0, ldres = 0;
+  uint64_t wrows = 0;
+  switch (which) {
+    case 0: W = w.qkv; N = e->qkv_rows; ldy = N; wrows = N; break;
+    case 1: W = w.o; N = H; K = Hq * D; x = e->attnb; ldx = K; y = e->h; res = e->h; ldy = H; ldres = H; epi = EPI_RESADD; wrows = H; break;
+    case 2: W = w.gu; N = I; y = e->act; ldy = I; epi = EPI_SWIGLU; wrows = 2ull * I; break;
+    case 3: W = w.down; N = H; K = I; x = e->act; ldx = I; y = e->h; res = e->h; ldy = H; ldres = H; epi = EPI_RESADD; wrows = H; break;
+    case 4: W = e->heads; N = e->heads_rows; y = e->logits; ldy = e->heads_ld; epi = EPI_LOGITS; ps = c.vocab;
+      pp = e->audio_rows; po = e->audio_rows - 1; wrows = N; break;
+    default: return fail(MTTS_E_INVALID, "bad which");
+  }
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
+  HIPCHK(gemv(W, x, ldx, y, ldy, res, ldres, B, N, K, epi, ps, pp, po, s));
+  HIPCHK(hipEventRecord(a, s));
+  for (int i = 0; i < iters; ++i) HIPCHK(gemv(W, x, ldx, y, ldy, res, ldres, B, N, K, epi, ps, pp, po, s));
+  HIPCHK(hipEventRecord(b, s));
+  HIPCHK(hipEventSynchronize(b));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  *avg_ms = ms / iters;
+  // algorithmic bytes: weights once + activations in + outputs (+ residual read)
+  *alg_bytes = 2ull * wrows * K + 2ull * B * K + 2ull * B * N * (res ? 2 : 1);
+  return 0;
+}

@@ -1,0 +1,112 @@
+// Kernel argument structs and launch entry points shared by the HIP kernels and the engine.
+#pragma once
+#include "common.h"
+
+namespace mtts {
+
+constexpr int64_t I64MAX = 0x7fffffffffffffffLL;
+constexpr int MAXK = 64;  // largest top-k handled on device
+
+enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
+
+struct GemvArgs {
+  const bf16_t* w;     // packed tiles
+  const bf16_t* x;     // [B, ldx] activations (bf16)
+  bf16_t* y;           // [B, ldy] output
+  const bf16_t* res;   // residual [B, ldres] (EPI_RESADD; may alias y)
+  int ldx, ldy, ldres;
+  int B;               // active rows of x / y
+  int N;               // valid output columns
+  int K;               // reduction length (multiple of 32)
+  int KT;              // K / 32
+  // EPI_LOGITS: columns n >= pad_start with (n - pad_start) % pad_period == pad_off -> -inf
+  int pad_start, pad_period, pad_off;
+};
+
+struct QKRopeArgs {
+  const bf16_t* qkv;
+  bf16_t* q_out;
+  bf16_t* kc;
+  bf16_t* vc;
+  const bf16_t* qn_w;
+  const bf16_t* kn_w;
+  const bf16_t* cos_t;  // [max_pos, D]
+  const bf16_t* sin_t;
+  const int* pos_base;  // device: position of token s=0 (same for all rows)
+  int S;                // tokens per row
+  int Hq, Hkv, D;
+  int Cmax;
+  float eps;
+  int M;
+};
+
+struct AttnArgs {
+  const bf16_t* q;       // [M, Hq*D]
+  const bf16_t* kc;      // [Bmax][Hkv][Cmax][D]
+  const bf16_t* vc;
+  const uint8_t* mask;   // [Bmax][Cmax]
+  const int* pos_base;   // device: absolute position of token s=0
+  float* part_o;         // [M][n_split][Hq][D]
+  float* part_ml;        // [M][n_split][Hq][2]
+  bf16_t* out;           // [M, Hq*D]
+  int S, Hq, Hkv, D, Cmax, CH, n_split, M;
+  float scale;
+};
+
+struct GenDev {
+  // scalars
+  int T0;          // prompt length
+  int step;        // time_step of the logits being sampled
+  int fwd_pos;     // absolute position of the token fed to the next forward
+  int done_step;   // first step at which every row had stopped, -1 if none yet
+  int B, n_vq, C, Ltot, Cmax;
+  int vocab, audio_rows;  // text vocab, 1025
+  int heads_ld;           // row stride of the logits buffer
+  int P, part_len;        // text partitions
+  // sampling
+  float text_temp, text_top_p, audio_temp, audio_top_p, rep_penalty;
+  int text_top_k, audio_top_k, text_sample, audio_sample;
+  unsigned long long seed;
+  MttsIds ids;
+};
+
+struct GenBufs {
+  GenDev* st;
+  const bf16_t* logits;  // [B, heads_ld] bf16: text | audio_0 (1025) | audio_1 ...
+  int* is_stopping;      // [B]
+  int* is_audio;         // [B]
+  int64_t* audio_len;    // [B]
+  int64_t* delayed;      // [B]
+  int64_t* cur_ids;      // [B, C]
+  int64_t* gen_ids;      // [B, Ltot, C]
+  uint8_t* mask;         // [B, Cmax]
+  uint8_t* seen;         // [2, audio_rows] union of the audio history (ch 1 | ch >= 2)
+  float* part_val;       // [B, P, K]
+  int* part_idx;
+  int* text_cand;        // [B]
+  int* audio_cand;       // [B, n_vq]
+  const int* forced;     // [max_new] text override for sampled rows (-1 none) or nullptr
+};
+
+// gemv.hip
+hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int ldy, const bf16_t* res, int ldres,
+                int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, hipStream_t s);
+hipError_t pack_weight(const bf16_t* src, bf16_t* dst, int rows, int K, int row_offset, int interleave, int which,
+                       hipStream_t s);
+// norm_rope.hip
+hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
+                 bf16_t* h, int M, hipStream_t s);
+hipError_t rmsnorm(const bf16_t* x, size_t x_off, size_t x_stride, const bf16_t* w, bf16_t* y, int M, int H, float eps,
+                   hipStream_t s);
+hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s);
+// attention.hip
+size_t attn_smem_bytes(int G, int D, int CH);
+hipError_t attention(const AttnArgs& a, hipStream_t s);
+// sample.hip
+hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
+hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);
+// init.hip
+hipError_t fill_uniform_bf16(bf16_t* dst, size_t n, unsigned long long seed, unsigned long long tensor_id, float scale,
+                             float offset, hipStream_t s);
+
+}  // namespace mtts

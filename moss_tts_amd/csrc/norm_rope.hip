@@ -1,0 +1,163 @@
+// Embedding sum, RMSNorm, q/k-norm + RoPE + KV-cache append.
+#include "kernels.h"
+
+namespace mtts {
+
+// ---------------------------------------------------------------------------
+// h[m, :] = E_text[ids[m,0]] + E_0[ids[m,1]] + ... + E_{n-1}[ids[m,n]], each add rounded to
+// bf16 left to right (moss_tts_delay/modeling_moss_tts.py:196-213).  One block per token.
+__global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int C, const bf16_t* __restrict__ emb_text,
+                                                    const bf16_t* __restrict__ emb_audio, int audio_rows, int H,
+                                                    bf16_t* __restrict__ h) {
+  const int m = blockIdx.x;
+  const int64_t* id = ids + (size_t)m * C;
+  const int nchunk = H >> 3;
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float e[8];
+    unpack8(*reinterpret_cast<const uint4*>(emb_text + (size_t)id[0] * H + c * 8), e);
+    for (int j = 1; j < C; ++j) {
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>(emb_audio + ((size_t)(j - 1) * audio_rows + id[j]) * H + c * 8), a);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) e[i] = rbf(e[i] + a[i]);
+    }
+    uint4 o;
+    o.x = pack2(e[0], e[1]); o.y = pack2(e[2], e[3]); o.z = pack2(e[4], e[5]); o.w = pack2(e[6], e[7]);
+    *reinterpret_cast<uint4*>(h + (size_t)m * H + c * 8) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Qwen3RMSNorm (TF/models/qwen3/modeling_qwen3.py:59-64): fp32 statistics,
+// y = bf16(w * bf16(x * rsqrt(mean(x^2) + eps))).  One block per row.
+// Row m of the input is x + x_off + m * x_stride (lets the heads pick the last token).
+__global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__ x, size_t x_off, size_t x_stride,
+                                                      const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int H,
+                                                      float eps) {
+  const int m = blockIdx.x;
+  const bf16_t* xr = x + x_off + (size_t)m * x_stride;
+  const int nchunk = H >> 3;
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ss += v[i] * v[i];
+  }
+  __shared__ float part[4];
+  ss = wave_sum(ss);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = ((part[0] + part[1]) + part[2]) + part[3];
+  const float r = 1.0f / sqrtf(tot / (float)H + eps);
+  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
+    float v[8], g[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v);
+    unpack8(*reinterpret_cast<const uint4*>(w + c * 8), g);
+    uint4 o;
+    float q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) q[i] = rbf(g[i] * rbf(v[i] * r));
+    o.x = pack2(q[0], q[1]); o.y = pack2(q[2], q[3]); o.z = pack2(q[4], q[5]); o.w = pack2(q[6], q[7]);
+    *reinterpret_cast<uint4*>(y + (size_t)m * H + c * 8) = o;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Per-head q_norm / k_norm (TF/.../modeling_qwen3.py:252-254), RoPE in bf16
+// (:148-170, cos/sin from a bf16 table computed in fp32, :126-137) and the KV
+// cache append (DynamicLayer.update, TF/cache_utils.py:127-145) as an in-place
+// write at the token's absolute position.
+//
+// qkv   [M, (Hq + 2 Hkv) * D] (bf16, output of the fused q|k|v GEMV)
+// q_out [M, Hq * D]
+// cache k/v: [Bmax][Hkv][Cmax][D] per layer; token m = b*S + s sits at position pos0[b?] + s
+// One wave per (token, head); D <= 128, each lane holds dims 2l, 2l+1.
+
+__global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const int gw = blockIdx.x * 4 + (threadIdx.x >> 6);  // global wave = (token, head)
+  const int heads = a.Hq + 2 * a.Hkv;
+  if (gw >= a.M * heads) return;
+  const int m = gw / heads;
+  const int hd = gw % heads;
+  const int b = m / a.S, s = m % a.S;
+  const int pos = *a.pos_base + s;
+  const int D = a.D;
+  const bool act = 2 * lane < D;
+  const bf16_t* src = a.qkv + (size_t)m * heads * D + (size_t)hd * D;
+  float x0 = 0.f, x1 = 0.f;
+  if (act) {
+    const uint32_t pr = *reinterpret_cast<const uint32_t*>(src + 2 * lane);
+    x0 = __uint_as_float(pr << 16);
+    x1 = __uint_as_float(pr & 0xffff0000u);
+  }
+  if (hd >= a.Hq + a.Hkv) {  // V head: copy into the cache
+    const int kvh = hd - a.Hq - a.Hkv;
+    if (act) {
+      bf16_t* dst = a.vc + (((size_t)b * a.Hkv + kvh) * a.Cmax + pos) * D;
+      *reinterpret_cast<uint32_t*>(dst + 2 * lane) = pack2(x0, x1);
+    }
+    return;
+  }
+  const bool isq = hd < a.Hq;
+  const bf16_t* nw = isq ? a.qn_w : a.kn_w;
+  // RMSNorm over D in fp32
+  float ss = wave_sum(x0 * x0 + x1 * x1);
+  const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
+  float w0 = 0.f, w1 = 0.f;
+  if (act) {
+    const uint32_t pw = *reinterpret_cast<const uint32_t*>(nw + 2 * lane);
+    w0 = __uint_as_float(pw << 16);
+    w1 = __uint_as_float(pw & 0xffff0000u);
+  }
+  const float n0 = rbf(w0 * rbf(x0 * r));
+  const float n1 = rbf(w1 * rbf(x1 * r));
+  // rotate_half: dims d < D/2 take -x[d + D/2], dims >= D/2 take x[d - D/2]; partner lane = lane +- D/4
+  const int q4 = D >> 2;
+  const int partner = (2 * lane < D / 2) ? lane + q4 : lane - q4;
+  const float p0 = __shfl(n0, partner, 64);
+  const float p1 = __shfl(n1, partner, 64);
+  const float sg = (2 * lane < D / 2) ? -1.f : 1.f;
+  float c0 = 0.f, c1 = 0.f, s0 = 0.f, s1 = 0.f;
+  if (act) {
+    const uint32_t pc = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
+    const uint32_t ps = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
+    c0 = __uint_as_float(pc << 16); c1 = __uint_as_float(pc & 0xffff0000u);
+    s0 = __uint_as_float(ps << 16); s1 = __uint_as_float(ps & 0xffff0000u);
+  }
+  const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
+  const float o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+  if (!act) return;
+  if (isq) {
+    bf16_t* dst = a.q_out + (size_t)m * a.Hq * D + (size_t)hd * D;
+    *reinterpret_cast<uint32_t*>(dst + 2 * lane) = pack2(o0, o1);
+  } else {
+    const int kvh = hd - a.Hq;
+    bf16_t* dst = a.kc + (((size_t)b * a.Hkv + kvh) * a.Cmax + pos) * D;
+    *reinterpret_cast<uint32_t*>(dst + 2 * lane) = pack2(o0, o1);
+  }
+}
+
+hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
+                 bf16_t* h, int M, hipStream_t s) {
+  if (H % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, s, ids, C, emb_text, emb_audio, audio_rows, H, h);
+  return hipGetLastError();
+}
+
+hipError_t rmsnorm(const bf16_t* x, size_t x_off, size_t x_stride, const bf16_t* w, bf16_t* y, int M, int H, float eps,
+                   hipStream_t s) {
+  if (H % 8) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(rmsnorm_kernel, dim3(M), dim3(256), 0, s, x, x_off, x_stride, w, y, H, eps);
+  return hipGetLastError();
+}
+
+hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s) {
+  if (a.D > 128 || a.D % 4) return hipErrorInvalidValue;
+  const int waves = a.M * (a.Hq + 2 * a.Hkv);
+  hipLaunchKernelGGL(qk_norm_rope_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace mtts

@@ -1,0 +1,169 @@
+"""Python host side of the engine: owns an `mtts_engine` (libmtts.so) and moves
+torch device tensors across the C ABI as raw pointers.
+
+PyTorch is plumbing here (device memory, streams); every arithmetic op of the
+decode path runs in the HIP kernels of `csrc/`.
+"""
+import ctypes
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import torch
+
+from . import _native as N
+
+
+@dataclass
+class EngineConfig:
+    """Model shape (MossTTSDelayConfig + nested Qwen3Config) and engine capacity."""
+    hidden: int = 4096
+    layers: int = 36
+    n_heads: int = 32
+    n_kv: int = 8
+    head_dim: int = 128
+    inter: int = 12288
+    vocab: int = 151936
+    n_vq: int = 32
+    audio_vocab: int = 1024
+    rope_theta: float = 1_000_000.0
+    rms_eps: float = 1e-6
+    pad_token_id: int = 151643
+    im_start_token_id: int = 151644
+    im_end_token_id: int = 151645
+    audio_start_token_id: int = 151652
+    audio_end_token_id: int = 151653
+    audio_user_slot_token_id: int = 151654
+    audio_assistant_gen_slot_token_id: int = 151656
+    audio_assistant_delay_slot_token_id: int = 151662
+    audio_pad_code: int = 1024
+    max_batch: int = 32
+    max_ctx: int = 2048
+    max_prefill_tokens: int = 8192
+
+    def to_c(self):
+        c = N.MttsConfig()
+        for name, _ in N.MttsConfig._fields_:
+            setattr(c, name, getattr(self, name))
+        return c
+
+    @classmethod
+    def from_hf(cls, config, **cap):
+        """From a MossTTSDelayConfig-like object (reference `configuration_moss_tts.py:62-103`)."""
+        lc = config.language_config
+        rope = getattr(lc, "rope_parameters", None) or {}
+        theta = rope.get("rope_theta", getattr(lc, "rope_theta", 10000.0))
+        kw = dict(hidden=lc.hidden_size, layers=lc.num_hidden_layers, n_heads=lc.num_attention_heads,
+                  n_kv=lc.num_key_value_heads,
+                  head_dim=getattr(lc, "head_dim", None) or lc.hidden_size // lc.num_attention_heads,
+                  inter=lc.intermediate_size, vocab=lc.vocab_size, n_vq=config.n_vq,
+                  audio_vocab=config.audio_vocab_size, rope_theta=float(theta), rms_eps=float(lc.rms_norm_eps),
+                  pad_token_id=config.pad_token_id, im_start_token_id=config.im_start_token_id,
+                  im_end_token_id=config.im_end_token_id, audio_start_token_id=config.audio_start_token_id,
+                  audio_end_token_id=config.audio_end_token_id,
+                  audio_user_slot_token_id=config.audio_user_slot_token_id,
+                  audio_assistant_gen_slot_token_id=config.audio_assistant_gen_slot_token_id,
+                  audio_assistant_delay_slot_token_id=config.audio_assistant_delay_slot_token_id,
+                  audio_pad_code=config.audio_pad_code)
+        kw.update(cap)
+        return cls(**kw)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Engine:
+    """One engine = one GPU.  Not re-entrant (the reference's model object is not either)."""
+
+    def __init__(self, cfg: EngineConfig, device: int = 0):
+        if not torch.cuda.is_available():
+            raise RuntimeError("moss_tts_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
+        self.cfg = cfg
+        self.device = torch.device("cuda", device)
+        h = ctypes.c_void_p()
+        N.check(N.load().mtts_engine_create(ctypes.byref(cfg.to_c()), device, ctypes.byref(h)), "mtts_engine_create")
+        self._h = h
+        self.heads_ld = N.load().mtts_heads_ld(h)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            N.load().mtts_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- weights ---------------------------------------------------------------
+    def load_weight(self, name: str, tensor: torch.Tensor):
+        t = tensor.detach().to(torch.bfloat16).contiguous()
+        on_dev = 1 if t.is_cuda else 0
+        if t.is_cuda and t.device != self.device:
+            t = t.to(self.device)
+        N.check(N.load().mtts_engine_load_weight(self._h, name.encode(), _ptr(t), t.numel() * 2, on_dev), name)
+
+    def load_state_dict(self, sd: Dict[str, torch.Tensor]):
+        for k, v in sd.items():
+            if "rotary_emb" in k:
+                continue
+            self.load_weight(k, v)
+
+    def init_random(self, seed: int = 0):
+        N.check(N.load().mtts_engine_init_random(self._h, seed), "init_random")
+
+    def weight_bytes(self):
+        v = ctypes.c_uint64()
+        N.check(N.load().mtts_engine_weight_bytes(self._h, ctypes.byref(v)), "weight_bytes")
+        return int(v.value)
+
+    # ---- forward / generate ----------------------------------------------------
+    def forward(self, ids: torch.Tensor, mask: torch.Tensor, past: int) -> torch.Tensor:
+        """Teacher-forced forward: returns bf16 logits [B, heads_ld] of the last position."""
+        B, S, _ = ids.shape
+        ids = ids.to(self.device, torch.int64).contiguous()
+        mask = mask.to(self.device, torch.uint8).contiguous()
+        out = torch.empty(B, self.heads_ld, dtype=torch.bfloat16, device=self.device)
+        N.check(N.load().mtts_forward(self._h, _ptr(ids), _ptr(mask), B, S, past, _ptr(out),
+                                      _stream_ptr(self.device)), "forward")
+        return out
+
+    def split_logits(self, logits: torch.Tensor):
+        V, A = self.cfg.vocab, self.cfg.audio_vocab + 1
+        return [logits[:, :V]] + [logits[:, V + j * A: V + (j + 1) * A] for j in range(self.cfg.n_vq)]
+
+    def generate_ids(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor], max_new_tokens: int,
+                     sampling: N.MttsSampling, forced_text: Optional[torch.Tensor] = None, chunk: int = 16):
+        """Runs the whole device loop; returns generation_ids [B, T + n, 1+n_vq] (prompt included)."""
+        B, T, C = input_ids.shape
+        ids = input_ids.to(self.device, torch.int64).contiguous()
+        mask = None if attention_mask is None else attention_mask.to(self.device, torch.uint8).contiguous()
+        forced = None
+        if forced_text is not None:
+            forced = forced_text.to(self.device, torch.int32).contiguous()
+            assert forced.numel() >= max_new_tokens
+        n = ctypes.c_int()
+        N.check(N.load().mtts_generate(self._h, _ptr(ids), _ptr(mask), B, T, max_new_tokens, ctypes.byref(sampling),
+                                       _ptr(forced), chunk, ctypes.byref(n), _stream_ptr(self.device)), "generate")
+        out = torch.empty(B, T + n.value, C, dtype=torch.int64, device=self.device)
+        N.check(N.load().mtts_generate_fetch(self._h, _ptr(out), n.value, _stream_ptr(self.device)), "fetch")
+        return out
+
+
+def sampling_params(text_temperature=1.5, text_top_p=1.0, text_top_k=50, audio_temperature=1.7, audio_top_p=0.8,
+                    audio_top_k=25, audio_repetition_penalty=1.0, seed=0):
+    s = N.MttsSampling()
+    s.text_temperature = text_temperature
+    s.text_top_p = text_top_p
+    s.text_top_k = text_top_k
+    s.audio_temperature = audio_temperature
+    s.audio_top_p = audio_top_p
+    s.audio_top_k = audio_top_k
+    s.audio_repetition_penalty = audio_repetition_penalty
+    s.seed = seed
+    return s

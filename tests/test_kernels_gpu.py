@@ -1,0 +1,222 @@
+"""Kernel-level parity: each HIP kernel (called through the C ABI) against the
+numpy oracle on the same seeded inputs.  bf16 tolerance: results within the
+bf16 rounding band of the oracle (different fp32 summation order)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import bf16 as B16
+from oracle import moss_delay as O
+from oracle import prng
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def N():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from moss_tts_amd import _native
+    _native.load()
+    return _native
+
+
+def dev_bf16(a):
+    """float32 numpy (bf16-representable) -> torch bf16 cuda"""
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).to(torch.bfloat16).cuda()
+
+
+def host(t):
+    return t.float().cpu().numpy()
+
+
+def P(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def within_band(got, want, ulps=1.0, scale=None):
+    """|got - want| <= ulps * ulp_bf16(scale) element-wise (scale defaults to |want|)"""
+    from tests.parity_util import ulp_bf16
+    s = np.abs(want) if scale is None else scale
+    return np.abs(got - want) <= ulps * ulp_bf16(s) + 1e-30
+
+
+def rand_bf16(rng, shape, scale=1.0):
+    return B16.rnd(rng.standard_normal(shape).astype(np.float32) * np.float32(scale))
+
+
+@pytest.mark.parametrize("B,Nr,K", [(1, 48, 64), (5, 4100, 256), (16, 96, 4096), (17, 64, 128), (32, 1040, 512),
+                                    (40, 48, 96)])
+def test_gemv_store(N, B, Nr, K):
+    rng = np.random.default_rng(B * 1000 + Nr + K)
+    W = rand_bf16(rng, (Nr, K), K ** -0.5)
+    x = rand_bf16(rng, (B, K))
+    wd = dev_bf16(W)
+    packed = torch.zeros(N.load().mtts_k_packed_bytes(Nr, K) // 2, dtype=torch.bfloat16, device="cuda")
+    N.call("mtts_k_pack", P(wd), P(packed), Nr, K, 0, 0, 0, None)
+    xd = dev_bf16(x)
+    y = torch.zeros(B, Nr, dtype=torch.bfloat16, device="cuda")
+    N.call("mtts_k_gemv", P(packed), P(xd), K, P(y), Nr, None, 0, B, Nr, K, 0, 0, 1, 0, None)
+    torch.cuda.synchronize()
+    want = O.linear(O._Ctx("bf16"), x, W)
+    got = host(y)
+    rowscale = np.abs(want).max(axis=1, keepdims=True)
+    assert within_band(got, want, 1.0, scale=np.maximum(np.abs(want), rowscale / 4)).all(), np.abs(got - want).max()
+    assert np.mean(got == want) > 0.9
+
+
+def test_gemv_epilogues(N):
+    rng = np.random.default_rng(5)
+    ctx = O._Ctx("bf16")
+    B, H, I = 3, 256, 96
+    x = rand_bf16(rng, (B, H))
+    Wg, Wu = rand_bf16(rng, (I, H), H ** -0.5), rand_bf16(rng, (I, H), H ** -0.5)
+    packed = torch.zeros(N.load().mtts_k_packed_bytes(2 * I, H) // 2, dtype=torch.bfloat16, device="cuda")
+    wgd, wud = dev_bf16(Wg), dev_bf16(Wu)
+    N.call("mtts_k_pack", P(wgd), P(packed), I, H, 0, 1, 0, None)
+    N.call("mtts_k_pack", P(wud), P(packed), I, H, 0, 1, 1, None)
+    y = torch.zeros(B, I, dtype=torch.bfloat16, device="cuda")
+    xd = dev_bf16(x)
+    N.call("mtts_k_gemv", P(packed), P(xd), H, P(y), I, None, 0, B, I, H, 2, 0, 1, 0, None)
+    torch.cuda.synchronize()
+    g, u = O.linear(ctx, x, Wg), O.linear(ctx, x, Wu)
+    want = ctx.r(ctx.r(O.silu(g)) * u)
+    got = host(y)
+    assert within_band(got, want, 2.0, scale=np.abs(want).max()).all()
+    # residual add, in place
+    Wo = rand_bf16(rng, (H, I), I ** -0.5)
+    po = torch.zeros(N.load().mtts_k_packed_bytes(H, I) // 2, dtype=torch.bfloat16, device="cuda")
+    wod = dev_bf16(Wo)
+    N.call("mtts_k_pack", P(wod), P(po), H, I, 0, 0, 0, None)
+    res = rand_bf16(rng, (B, H))
+    hd = dev_bf16(res)
+    N.call("mtts_k_gemv", P(po), P(y), I, P(hd), H, P(hd), H, B, H, I, 1, 0, 1, 0, None)
+    torch.cuda.synchronize()
+    want2 = ctx.r(res + O.linear(ctx, got, Wo))
+    assert within_band(host(hd), want2, 1.0, scale=np.abs(want2).max()).all()
+    # logits: pad columns -inf
+    Nr = 3 * 1025
+    Wh = rand_bf16(rng, (Nr, H), H ** -0.5)
+    ph = torch.zeros(N.load().mtts_k_packed_bytes(Nr, H) // 2, dtype=torch.bfloat16, device="cuda")
+    whd = dev_bf16(Wh)
+    N.call("mtts_k_pack", P(whd), P(ph), Nr, H, 0, 0, 0, None)
+    lg = torch.zeros(B, Nr, dtype=torch.bfloat16, device="cuda")
+    N.call("mtts_k_gemv", P(ph), P(xd), H, P(lg), Nr, None, 0, B, Nr, H, 3, 0, 1025, 1024, None)
+    torch.cuda.synchronize()
+    got = host(lg)
+    assert np.isneginf(got[:, 1024::1025]).all()
+    fin = np.isfinite(got)
+    assert fin.sum() == B * (Nr - 3)
+
+
+@pytest.mark.parametrize("M,H", [(1, 64), (7, 4096), (3, 12288)])
+def test_rmsnorm(N, M, H):
+    rng = np.random.default_rng(M + H)
+    x = rand_bf16(rng, (M, H), 3.0)
+    w = B16.rnd(1 + 0.25 * rng.standard_normal(H).astype(np.float32))
+    y = torch.zeros(M, H, dtype=torch.bfloat16, device="cuda")
+    xd, wd = dev_bf16(x), dev_bf16(w)  # keep the device tensors alive across the call
+    N.call("mtts_k_rmsnorm", P(xd), 0, H, P(wd), P(y), M, H, ctypes.c_float(1e-6), None)
+    torch.cuda.synchronize()
+    want = O.rmsnorm(O._Ctx("bf16"), x, w, 1e-6)
+    got = host(y)
+    assert within_band(got, want, 1.0).all()
+    assert np.mean(got == want) > 0.99
+
+
+def test_embed_exact(N):
+    cfg = O.tiny_cfg(n_vq=4)
+    rng = np.random.default_rng(1)
+    H = 64
+    et = rand_bf16(rng, (cfg.vocab, H))
+    ea = rand_bf16(rng, (cfg.n_vq, 1025, H))
+    ids = np.concatenate([rng.integers(0, cfg.vocab, (6, 1)), rng.integers(0, 1025, (6, cfg.n_vq))], 1).astype(np.int64)
+    h = torch.zeros(6, H, dtype=torch.bfloat16, device="cuda")
+    idd = torch.from_numpy(ids).cuda()
+    etd, ead = dev_bf16(et), dev_bf16(ea)
+    N.call("mtts_k_embed", P(idd), cfg.n_vq + 1, P(etd), P(ead), 1025, H, P(h), 6, None)
+    torch.cuda.synchronize()
+    W = {"language_model.embed_tokens.weight": et}
+    for j in range(cfg.n_vq):
+        W[f"emb_ext.{j}.weight"] = ea[j]
+    want = O.embed(O._Ctx("bf16"), W, cfg, ids)
+    assert (host(h) == want).all()
+
+
+def test_fill_uniform_matches_oracle_prng(N):
+    n = 5000
+    t = torch.zeros(n, dtype=torch.bfloat16, device="cuda")
+    N.call("mtts_k_fill_uniform", P(t), n, 7, 123, ctypes.c_float(0.05), ctypes.c_float(1.0), None)
+    torch.cuda.synchronize()
+    want = B16.rnd(prng.tensor(7, 123, (n,), 0.05, 1.0))
+    assert (host(t) == want).all()
+
+
+def test_rope_table_matches_oracle():
+    from moss_tts_amd import _native as Nn
+    Nn.load()
+    D, npos = 128, 4096
+    cs = np.zeros((npos, D), np.uint16)
+    sn = np.zeros((npos, D), np.uint16)
+    Nn.call("mtts_rope_table", ctypes.c_float(1e6), D, npos, cs.ctypes.data_as(ctypes.c_void_p),
+            sn.ctypes.data_as(ctypes.c_void_p))
+    c, s = O.rope_cos_sin(O._Ctx("bf16"), O.Cfg(), np.arange(npos))
+    assert np.mean(B16.from_bits(cs) == c) > 0.999
+    assert np.abs(B16.from_bits(cs) - c).max() <= 2 ** -8
+
+
+@pytest.mark.parametrize("S,past,D,Hq,Hkv", [(1, 10, 128, 32, 8), (5, 0, 16, 4, 2), (3, 300, 128, 8, 8)])
+def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
+    rng = np.random.default_rng(S * 7 + past)
+    ctx = O._Ctx("bf16")
+    B, Cmax = 2, 512
+    M = B * S
+    heads = Hq + 2 * Hkv
+    qkv = rand_bf16(rng, (M, heads * D), 2.0)
+    qn = B16.rnd(1 + 0.25 * rng.standard_normal(D).astype(np.float32))
+    kn = B16.rnd(1 + 0.25 * rng.standard_normal(D).astype(np.float32))
+    cfg = O.Cfg(head_dim=D, rope_theta=1e6)
+    cos, sin = O.rope_cos_sin(ctx, cfg, np.arange(Cmax))
+    # existing cache rows 0..past-1
+    kc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
+    vc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
+    kc, vc = dev_bf16(kc0), dev_bf16(vc0)
+    qo = torch.zeros(M, Hq * D, dtype=torch.bfloat16, device="cuda")
+    pos = torch.tensor([past], dtype=torch.int32, device="cuda")
+    keep = [dev_bf16(a) for a in (qkv, qn, kn, cos, sin)]  # alive across the call
+    N.call("mtts_k_qk_norm_rope", P(keep[0]), P(qo), P(kc), P(vc), P(keep[1]), P(keep[2]),
+           P(keep[3]), P(keep[4]), P(pos), M, S, Hq, Hkv, D, Cmax, ctypes.c_float(1e-6), None)
+    torch.cuda.synchronize()
+    x = qkv.reshape(B, S, heads, D)
+    q = O.rmsnorm(ctx, x[:, :, :Hq], qn, 1e-6).transpose(0, 2, 1, 3)
+    k = O.rmsnorm(ctx, x[:, :, Hq:Hq + Hkv], kn, 1e-6).transpose(0, 2, 1, 3)
+    v = x[:, :, Hq + Hkv:].transpose(0, 2, 1, 3)
+    q = O.apply_rope(ctx, q, cos[past:past + S], sin[past:past + S])
+    k = O.apply_rope(ctx, k, cos[past:past + S], sin[past:past + S])
+    gq = host(qo).reshape(B, S, Hq, D).transpose(0, 2, 1, 3)
+    assert within_band(gq, q, 1.0).all() and np.mean(gq == q) > 0.98
+    kcg, vcg = host(kc), host(vc)
+    assert within_band(kcg[:, :, past:past + S], k, 1.0).all()
+    assert (vcg[:, :, past:past + S] == v).all()
+    assert (kcg[:, :, :past] == kc0[:, :, :past]).all()
+    # attention over the cache with a left-padding mask on row 1
+    mask = np.ones((B, Cmax), np.uint8)
+    mask[1, :3] = 0
+    ctxlen = past + S
+    for CH, n_split in ((64, (ctxlen + 63) // 64), (256, (ctxlen + 255) // 256)):
+        ws = torch.zeros(N.load().mtts_k_attention_ws_bytes(M, Hq, D, n_split) // 4 + 1, dtype=torch.float32,
+                         device="cuda")
+        out = torch.zeros(M, Hq * D, dtype=torch.bfloat16, device="cuda")
+        md = torch.from_numpy(mask).cuda()
+        N.call("mtts_k_attention", P(qo), P(kc), P(vc), P(md), P(pos), P(out), P(ws),
+               M, S, Hq, Hkv, D, Cmax, CH, n_split, None)
+        torch.cuda.synchronize()
+        K = kcg[:, :, :ctxlen]
+        V = vcg[:, :, :ctxlen]
+        want = O.attention(ctx, gq, K, V, mask[:, :ctxlen].astype(bool), np.arange(past, past + S), D ** -0.5)
+        got = host(out).reshape(B, S, Hq, D).transpose(0, 2, 1, 3)
+        err = np.abs(got - want)
+        assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), (CH, err.max())
