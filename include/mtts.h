@@ -112,6 +112,12 @@ size_t mtts_k_packed_bytes(int rows, int K);
 /* y[B,N] = epi(x[B,K] . W^T); epi 0 store, 1 residual add (res), 2 swiglu (N = I), 3 logits */
 int mtts_k_gemv(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                 int ldres, int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, void* stream);
+/* as mtts_k_gemv plus the fused RMSNorm prologue (ss_in: per-16-column sums of squares of x,
+ * norm_w: RMSNorm weight; NULL = off), the residual epilogue's sums of squares (ss_out) and a
+ * waves-per-block override (0 = automatic, 4/8/16) */
+int mtts_k_gemv_ex(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                   int ldres, int B, int N, int K, int epi, const float* ss_in, int ld_ss, int n_ss,
+                   const uint16_t* norm_w, float eps, float* ss_out, int ld_ss_out, int force_nw, void* stream);
 int mtts_k_rmsnorm(const uint16_t* x, size_t x_off, size_t x_stride, const uint16_t* w, uint16_t* y, int M, int H,
                    float eps, void* stream);
 int mtts_k_embed(const int64_t* ids, int C, const uint16_t* emb_text, const uint16_t* emb_audio, int audio_rows,
@@ -125,6 +131,12 @@ size_t mtts_k_attention_ws_bytes(int M, int Hq, int D, int n_split);
 int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
                      const int32_t* pos_base_dev, uint16_t* out, void* workspace_dev, int M, int S, int Hq, int Hkv,
                      int D, int Cmax, int CH, int n_split, void* stream);
+/* fused decode step of one layer's attention: q/k RMSNorm + RoPE of the new token (qkv
+ * [B, (Hq+2Hkv)*D]), k/v appended to the cache at *pos_dev, attention over keys 0..pos
+ * under mask [B, Cmax]; out [B, Hq*D] */
+int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, const uint16_t* kn_w, const uint16_t* cos_t,
+                       const uint16_t* sin_t, uint16_t* kc, uint16_t* vc, const uint8_t* mask, const int32_t* pos_dev,
+                       uint16_t* out, int B, int Hq, int Hkv, int D, int Cmax, float eps, void* stream);
 /* RoPE table exactly as the engine builds it: bf16 cos/sin [n_pos, D] on the host */
 int mtts_rope_table(float theta, int D, int n_pos, uint16_t* cos_host, uint16_t* sin_host);
 int mtts_k_fill_uniform(uint16_t* dst, size_t n, uint64_t seed, uint64_t tensor_id, float scale, float offset,

@@ -61,11 +61,13 @@ _SIGS = {
     "mtts_k_pack": (I, [P, P, I, I, I, I, I, P]),
     "mtts_k_packed_bytes": (SZ, [I, I]),
     "mtts_k_gemv": (I, [P, P, I, P, I, P, I, I, I, I, I, I, I, I, P]),
+    "mtts_k_gemv_ex": (I, [P, P, I, P, I, P, I, I, I, I, I, P, I, I, P, F, P, I, I, P]),
     "mtts_k_rmsnorm": (I, [P, SZ, SZ, P, P, I, I, F, P]),
     "mtts_k_embed": (I, [P, I, P, P, I, I, P, I, P]),
     "mtts_k_qk_norm_rope": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P]),
     "mtts_k_attention_ws_bytes": (SZ, [I, I, I, I]),
     "mtts_k_attention": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
+    "mtts_k_attn_decode": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
     "mtts_rope_table": (I, [F, I, I, P, P]),
     "mtts_k_fill_uniform": (I, [P, SZ, U64, U64, F, F, P]),
 }

@@ -44,7 +44,7 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   const int KPW = 64 / LPK;      // keys per wave pass
   const int dl = (lane % LPK) * 8;
   const bf16_t* kbase = a.kc + ((size_t)b * a.Hkv + kvh) * a.Cmax * D;
-  const bf16_t* vbase = a.vc + ((size_t)b * a.Hkv + kvh) * a.Cmax * D;
+  const bf16_t* vbase = a.vc + ((size_t)b * a.Hkv + kvh) * D * a.Cmax;  // V^T [D][Cmax]
   const uint8_t* mrow = a.mask + (size_t)b * a.Cmax;
   for (int kb = c0 + wave * KPW; kb < c1; kb += 4 * KPW) {
     const int key = kb + lane / LPK;
@@ -97,7 +97,8 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
     for (int i = 0; i < 8; ++i) acc[h][i] = 0.f;
   for (int key = c0 + slot; key < c1; key += slots) {
     float vv[8];
-    unpack8(*reinterpret_cast<const uint4*>(vbase + (size_t)key * D + dd), vv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) vv[i] = bf2f(vbase[(size_t)(dd + i) * a.Cmax + key]);
 #pragma unroll
     for (int h = 0; h < G; ++h) {
       const float p = s_s[h * a.CH + (key - c0)];
@@ -180,6 +181,297 @@ hipError_t attention(const AttnArgs& a0, hipStream_t st) {
   const int waves = a.M * a.Hq;
   hipLaunchKernelGGL(attn_combine_kernel, dim3((waves + 3) / 4), dim3(256), 0, st, a);
   return hipGetLastError();
+}
+
+}  // namespace mtts
+
+// ===========================================================================
+// Fused decode attention (one new token per row), MFMA form.  One 512-thread block (8 waves)
+// per (row b, KV head).  Prologue: q_norm / k_norm (TF/.../modeling_qwen3.py:252-254) and
+// RoPE (:148-170) of the new token's G query heads and key; k and v appended to the cache
+// at `pos` (TF/cache_utils.py:127-145).  Then each wave takes 64-key chunks:
+//   S[key][head]  = K_tile[16 keys x 32 dims] . Q^T[32 dims x 16 heads]   (v_mfma 16x16x32 bf16,
+//                   K rows streamed from the cache as A operands, Q^T fragments in 16 VGPRs)
+//   softmax per head over the chunk (fp32, probabilities rounded to bf16 like the reference)
+//   O[head][dim] += P[16 heads x 32 keys] . V[32 keys x 16 dims]          (v_mfma 16x16x32 bf16,
+//                   P through 2 KiB of LDS, V from the TRANSPOSED cache [dim][position] so a
+//                   lane's 8 keys are one 16-byte load)
+// with online rescaling across chunks; the 8 wave partials merge in LDS in a fixed order.
+// Cache layouts: K [Bmax][Hkv][Cmax][D], V [Bmax][Hkv][D][Cmax].
+namespace mtts {
+
+template <int G, int D>
+__global__ __launch_bounds__(512) void attn_decode_kernel(DecAttnArgs a) {
+  constexpr int NWV = 8;
+  constexpr int QS = (D + 31) / 32;  // 32-dim MFMA steps of q.k
+  constexpr int DT = (D + 15) / 16;  // 16-dim output tiles of p.v
+  const int kvh = blockIdx.x, b = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int pos = *a.pos;
+  const int Cmax = a.Cmax;
+  __shared__ __attribute__((aligned(16))) bf16_t q_s[16][QS * 32];   // bf16 q (heads >= G zero)
+  __shared__ float k_s[D];
+  __shared__ float v_s[D];
+  __shared__ __attribute__((aligned(16))) bf16_t p_s[NWV][16][64];
+  __shared__ float ml_s[NWV][G][2];
+  __shared__ float acc_s[NWV][G][D];
+
+  for (int i = threadIdx.x; i < 16 * QS * 32; i += 512) (&q_s[0][0])[i] = 0;
+  __syncthreads();
+  const int heads = a.Hq + 2 * a.Hkv;
+  const bf16_t* row = a.qkv + (size_t)b * heads * D;
+  bf16_t* kcache = a.kc + (((size_t)b * a.Hkv + kvh) * Cmax) * D;    // [Cmax][D]
+  bf16_t* vcache = a.vc + (((size_t)b * a.Hkv + kvh) * D) * Cmax;    // [D][Cmax]
+  // ---- prologue: norm + rope of the new token (waves 0..G-1: q heads, G: k, G+1: v) ----
+  if (wave < G + 2) {
+    const bool act = 2 * lane < D;
+    const int hd = wave < G ? kvh * G + wave : (wave == G ? a.Hq + kvh : a.Hq + a.Hkv + kvh);
+    float x0 = 0.f, x1 = 0.f;
+    if (act) {
+      const uint32_t pr = *reinterpret_cast<const uint32_t*>(row + (size_t)hd * D + 2 * lane);
+      x0 = __uint_as_float(pr << 16);
+      x1 = __uint_as_float(pr & 0xffff0000u);
+    }
+    if (wave == G + 1) {
+      if (act) {
+        v_s[2 * lane] = x0;
+        v_s[2 * lane + 1] = x1;
+        vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
+        vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
+      }
+    } else {
+      const bf16_t* nw = wave < G ? a.qn_w : a.kn_w;
+      const float ss = wave_sum(x0 * x0 + x1 * x1);
+      const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
+      float w0 = 0.f, w1 = 0.f, c0 = 0.f, c1 = 0.f, s0 = 0.f, s1 = 0.f;
+      if (act) {
+        const uint32_t pw = *reinterpret_cast<const uint32_t*>(nw + 2 * lane);
+        w0 = __uint_as_float(pw << 16); w1 = __uint_as_float(pw & 0xffff0000u);
+        const uint32_t pc = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
+        const uint32_t ps = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
+        c0 = __uint_as_float(pc << 16); c1 = __uint_as_float(pc & 0xffff0000u);
+        s0 = __uint_as_float(ps << 16); s1 = __uint_as_float(ps & 0xffff0000u);
+      }
+      const float n0 = rbf(w0 * rbf(x0 * r)), n1 = rbf(w1 * rbf(x1 * r));
+      constexpr int q4 = D / 4;
+      const bool lo = 2 * lane < D / 2;
+      const int partner = lo ? lane + q4 : lane - q4;
+      const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
+      const float sg = lo ? -1.f : 1.f;
+      const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
+      const float o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+      if (act) {
+        if (wave < G) {
+          q_s[wave][2 * lane] = f2bf(o0);
+          q_s[wave][2 * lane + 1] = f2bf(o1);
+        } else {
+          k_s[2 * lane] = o0;
+          k_s[2 * lane + 1] = o1;
+          *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // Q^T B-operand fragments: lane -> head (lane & 15), dims s*32 + 8*(lane>>4) .. +7
+  const int g4 = lane >> 4, c16 = lane & 15;
+  bf16x8 qf[QS];
+#pragma unroll
+  for (int st = 0; st < QS; ++st) qf[st] = *reinterpret_cast<const bf16x8*>(&q_s[c16][st * 32 + 8 * g4]);
+
+  const uint8_t* mrow = a.mask + (size_t)b * Cmax;
+  float m_run = -INFINITY, l_run = 0.f;  // stats of head (lane & 15)
+  f32x4 o_run[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o_run[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int nchunks = (pos + 64) / 64;
+  for (int c = wave; c < nchunks; c += NWV) {
+    const int k0 = c * 64;
+    // ---- issue every load of the chunk first: K tiles, V^T tiles, mask bytes ----
+    u32x4 kt[4][QS];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int key = k0 + t * 16 + c16;
+#pragma unroll
+      for (int st = 0; st < QS; ++st) {
+        const int d0 = st * 32 + 8 * g4;
+        kt[t][st] = (key < pos && d0 < D) ? *reinterpret_cast<const u32x4*>(kcache + (size_t)key * D + d0)
+                                          : (u32x4){0u, 0u, 0u, 0u};
+      }
+    }
+    // V^T B-operand fragments: lane -> dim dt*16 + c16, keys k0 + ks*32 + 8*g4 .. +7
+    u32x4 vt[DT][2];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int dim = dt * 16 + c16;
+        const int kb = k0 + ks * 32 + 8 * g4;
+        vt[dt][ks] = (dim < D && kb < pos) ? *reinterpret_cast<const u32x4*>(vcache + (size_t)dim * Cmax + kb)
+                                           : (u32x4){0u, 0u, 0u, 0u};
+      }
+    // mask bytes of this lane's 16 keys (4 per tile, contiguous; Cmax is a multiple of 64)
+    uint32_t mk[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) mk[t] = *reinterpret_cast<const uint32_t*>(mrow + k0 + t * 16 + g4 * 4);
+
+    // ---- S = K . Q^T for 4 tiles of 16 keys (new key patched from LDS) ----
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (k0 + t * 16 + c16 == pos) {
+#pragma unroll
+        for (int st = 0; st < QS; ++st) {
+          const int d0 = st * 32 + 8 * g4;
+          u32x4 v = {0u, 0u, 0u, 0u};
+          if (d0 < D)
+            for (int i = 0; i < 4; ++i) v[i] = pack2(k_s[d0 + 2 * i], k_s[d0 + 2 * i + 1]);
+          kt[t][st] = v;
+        }
+      }
+    }
+    f32x4 sacc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < QS; ++st)
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][st]), qf[st], sacc[t], 0, 0, 0);
+    }
+    // V^T: keys >= pos zeroed, the new token's value patched from LDS
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int dim = dt * 16 + c16;
+        const int kb = k0 + ks * 32 + 8 * g4;
+        if (dim < D && kb + 8 > pos && kb <= pos) {
+          u32x4 v = vt[dt][ks];
+          const uint32_t nv = (uint32_t)f2bf(v_s[dim]);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int kk = kb + 2 * i;
+            const uint32_t lo = kk < pos ? (v[i] & 0xffffu) : (kk == pos ? nv : 0u);
+            const uint32_t hi = kk + 1 < pos ? (v[i] >> 16) : (kk + 1 == pos ? nv : 0u);
+            v[i] = lo | (hi << 16);
+          }
+          vt[dt][ks] = v;
+        }
+      }
+    // ---- softmax over the chunk for head c16 (rows: keys t*16 + g4*4 + r) ----
+    float sv[4][4];
+    float mc = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + t * 16 + g4 * 4 + r;
+        const bool valid = key <= pos && ((mk[t] >> (8 * r)) & 0xffu);
+        sv[t][r] = valid ? sacc[t][r] * a.scale : -INFINITY;
+        mc = fmaxf(mc, sv[t][r]);
+      }
+    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    float lc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float pr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
+        lc += p;
+        pr[r] = p;
+      }
+      uint2 pk;
+      pk.x = pack2(pr[0], pr[1]);
+      pk.y = pack2(pr[2], pr[3]);
+      *reinterpret_cast<uint2*>(&p_s[wave][c16][t * 16 + g4 * 4]) = pk;  // bf16-rounded probabilities
+    }
+    lc += __shfl_xor(lc, 16, 64);
+    lc += __shfl_xor(lc, 32, 64);
+    const float mn = fmaxf(m_run, mc);
+    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
+    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
+    l_run = l_run * alpha + lc * beta;
+    m_run = mn;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // ---- O_chunk = P . V ----
+    bf16x8 pf[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) pf[ks] = *reinterpret_cast<const bf16x8*>(&p_s[wave][c16][ks * 32 + 8 * g4]);
+    // rescale factors of the output rows (heads g4*4 + r) from the lanes that own those heads
+    float al[4], be[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      al[r] = __shfl(alpha, g4 * 4 + r, 64);
+      be[r] = __shfl(beta, g4 * 4 + r, 64);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      f32x4 oc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[ks], __builtin_bit_cast(bf16x8, vt[dt][ks]), oc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  // ---- merge the 8 wave partials (fixed order) ----
+  if (lane < G) {
+    ml_s[wave][lane][0] = m_run;
+    ml_s[wave][lane][1] = l_run;
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = g4 * 4 + r, dim = dt * 16 + c16;
+      if (h < G && dim < D) acc_s[wave][h][dim] = o_run[dt][r];
+    }
+  __syncthreads();
+  const int t = threadIdx.x;
+  for (int e = t; e < G * D; e += 512) {
+    const int h = e / D, d = e % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) M = fmaxf(M, ml_s[w][h][0]);
+    float L = 0.f, o = 0.f;
+#pragma unroll
+    for (int w = 0; w < NWV; ++w) {
+      const float mw = ml_s[w][h][0];
+      const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
+      L += f * ml_s[w][h][1];
+      o += f * acc_s[w][h][d];
+    }
+    a.out[(size_t)b * a.Hq * D + (size_t)(kvh * G + h) * D + d] = f2bf(L > 0.f ? o / L : 0.f);
+  }
+}
+
+template <int D>
+static hipError_t attn_decode_d(const DecAttnArgs& a, int G, int B, hipStream_t s) {
+  dim3 grid(a.Hkv, B);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((attn_decode_kernel<1, D>), grid, dim3(512), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((attn_decode_kernel<2, D>), grid, dim3(512), 0, s, a); break;
+    case 4: hipLaunchKernelGGL((attn_decode_kernel<4, D>), grid, dim3(512), 0, s, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s) {
+  const int G = a.Hq / a.Hkv;
+  if (a.Hq % a.Hkv || G > 4) return hipErrorInvalidValue;  // G + 2 prologue waves <= 8
+  if (a.Cmax % 8) return hipErrorInvalidValue;             // 16-byte V^T fragments
+  switch (a.D) {
+    case 128: return attn_decode_d<128>(a, G, B, s);
+    case 64: return attn_decode_d<64>(a, G, B, s);
+    case 16: return attn_decode_d<16>(a, G, B, s);
+    default: return hipErrorInvalidValue;
+  }
 }
 
 }  // namespace mtts

@@ -58,6 +58,7 @@ struct mtts_engine {
   uint8_t* mask = nullptr;
   // workspace
   int Mmax = 0;
+  float* ss = nullptr;  // [Mmax, H/16] per-tile sums of squares of the residual stream
   bf16_t *h = nullptr, *xn = nullptr, *qkvb = nullptr, *qb = nullptr, *attnb = nullptr, *act = nullptr;
   float* part = nullptr;
   size_t part_floats = 0;
@@ -166,7 +167,7 @@ static int alloc_capacity(mtts_engine* e) {
   // workspaces
   e->Mmax = std::max(c.max_batch, c.max_prefill_tokens);
   const size_t M = e->Mmax;
-  if ((rc = e->alloc(&e->h, M * H)) || (rc = e->alloc(&e->xn, M * H)) || (rc = e->alloc(&e->qkvb, M * e->qkv_rows)) ||
+  if ((rc = e->alloc(&e->ss, M * (H / 16))) || (rc = e->alloc(&e->h, M * H)) || (rc = e->alloc(&e->xn, M * H)) || (rc = e->alloc(&e->qkvb, M * e->qkv_rows)) ||
       (rc = e->alloc(&e->qb, M * Hq * D)) || (rc = e->alloc(&e->attnb, M * Hq * D)) || (rc = e->alloc(&e->act, M * I)))
     return rc;
   const size_t ns_dec = (c.max_ctx + CH_DECODE - 1) / CH_DECODE;
@@ -200,6 +201,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (hipSetDevice(device) != hipSuccess) return fail(MTTS_E_HIP, "hipSetDevice failed");
   mtts_engine* e = new mtts_engine();
   e->c = c;
+  e->c.max_ctx = (c.max_ctx + 63) / 64 * 64;  // 16-byte V^T fragments, whole 64-key chunks
   if (e->c.max_prefill_tokens <= 0) e->c.max_prefill_tokens = 8192;
   e->device = device;
   auto bail = [&](int rc) {
@@ -251,7 +253,7 @@ extern "C" int mtts_engine_reserve(mtts_engine* e, int max_batch, int max_ctx, i
   for (void* p : e->cap_allocs) hipFree(p);
   e->cap_allocs.clear();
   e->c.max_batch = max_batch;
-  e->c.max_ctx = max_ctx;
+  e->c.max_ctx = (max_ctx + 63) / 64 * 64;
   e->c.max_prefill_tokens = max_prefill_tokens > 0 ? max_prefill_tokens : 8192;
   e->gen_B = 0;
   int rc = alloc_capacity(e);
@@ -400,40 +402,62 @@ extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
 }
 
 // ---------------------------------------------------------------------------
-// forward over rows [b0, b0+B) with S tokens each; pos_base device pointer
+// forward over rows [b0, b0+B) with S tokens each; pos_base device pointer.
+// Per layer: input RMSNorm (single pass, from the residual epilogue's sums of squares) ->
+// q|k|v GEMV -> attention (decode: one fused kernel incl. q/k norm, RoPE, KV append;
+// prefill: norm/rope/append + split-K attention + combine) -> o_proj GEMV (+residual,
+// +sums of squares) -> post-attention RMSNorm -> gate|up GEMV (SwiGLU epilogue) -> down
+// GEMV (+residual, +sums of squares).
 static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
                         int n_split, bf16_t* logits_out, hipStream_t s) {
   const mtts_config& c = e->c;
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter, C = c.n_vq + 1;
   const int M = B * S;
-  HIPCHK(embed(ids, C, e->emb_text, e->emb_audio, e->audio_rows, H, e->h, M, s));
+  const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
+  HIPCHK(embed(ids, C, e->emb_text, e->emb_audio, e->audio_rows, H, e->h, M, s, e->ss, NT));
   const float eps = c.rms_eps;
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& w = e->L[l];
-    HIPCHK(rmsnorm(e->h, 0, H, w.in_norm, e->xn, M, H, eps, s));
-    HIPCHK(gemv(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, nullptr, 0, M, e->qkv_rows, H, EPI_STORE, 0, 1, 0, s));
-    QKRopeArgs qa;
-    qa.qkv = e->qkvb; qa.q_out = e->qb;
-    qa.kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
-    qa.vc = e->vc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
-    qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = e->cos_t; qa.sin_t = e->sin_t;
-    qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = c.max_ctx; qa.eps = eps; qa.M = M;
-    HIPCHK(qk_norm_rope(qa, s));
-    AttnArgs aa;
-    aa.q = e->qb; aa.kc = qa.kc; aa.vc = qa.vc; aa.mask = e->mask + (size_t)b0 * c.max_ctx; aa.pos_base = pos_base;
-    aa.part_o = e->part; aa.part_ml = e->part + (size_t)M * n_split * Hq * D; aa.out = e->attnb;
-    aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = c.max_ctx; aa.CH = CH; aa.n_split = n_split; aa.M = M;
-    aa.scale = 1.0f / std::sqrt((float)D);
-    HIPCHK(attention(aa, s));
-    HIPCHK(gemv(w.o, e->attnb, Hq * D, e->h, H, e->h, H, M, H, Hq * D, EPI_RESADD, 0, 1, 0, s));
-    HIPCHK(rmsnorm(e->h, 0, H, w.post_norm, e->xn, M, H, eps, s));
-    HIPCHK(gemv(w.gu, e->xn, H, e->act, I, nullptr, 0, M, I, H, EPI_SWIGLU, 0, 1, 0, s));
-    HIPCHK(gemv(w.down, e->act, I, e->h, H, e->h, H, M, H, I, EPI_RESADD, 0, 1, 0, s));
+    bf16_t* kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
+    bf16_t* vc = e->vc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
+    HIPCHK(rmsnorm_ss(e->h, 0, H, e->ss, 0, NT, w.in_norm, e->xn, M, H, eps, s));
+    GemvArgs g = gemv_args(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, M, e->qkv_rows, H);
+    HIPCHK(gemv_ex(g, EPI_STORE, s));
+    if (S == 1) {
+      DecAttnArgs da;
+      da.qkv = e->qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = e->cos_t; da.sin_t = e->sin_t;
+      da.kc = kc; da.vc = vc; da.mask = e->mask + (size_t)b0 * c.max_ctx; da.pos = pos_base; da.out = e->attnb;
+      da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = c.max_ctx; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
+      HIPCHK(attn_decode(da, B, s));
+    } else {
+      QKRopeArgs qa;
+      qa.qkv = e->qkvb; qa.q_out = e->qb; qa.kc = kc; qa.vc = vc;
+      qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = e->cos_t; qa.sin_t = e->sin_t;
+      qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = c.max_ctx; qa.eps = eps; qa.M = M;
+      HIPCHK(qk_norm_rope(qa, s));
+      AttnArgs aa;
+      aa.q = e->qb; aa.kc = kc; aa.vc = vc; aa.mask = e->mask + (size_t)b0 * c.max_ctx; aa.pos_base = pos_base;
+      aa.part_o = e->part; aa.part_ml = e->part + (size_t)M * n_split * Hq * D; aa.out = e->attnb;
+      aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = c.max_ctx; aa.CH = CH; aa.n_split = n_split; aa.M = M;
+      aa.scale = 1.0f / std::sqrt((float)D);
+      HIPCHK(attention(aa, s));
+    }
+    g = gemv_args(w.o, e->attnb, Hq * D, e->h, H, M, H, Hq * D);
+    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT;
+    HIPCHK(gemv_ex(g, EPI_RESADD, s));
+    HIPCHK(rmsnorm_ss(e->h, 0, H, e->ss, 0, NT, w.post_norm, e->xn, M, H, eps, s));
+    g = gemv_args(w.gu, e->xn, H, e->act, I, M, I, H);
+    HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
+    g = gemv_args(w.down, e->act, I, e->h, H, M, H, I);
+    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT;
+    HIPCHK(gemv_ex(g, EPI_RESADD, s));
   }
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
-  HIPCHK(rmsnorm(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->final_norm, e->xn, B, H, eps, s));
-  HIPCHK(gemv(e->heads, e->xn, H, logits_out, e->heads_ld, nullptr, 0, B, e->heads_rows, H, EPI_LOGITS, c.vocab,
-              e->audio_rows, e->audio_rows - 1, s));
+  HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
+                    e->final_norm, e->xn, B, H, eps, s));
+  GemvArgs g = gemv_args(e->heads, e->xn, H, logits_out, e->heads_ld, B, e->heads_rows, H);
+  g.pad_start = c.vocab; g.pad_period = e->audio_rows; g.pad_off = e->audio_rows - 1;
+  HIPCHK(gemv_ex(g, EPI_LOGITS, s));
   return 0;
 }
 
@@ -441,7 +465,7 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
 static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s) {
   const mtts_config& c = e->c;
   if (S > e->Mmax) return fail(MTTS_E_UNSUPPORTED, "prompt longer than max_prefill_tokens");
-  HIPCHK(hipMemcpyAsync(e->d_pos, &past, sizeof(int), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->d_pos), past, 1, s));
   const int rows_per = std::max(1, e->Mmax / S);
   const int CH = S == 1 ? CH_DECODE : CH_PREFILL;
   const int n_split = (past + S + CH - 1) / CH;
@@ -701,5 +725,31 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
   *avg_ms = ms / iters;
   // algorithmic bytes: weights once + activations in + outputs (+ residual read)
   *alg_bytes = 2ull * wrows * K + 2ull * B * K + 2ull * B * N * (res ? 2 : 1);
+  return 0;
+}
+
+extern "C" int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, const uint16_t* kn_w, const uint16_t* cos_t,
+                                  const uint16_t* sin_t, uint16_t* kc, uint16_t* vc, const uint8_t* mask,
+                                  const int32_t* pos, uint16_t* out, int B, int Hq, int Hkv, int D, int Cmax, float eps,
+                                  void* stream) {
+  DecAttnArgs a;
+  a.qkv = qkv; a.qn_w = qn_w; a.kn_w = kn_w; a.cos_t = cos_t; a.sin_t = sin_t; a.kc = kc; a.vc = vc; a.mask = mask;
+  a.pos = pos; a.out = out; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.eps = eps;
+  a.scale = 1.0f / std::sqrt((float)D);
+  HIPCHK(attn_decode(a, B, (hipStream_t)stream));
+  return 0;
+}
+
+// full-control GEMV (fused norm prologue, sum-of-squares epilogue, waves-per-block override)
+extern "C" int mtts_k_gemv_ex(const uint16_t* w, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                              int ldres, int B, int N, int K, int epi, const float* ss_in, int ld_ss, int n_ss,
+                              const uint16_t* norm_w, float eps, float* ss_out, int ld_ss_out, int force_nw,
+                              void* stream) {
+  GemvArgs a = gemv_args(w, x, ldx, y, ldy, B, N, K);
+  a.res = res; a.ldres = ldres;
+  a.ss_in = ss_in; a.ld_ss = ld_ss; a.n_ss = n_ss; a.nw = norm_w; a.eps = eps;
+  a.ss_out = ss_out; a.ld_ss_out = ld_ss_out; a.force_nw = force_nw;
+  if (epi == EPI_LOGITS) return fail(MTTS_E_INVALID, "use mtts_k_gemv for logits");
+  HIPCHK(gemv_ex(a, epi, (hipStream_t)stream));
   return 0;
 }

@@ -7,27 +7,43 @@
 // HBM layout ("MFMA-tile packed"): W is stored as 1 KiB tiles of 16 rows x 32 k, in
 // exactly the A-operand order of v_mfma_f32_16x16x32_bf16 (lane l holds row l&15,
 // k = 8*(l>>4) .. +7), tiles ordered [row_tile][k_tile].  A wave's stream over its
-// K range is therefore one contiguous run of 1 KiB wave-loads (16 B/lane, fully
-// coalesced), each feeding one MFMA with no LDS round trip.
+// K range is one contiguous run of 1 KiB wave-loads (16 B/lane, fully coalesced,
+// non-temporal: each weight byte is read once per step), each feeding one MFMA with
+// no LDS round trip.  x (the B activation rows) is the MFMA B operand, read from L2.
 //
-// Work split: one 256-thread block per 16-row output tile (RT=2: a gate tile and an
-// up tile that share x fragments), the 4 waves split K, partial tiles are reduced
-// through LDS in a fixed order (deterministic), and the epilogue fuses the op that
-// follows the matmul in the reference (residual add, SwiGLU, audio pad-column mask).
+// Work split: one block of NW waves per 16-row output tile (RT=2: a gate tile and an
+// up tile that share x fragments); the NW waves split K and their partial tiles are
+// reduced through LDS in a fixed order (deterministic).  NW is picked per matrix so
+// that every CU holds enough waves (bytes in flight) even for 4096-row matrices.
+//
+// Fusions: the RMSNorm that precedes q|k|v, gate|up and the heads runs in the prologue
+// (x is normalised per fragment from per-tile sums of squares), and the op that follows
+// the matmul runs in the epilogue (residual add + its sums of squares, SwiGLU, the
+// audio-head pad column mask).
 #include "kernels.h"
 
 namespace mtts {
 
+// bf16(nw * bf16(x * r)) for 8 packed elements (Qwen3RMSNorm rounding points)
+__device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
+  u32x4 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float x0 = __uint_as_float(xv[i] << 16), x1 = __uint_as_float(xv[i] & 0xffff0000u);
+    const float w0 = __uint_as_float(wv[i] << 16), w1 = __uint_as_float(wv[i] & 0xffff0000u);
+    o[i] = pack2(w0 * rbf(x0 * r), w1 * rbf(x1 * r));
+  }
+  return o;
+}
 
-
-template <int NB, int RT, int EPI>
-__global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
+template <int NB, int RT, int EPI, bool NORM, int NW>
+__global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
   constexpr int U = 8;  // k-tiles in flight per wave
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int bt = blockIdx.x;  // output row tile
   const int KT = a.KT;
-  const int per = (KT + 3) >> 2;
+  const int per = (KT + NW - 1) / NW;
   const int kt0 = wave * per;
   const int kt1 = min(KT, kt0 + per);
 
@@ -45,26 +61,65 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
   // B operand: x rows (b = lane&15 + 16 nb), 8 consecutive k at 8*(lane>>4)
   const u32x4* xbase[NB];
   bool xok[NB];
+  float rr[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int b = (lane & 15) + 16 * nb;
     xok[nb] = b < a.B;
     xbase[nb] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
+    rr[nb] = 0.f;
   }
+  const u32x4* nwbase = NORM ? reinterpret_cast<const u32x4*>(a.nw + (lane >> 4) * 8) : nullptr;
 
+  // all loads of the first k-batch (weights, x fragments, norm weights) go out before the
+  // latency-bound norm prologue, so that prologue overlaps the first HBM round trip
   int kt = kt0;
-  for (; kt + U <= kt1; kt += U) {
-    u32x4 wa[RT][U];
-    u32x4 xb[NB][U];
+  u32x4 wa[RT][U];
+  u32x4 xb[NB][U];
+  u32x4 wn[U];
+  auto issue = [&](int k) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < RT; ++r) wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)(kt + u) * 64);
+      for (int r = 0; r < RT; ++r) wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)(k + u) * 64);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb)
-        xb[nb][u] = xok[nb] ? xbase[nb][(kt + u) * 4] : (u32x4){0u, 0u, 0u, 0u};
+        xb[nb][u] = xok[nb] ? xbase[nb][(k + u) * 4] : (u32x4){0u, 0u, 0u, 0u};
+    if constexpr (NORM) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wn[u] = nwbase[(k + u) * 4];
+    }
+  };
+  if (kt + U <= kt1) issue(kt);
+  if constexpr (NORM) {
+    // r_b = rsqrt(mean(x_b^2) + eps) from the producer's per-16-column sums of squares:
+    // one coalesced float4 per lane per row, a wave reduction, lanes keep their own rows
+    const int nrow = min(a.B, 16 * NB);
+    for (int b = 0; b < nrow; ++b) {
+      const float* sp = a.ss_in + (size_t)b * a.ld_ss;
+      float ss = 0.f;
+      for (int t4 = lane * 4; t4 < a.n_ss; t4 += 256) {
+        const float4 v = *reinterpret_cast<const float4*>(sp + t4);
+        ss += (v.x + v.y) + (v.z + v.w);
+      }
+      ss = wave_sum(ss);
+      const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb)
+        if ((lane & 15) + 16 * nb == b) rr[nb] = r;
+    }
+  }
+
+  for (; kt + U <= kt1; kt += U) {
+    if (kt != kt0) issue(kt);
+    if constexpr (NORM) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int nb = 0; nb < NB; ++nb) xb[nb][u] = norm8(xb[nb][u], wn[u], rr[nb]);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -75,20 +130,25 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
               __builtin_bit_cast(bf16x8, wa[r][u]), __builtin_bit_cast(bf16x8, xb[nb][u]), acc[r][nb], 0, 0, 0);
   }
   for (; kt < kt1; ++kt) {
+    u32x4 xv[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      xv[nb] = xok[nb] ? xbase[nb][kt * 4] : (u32x4){0u, 0u, 0u, 0u};
+      if constexpr (NORM) xv[nb] = norm8(xv[nb], nwbase[kt * 4], rr[nb]);
+    }
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
-      u32x4 wv = __builtin_nontemporal_load(wbase[r] + (size_t)kt * 64);
+      const u32x4 wv = __builtin_nontemporal_load(wbase[r] + (size_t)kt * 64);
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) {
-        u32x4 xv = xok[nb] ? xbase[nb][kt * 4] : (u32x4){0u, 0u, 0u, 0u};
+      for (int nb = 0; nb < NB; ++nb)
         acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, xv), acc[r][nb], 0, 0, 0);
-      }
+            __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, xv[nb]), acc[r][nb], 0, 0, 0);
     }
   }
 
-  // ---- fixed-order reduction of the 4 waves' partial tiles through LDS ----
-  __shared__ float red[4][RT][NB][256];
+  // ---- fixed-order reduction of the NW waves' partial tiles through LDS ----
+  __shared__ float red[NW][RT][NB][256];
+  __shared__ float sq[NB][16][17];
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -98,34 +158,54 @@ __global__ __launch_bounds__(256) void gemv_kernel(GemvArgs a) {
   __syncthreads();
 
   const int t = threadIdx.x;
-  // element t: lane = t/4, reg = t%4 -> n = ((lane>>4)*4 + reg), b = lane & 15
-  const int ln = t >> 2;
-  const int nl = ((ln >> 4) << 2) + (t & 3);
-  const int n = bt * 16 + nl;
+  if (t < 256) {
+    // element t: lane = t/4, reg = t%4 -> n = ((lane>>4)*4 + reg), b = lane & 15
+    const int ln = t >> 2;
+    const int nl = ((ln >> 4) << 2) + (t & 3);
+    const int n = bt * 16 + nl;
 #pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    const int b = (ln & 15) + 16 * nb;
-    float v[RT];
+    for (int nb = 0; nb < NB; ++nb) {
+      const int bl = ln & 15;
+      const int b = bl + 16 * nb;
+      float v[RT];
 #pragma unroll
-    for (int r = 0; r < RT; ++r)
-      v[r] = ((red[0][r][nb][t] + red[1][r][nb][t]) + red[2][r][nb][t]) + red[3][r][nb][t];
-    if (b >= a.B || n >= a.N) continue;
-    bf16_t out;
-    if constexpr (EPI == EPI_STORE) {
-      out = f2bf(v[0]);
-    } else if constexpr (EPI == EPI_LOGITS) {
-      out = f2bf(v[0]);
-      if (n >= a.pad_start && ((n - a.pad_start) % a.pad_period) == a.pad_off) out = 0xFF80;  // -inf
-    } else if constexpr (EPI == EPI_RESADD) {
-      // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
-      out = f2bf(bf2f(a.res[(size_t)b * a.ldres + n]) + rbf(v[0]));
-    } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
-      const float g = rbf(v[0]);
-      const float u = rbf(v[RT - 1]);
-      const float s = rbf(g / (1.0f + expf(-g)));
-      out = f2bf(s * u);
+      for (int r = 0; r < RT; ++r) {
+        float s = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) s += red[w][r][nb][t];
+        v[r] = s;
+      }
+      bf16_t out = 0;
+      if constexpr (EPI == EPI_STORE) {
+        out = f2bf(v[0]);
+      } else if constexpr (EPI == EPI_LOGITS) {
+        out = f2bf(v[0]);
+        if (n >= a.pad_start && ((n - a.pad_start) % a.pad_period) == a.pad_off) out = 0xFF80;  // -inf
+      } else if constexpr (EPI == EPI_RESADD) {
+        // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
+        if (b < a.B && n < a.N) out = f2bf(bf2f(a.res[(size_t)b * a.ldres + n]) + rbf(v[0]));
+        const float ho = bf2f(out);
+        sq[nb][bl][nl] = ho * ho;
+      } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
+        const float g = rbf(v[0]);
+        const float u = rbf(v[RT - 1]);
+        const float s = rbf(g / (1.0f + expf(-g)));
+        out = f2bf(s * u);
+      }
+      if (b < a.B && n < a.N) a.y[(size_t)b * a.ldy + n] = out;
     }
-    a.y[(size_t)b * a.ldy + n] = out;
+  }
+  if constexpr (EPI == EPI_RESADD) {
+    __syncthreads();
+    if (a.ss_out && t < 16 * NB) {
+      const int nb = t >> 4, bl = t & 15, b = bl + 16 * nb;
+      if (b < a.B) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) s += sq[nb][bl][i];
+        a.ss_out[(size_t)b * a.ld_ss_out + bt] = s;
+      }
+    }
   }
 }
 
@@ -150,42 +230,67 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
   }
 }
 
-}  // namespace mtts
-
 // ---------------------------------------------------------------------------
-// launch helpers (used by the engine and by the kernel-level C-ABI)
-namespace mtts {
-
-template <int NB, int RT, int EPI>
-static void launch_gemv_t(const GemvArgs& a, int n_tiles, hipStream_t s) {
-  hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI>), dim3(n_tiles), dim3(256), 0, s, a);
+template <int NB, int RT, int EPI, bool NORM>
+static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
+  // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
+  // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
+  const int rows = n_tiles * RT * 16;
+  if (a.force_nw == 4 || a.force_nw == 8 || a.force_nw == 16) {
+    if (a.force_nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4>), dim3(n_tiles), dim3(256), 0, s, a);
+    if (a.force_nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8>), dim3(n_tiles), dim3(512), 0, s, a);
+    if (a.force_nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16>), dim3(n_tiles), dim3(1024), 0, s, a);
+    return;
+  }
+  if (a.KT < 64)
+    hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4>), dim3(n_tiles), dim3(256), 0, s, a);
+  else if (rows >= 8192 || a.KT < 128)
+    hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8>), dim3(n_tiles), dim3(512), 0, s, a);
+  else
+    hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16>), dim3(n_tiles), dim3(1024), 0, s, a);
 }
 
-// y = epi(x . W^T) for B rows; chunks of 32 rows (weights re-streamed per chunk)
-hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int ldy, const bf16_t* res, int ldres,
-                int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, hipStream_t s) {
-  if (K % 32 != 0 || B <= 0 || N <= 0) return hipErrorInvalidValue;
-  for (int b0 = 0; b0 < B; b0 += 32) {
-    GemvArgs a;
-    a.w = wpacked;
-    a.x = x + (size_t)b0 * ldx;
-    a.y = y + (size_t)b0 * ldy;
-    a.res = res ? res + (size_t)b0 * ldres : nullptr;
-    a.ldx = ldx; a.ldy = ldy; a.ldres = ldres;
-    a.B = min(32, B - b0);
-    a.N = N; a.K = K; a.KT = K / 32;
-    a.pad_start = pad_start; a.pad_period = pad_period > 0 ? pad_period : 1; a.pad_off = pad_off;
-    const int n_tiles = (N + 15) / 16;
-    const bool two = a.B > 16;
+template <int RT, int EPI>
+static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
+  const bool two = a.B > 16;
+  const bool norm = a.ss_in != nullptr;
+  if (two) norm ? launch_nw<2, RT, EPI, true>(a, n_tiles, s) : launch_nw<2, RT, EPI, false>(a, n_tiles, s);
+  else norm ? launch_nw<1, RT, EPI, true>(a, n_tiles, s) : launch_nw<1, RT, EPI, false>(a, n_tiles, s);
+}
+
+hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
+  if (a0.K % 32 != 0 || a0.B <= 0 || a0.N <= 0) return hipErrorInvalidValue;
+  for (int b0 = 0; b0 < a0.B; b0 += 32) {
+    GemvArgs a = a0;
+    a.x = a0.x + (size_t)b0 * a0.ldx;
+    a.y = a0.y + (size_t)b0 * a0.ldy;
+    a.res = a0.res ? a0.res + (size_t)b0 * a0.ldres : nullptr;
+    a.ss_in = a0.ss_in ? a0.ss_in + (size_t)b0 * a0.ld_ss : nullptr;
+    a.ss_out = a0.ss_out ? a0.ss_out + (size_t)b0 * a0.ld_ss_out : nullptr;
+    a.B = min(32, a0.B - b0);
+    a.KT = a0.K / 32;
+    if (a.pad_period <= 0) a.pad_period = 1;
+    const int n_tiles = (a0.N + 15) / 16;
     switch (epi) {
-      case EPI_STORE:  two ? launch_gemv_t<2, 1, EPI_STORE>(a, n_tiles, s) : launch_gemv_t<1, 1, EPI_STORE>(a, n_tiles, s); break;
-      case EPI_LOGITS: two ? launch_gemv_t<2, 1, EPI_LOGITS>(a, n_tiles, s) : launch_gemv_t<1, 1, EPI_LOGITS>(a, n_tiles, s); break;
-      case EPI_RESADD: two ? launch_gemv_t<2, 1, EPI_RESADD>(a, n_tiles, s) : launch_gemv_t<1, 1, EPI_RESADD>(a, n_tiles, s); break;
-      case EPI_SWIGLU: two ? launch_gemv_t<2, 2, EPI_SWIGLU>(a, n_tiles, s) : launch_gemv_t<1, 2, EPI_SWIGLU>(a, n_tiles, s); break;
+      case EPI_STORE: launch_epi<1, EPI_STORE>(a, n_tiles, s); break;
+      case EPI_LOGITS: launch_epi<1, EPI_LOGITS>(a, n_tiles, s); break;
+      case EPI_RESADD: launch_epi<1, EPI_RESADD>(a, n_tiles, s); break;
+      case EPI_SWIGLU: launch_epi<2, EPI_SWIGLU>(a, n_tiles, s); break;
       default: return hipErrorInvalidValue;
     }
   }
   return hipGetLastError();
+}
+
+hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int ldy, const bf16_t* res, int ldres,
+                int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, hipStream_t s) {
+  GemvArgs a = gemv_args(wpacked, x, ldx, y, ldy, B, N, K);
+  a.res = res;
+  a.ldres = ldres;
+  a.pad_start = pad_start;
+  a.pad_period = pad_period;
+  a.pad_off = pad_off;
+  return gemv_ex(a, epi, s);
 }
 
 hipError_t pack_weight(const bf16_t* src, bf16_t* dst, int rows, int K, int row_offset, int interleave, int which,

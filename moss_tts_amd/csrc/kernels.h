@@ -21,7 +21,25 @@ struct GemvArgs {
   int KT;              // K / 32
   // EPI_LOGITS: columns n >= pad_start with (n - pad_start) % pad_period == pad_off -> -inf
   int pad_start, pad_period, pad_off;
+  // fused Qwen3RMSNorm of x (TF/.../modeling_qwen3.py:59-64) when ss_in != nullptr:
+  //   x' = bf16(nw[k] * bf16(x[b,k] * r_b)),  r_b = 1/sqrt(sum_t ss_in[b*ld_ss + t] / K + eps)
+  // where ss_in holds per-16-column partial sums of squares of x (written by the producer)
+  const float* ss_in;
+  int ld_ss, n_ss;
+  const bf16_t* nw;
+  float eps;
+  // EPI_RESADD: writes the partial sum of squares of its 16 new residual columns per row
+  float* ss_out;       // [B, ld_ss_out] (nullptr: skip)
+  int ld_ss_out;
+  int force_nw;        // 0: automatic waves-per-block choice; 4/8/16: forced (tuning)
 };
+
+inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {
+  GemvArgs a{};
+  a.w = w; a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy; a.B = B; a.N = N; a.K = K; a.KT = K / 32;
+  a.pad_period = 1;
+  return a;
+}
 
 struct QKRopeArgs {
   const bf16_t* qkv;
@@ -51,6 +69,22 @@ struct AttnArgs {
   bf16_t* out;           // [M, Hq*D]
   int S, Hq, Hkv, D, Cmax, CH, n_split, M;
   float scale;
+};
+
+// fused decode attention: one new token per row
+struct DecAttnArgs {
+  const bf16_t* qkv;    // [B, (Hq + 2 Hkv) * D]  output of the q|k|v GEMV
+  const bf16_t* qn_w;
+  const bf16_t* kn_w;
+  const bf16_t* cos_t;  // [max_pos, D]
+  const bf16_t* sin_t;
+  bf16_t* kc;           // layer cache [Bmax][Hkv][Cmax][D]
+  bf16_t* vc;
+  const uint8_t* mask;  // [Bmax][Cmax]
+  const int* pos;       // device: absolute position of the new token
+  bf16_t* out;          // [B, Hq * D]
+  int Hq, Hkv, D, Cmax;
+  float eps, scale;
 };
 
 struct GenDev {
@@ -91,17 +125,22 @@ struct GenBufs {
 // gemv.hip
 hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int ldy, const bf16_t* res, int ldres,
                 int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, hipStream_t s);
+// full-control form (fused norm prologue / sum-of-squares epilogue); rows > 32 are chunked
+hipError_t gemv_ex(const GemvArgs& a, int epi, hipStream_t s);
 hipError_t pack_weight(const bf16_t* src, bf16_t* dst, int rows, int K, int row_offset, int interleave, int which,
                        hipStream_t s);
 // norm_rope.hip
 hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
-                 bf16_t* h, int M, hipStream_t s);
+                 bf16_t* h, int M, hipStream_t s, float* ss_out = nullptr, int ld_ss = 0);
 hipError_t rmsnorm(const bf16_t* x, size_t x_off, size_t x_stride, const bf16_t* w, bf16_t* y, int M, int H, float eps,
                    hipStream_t s);
+hipError_t rmsnorm_ss(const bf16_t* x, size_t x_off, size_t x_stride, const float* ss, size_t ss_off, size_t ss_stride,
+                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s);
 hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s);
 // attention.hip
 size_t attn_smem_bytes(int G, int D, int CH);
 hipError_t attention(const AttnArgs& a, hipStream_t s);
+hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);

@@ -6,14 +6,19 @@ namespace mtts {
 // ---------------------------------------------------------------------------
 // h[m, :] = E_text[ids[m,0]] + E_0[ids[m,1]] + ... + E_{n-1}[ids[m,n]], each add rounded to
 // bf16 left to right (moss_tts_delay/modeling_moss_tts.py:196-213).  One block per token.
+// Grid (M, H/2048): each thread owns one 8-wide chunk; it also emits the sum of squares of
+// every 16-column tile (pairs of chunks) for the fused RMSNorm of the first q|k|v GEMV.
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int C, const bf16_t* __restrict__ emb_text,
                                                     const bf16_t* __restrict__ emb_audio, int audio_rows, int H,
-                                                    bf16_t* __restrict__ h) {
+                                                    bf16_t* __restrict__ h, float* __restrict__ ss_out, int ld_ss) {
   const int m = blockIdx.x;
   const int64_t* id = ids + (size_t)m * C;
   const int nchunk = H >> 3;
-  for (int c = threadIdx.x; c < nchunk; c += blockDim.x) {
-    float e[8];
+  const int c = blockIdx.y * 256 + threadIdx.x;
+  const bool ok = c < nchunk;
+  float e[8];
+  for (int i = 0; i < 8; ++i) e[i] = 0.f;
+  if (ok) {
     unpack8(*reinterpret_cast<const uint4*>(emb_text + (size_t)id[0] * H + c * 8), e);
     for (int j = 1; j < C; ++j) {
       float a[8];
@@ -25,6 +30,11 @@ __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ 
     o.x = pack2(e[0], e[1]); o.y = pack2(e[2], e[3]); o.z = pack2(e[4], e[5]); o.w = pack2(e[6], e[7]);
     *reinterpret_cast<uint4*>(h + (size_t)m * H + c * 8) = o;
   }
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ss += e[i] * e[i];
+  ss += __shfl_xor(ss, 1, 64);
+  if (ss_out && ok && (c & 1) == 0) ss_out[(size_t)m * ld_ss + (c >> 1)] = ss;
 }
 
 // ---------------------------------------------------------------------------
@@ -64,6 +74,53 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// Single-pass Qwen3RMSNorm from the producer's per-16-column sums of squares (written by
+// the residual-add GEMV epilogue or the embedding kernel): every wave reduces the row's
+// H/16 partials itself (one float4 per lane), so there is no block-wide reduction and x
+// is read once.  Block = H/8 threads (one 16-byte chunk each), one block per row.
+__global__ __launch_bounds__(512) void rmsnorm_ss_kernel(const bf16_t* __restrict__ x, size_t x_off, size_t x_stride,
+                                                         const float* __restrict__ ss, size_t ss_off, size_t ss_stride,
+                                                         const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int H,
+                                                         float eps) {
+  const int m = blockIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int c = threadIdx.x;
+  const bf16_t* xr = x + x_off + (size_t)m * x_stride;
+  uint4 xv = make_uint4(0, 0, 0, 0), wv = make_uint4(0, 0, 0, 0);
+  const bool ok = c < (H >> 3);
+  if (ok) {
+    xv = *reinterpret_cast<const uint4*>(xr + c * 8);
+    wv = *reinterpret_cast<const uint4*>(w + c * 8);
+  }
+  const float* sp = ss + ss_off + (size_t)m * ss_stride;
+  float s = 0.f;
+  for (int t4 = lane * 4; t4 < (H >> 4); t4 += 256) {
+    const float4 v = *reinterpret_cast<const float4*>(sp + t4);
+    s += (v.x + v.y) + (v.z + v.w);
+  }
+  s = wave_sum(s);
+  const float r = 1.0f / sqrtf(s / (float)H + eps);
+  if (!ok) return;
+  float v[8], g[8], q[8];
+  unpack8(xv, v);
+  unpack8(wv, g);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = g[i] * rbf(v[i] * r);
+  uint4 o;
+  o.x = pack2(q[0], q[1]); o.y = pack2(q[2], q[3]); o.z = pack2(q[4], q[5]); o.w = pack2(q[6], q[7]);
+  *reinterpret_cast<uint4*>(y + (size_t)m * H + c * 8) = o;
+}
+
+hipError_t rmsnorm_ss(const bf16_t* x, size_t x_off, size_t x_stride, const float* ss, size_t ss_off, size_t ss_stride,
+                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s) {
+  if (H % 16 || H > 4096) return hipErrorInvalidValue;  // one 16-byte chunk per thread, <= 512 threads
+  const int threads = ((H / 8 + 63) / 64) * 64;
+  hipLaunchKernelGGL(rmsnorm_ss_kernel, dim3(M), dim3(threads < 64 ? 64 : threads), 0, s, x, x_off, x_stride, ss,
+                     ss_off, ss_stride, w, y, H, eps);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Per-head q_norm / k_norm (TF/.../modeling_qwen3.py:252-254), RoPE in bf16
 // (:148-170, cos/sin from a bf16 table computed in fp32, :126-137) and the KV
 // cache append (DynamicLayer.update, TF/cache_utils.py:127-145) as an in-place
@@ -94,9 +151,10 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
   }
   if (hd >= a.Hq + a.Hkv) {  // V head: copy into the cache
     const int kvh = hd - a.Hq - a.Hkv;
-    if (act) {
-      bf16_t* dst = a.vc + (((size_t)b * a.Hkv + kvh) * a.Cmax + pos) * D;
-      *reinterpret_cast<uint32_t*>(dst + 2 * lane) = pack2(x0, x1);
+    if (act) {  // V cache is stored transposed: [Hkv][D][Cmax]
+      bf16_t* dst = a.vc + ((size_t)b * a.Hkv + kvh) * D * a.Cmax + pos;
+      dst[(size_t)(2 * lane) * a.Cmax] = f2bf(x0);
+      dst[(size_t)(2 * lane + 1) * a.Cmax] = f2bf(x1);
     }
     return;
   }
@@ -140,9 +198,11 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
 }
 
 hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
-                 bf16_t* h, int M, hipStream_t s) {
-  if (H % 8) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(embed_kernel, dim3(M), dim3(256), 0, s, ids, C, emb_text, emb_audio, audio_rows, H, h);
+                 bf16_t* h, int M, hipStream_t s, float* ss_out, int ld_ss) {
+  if (H % 16) return hipErrorInvalidValue;
+  const int nchunk = H / 8;
+  hipLaunchKernelGGL(embed_kernel, dim3(M, (nchunk + 255) / 256), dim3(256), 0, s, ids, C, emb_text, emb_audio,
+                     audio_rows, H, h, ss_out, ld_ss);
   return hipGetLastError();
 }
 

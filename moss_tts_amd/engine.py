@@ -114,6 +114,13 @@ class Engine:
                 continue
             self.load_weight(k, v)
 
+    def reserve(self, max_batch: int, max_ctx: int, max_prefill_tokens: int = 0):
+        """Grow batch / context capacity (KV cache, activations) without reloading weights."""
+        c = self.cfg
+        max_prefill_tokens = max(max_prefill_tokens, c.max_prefill_tokens)
+        N.check(N.load().mtts_engine_reserve(self._h, max_batch, max_ctx, max_prefill_tokens), "reserve")
+        c.max_batch, c.max_ctx, c.max_prefill_tokens = max_batch, max_ctx, max_prefill_tokens
+
     def init_random(self, seed: int = 0):
         N.check(N.load().mtts_engine_init_random(self._h, seed), "init_random")
 

@@ -110,7 +110,8 @@ def test_teacher_forced_logits(gpu, golden, name):
         got_audio = np.stack(parts[1:], 1)
         want_audio = tr.audio_logits[s]
         fin = np.isfinite(want_audio)
-        assert (np.isfinite(got_audio) == fin).all()
+        bad = np.argwhere(np.isfinite(got_audio) != fin)
+        assert bad.size == 0, (name, s, bad[:8].tolist(), [float(got_audio[tuple(i)]) for i in bad[:8]])
         scale = np.max(np.abs(np.where(fin, want_audio, 0)), axis=-1, keepdims=True)
         tol = 8 * ulp_bf16(np.broadcast_to(scale, want_audio.shape))
         assert (np.abs(got_audio - want_audio)[fin] <= tol[fin]).all(), (s, np.abs(got_audio - want_audio)[fin].max())

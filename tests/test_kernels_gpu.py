@@ -180,9 +180,9 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
     kn = B16.rnd(1 + 0.25 * rng.standard_normal(D).astype(np.float32))
     cfg = O.Cfg(head_dim=D, rope_theta=1e6)
     cos, sin = O.rope_cos_sin(ctx, cfg, np.arange(Cmax))
-    # existing cache rows 0..past-1
+    # existing cache rows 0..past-1 (K [B,Hkv,Cmax,D]; V stored transposed [B,Hkv,D,Cmax])
     kc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
-    vc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
+    vc0 = rand_bf16(rng, (B, Hkv, D, Cmax))
     kc, vc = dev_bf16(kc0), dev_bf16(vc0)
     qo = torch.zeros(M, Hq * D, dtype=torch.bfloat16, device="cuda")
     pos = torch.tensor([past], dtype=torch.int32, device="cuda")
@@ -198,7 +198,7 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
     k = O.apply_rope(ctx, k, cos[past:past + S], sin[past:past + S])
     gq = host(qo).reshape(B, S, Hq, D).transpose(0, 2, 1, 3)
     assert within_band(gq, q, 1.0).all() and np.mean(gq == q) > 0.98
-    kcg, vcg = host(kc), host(vc)
+    kcg, vcg = host(kc), host(vc).transpose(0, 1, 3, 2)
     assert within_band(kcg[:, :, past:past + S], k, 1.0).all()
     assert (vcg[:, :, past:past + S] == v).all()
     assert (kcg[:, :, :past] == kc0[:, :, :past]).all()
@@ -220,3 +220,44 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
         got = host(out).reshape(B, S, Hq, D).transpose(0, 2, 1, 3)
         err = np.abs(got - want)
         assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), (CH, err.max())
+
+
+@pytest.mark.parametrize("past,D,Hq,Hkv,B", [(10, 128, 32, 8, 1), (0, 16, 4, 2, 3), (300, 128, 8, 2, 2), (700, 64, 4, 1, 2)])
+def test_attn_decode_fused(N, past, D, Hq, Hkv, B):
+    """Fused decode step (norm + rope + append + attention) against the oracle ops."""
+    rng = np.random.default_rng(past + D)
+    ctx = O._Ctx("bf16")
+    Cmax = 1024
+    heads = Hq + 2 * Hkv
+    qkv = rand_bf16(rng, (B, heads * D), 2.0)
+    qn = B16.rnd(1 + 0.25 * rng.standard_normal(D).astype(np.float32))
+    kn = B16.rnd(1 + 0.25 * rng.standard_normal(D).astype(np.float32))
+    cos, sin = O.rope_cos_sin(ctx, O.Cfg(head_dim=D, rope_theta=1e6), np.arange(Cmax))
+    kc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
+    vt0 = rand_bf16(rng, (B, Hkv, D, Cmax))
+    kc, vc = dev_bf16(kc0), dev_bf16(vt0)
+    mask = np.ones((B, Cmax), np.uint8)
+    if B > 1:
+        mask[1, :5] = 0
+    md = torch.from_numpy(mask).cuda()
+    pos = torch.tensor([past], dtype=torch.int32, device="cuda")
+    out = torch.zeros(B, Hq * D, dtype=torch.bfloat16, device="cuda")
+    keep = [dev_bf16(a) for a in (qkv, qn, kn, cos, sin)]
+    N.call("mtts_k_attn_decode", P(keep[0]), P(keep[1]), P(keep[2]), P(keep[3]), P(keep[4]), P(kc), P(vc), P(md),
+           P(pos), P(out), B, Hq, Hkv, D, Cmax, ctypes.c_float(1e-6), None)
+    torch.cuda.synchronize()
+    x = qkv.reshape(B, 1, heads, D)
+    q = O.apply_rope(ctx, O.rmsnorm(ctx, x[:, :, :Hq], qn, 1e-6).transpose(0, 2, 1, 3), cos[past:past + 1], sin[past:past + 1])
+    k = O.apply_rope(ctx, O.rmsnorm(ctx, x[:, :, Hq:Hq + Hkv], kn, 1e-6).transpose(0, 2, 1, 3), cos[past:past + 1],
+                     sin[past:past + 1])
+    v = x[:, :, Hq + Hkv:].transpose(0, 2, 1, 3)
+    kcg, vcg = host(kc), host(vc).transpose(0, 1, 3, 2)
+    assert within_band(kcg[:, :, past:past + 1], k, 1.0).all()
+    assert (vcg[:, :, past:past + 1] == v).all()
+    assert (kcg[:, :, :past] == kc0[:, :, :past]).all()
+    K = kcg[:, :, :past + 1]
+    V = vcg[:, :, :past + 1]
+    want = O.attention(ctx, q, K, V, mask[:, :past + 1].astype(bool), np.array([past]), D ** -0.5)
+    got = host(out).reshape(B, 1, Hq, D).transpose(0, 2, 1, 3)
+    err = np.abs(got - want)
+    assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), err.max()
