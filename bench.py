@@ -143,6 +143,7 @@ def main():
     ap.add_argument("--decode-steps", type=int, default=208)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--extra-batches", default="4,32", help="extra per-GPU batch sizes reported in batch_sweep")
     args = ap.parse_args()
 
     import torch
@@ -156,80 +157,91 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from moss_tts_amd.engine import Engine, EngineConfig, sampling_params
+    from moss_tts_amd import _native as Nn
+    import ctypes
     n_steps = args.decode_steps
     gen_frames = n_steps - 35
-    cfgd = dict(n_vq=32)
-    rng = np.random.default_rng(1 + rank)
-    prompts = [synthetic_prompt(cfgd, rng) for _ in range(args.batch)]
-    T = max(p.shape[0] for p in prompts)
-    from moss_tts_amd.processing_moss_tts import left_pad
-    padded = left_pad([torch.from_numpy(p) for p in prompts], 151643, 1024)
-    ids, mask = padded["input_ids"].numpy(), padded["attention_mask"].numpy()
-    ecfg = EngineConfig(layers=args.layers, max_batch=max(args.batch, 1), max_ctx=T + n_steps + 16,
-                        max_prefill_tokens=max(T * args.batch, 256))
+    extra = [int(x) for x in args.extra_batches.split(",") if x] if args.extra_batches else []
+    max_b = max([args.batch] + extra)
+    ecfg = EngineConfig(layers=args.layers, max_batch=max_b, max_ctx=256 + n_steps + 16,
+                        max_prefill_tokens=max(256 * max_b, 256))
     eng = Engine(ecfg, local)
     eng.init_random(seed=0)
-    ids_d = torch.from_numpy(ids).cuda()
-    mask_d = torch.from_numpy(mask.astype(np.uint8)).cuda()
     forced = torch.from_numpy(forced_schedule(n_steps, 32, gen_frames)).cuda()
     sp = sampling_params(text_temperature=0, audio_temperature=0)
 
-    def one():
-        return eng.generate_ids(ids_d, mask_d, n_steps, sp, forced_text=forced, chunk=16)
+    def run_batch(B, steps, warmup, latency=False):
+        """steps x generate() of B utterances; returns (wall s max over ranks, audio s summed
+        over ranks, T, frames of row 0, text-head steps, prefill ms, p50 first-chunk ms)"""
+        rng = np.random.default_rng(1 + rank)
+        prompts = [synthetic_prompt(cfgd, rng) for _ in range(B)]
+        from moss_tts_amd.processing_moss_tts import left_pad
+        padded = left_pad([torch.from_numpy(p) for p in prompts], 151643, 1024)
+        ids, mask = padded["input_ids"].numpy(), padded["attention_mask"].numpy()
+        T = ids.shape[1]
+        ids_d = torch.from_numpy(ids).cuda()
+        mask_d = torch.from_numpy(mask.astype(np.uint8)).cuda()
 
-    for _ in range(args.warmup):
-        out = one()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = one()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
-    # frames actually produced (de-delayed, non-pad rows after the assistant start)
-    g = out.cpu().numpy()
-    start = T  # generation starts after the trailing "<|im_start|>assistant\n" (im_start + 3)
-    frames = [count_audio_frames(g[b], start, 32) for b in range(args.batch)]
-    audio_s = sum(frames) / FRAME_RATE * args.steps
-    t = torch.tensor([dt, audio_s], dtype=torch.float64, device="cuda")
-    if world > 1:
-        tmax = t.clone()
-        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
-        t[0] = tmax[0]
-    dt_max, audio_total = float(t[0]), float(t[1])
+        def one():
+            return eng.generate_ids(ids_d, mask_d, n_steps, sp, forced_text=forced, chunk=16)
 
-    # first-chunk latency: prefill + decode until the first 1 s of audio (13 frames) has all
-    # n_vq codebooks (frame f is complete n_vq steps after its first codebook), codec excluded
-    lat = []
-    from moss_tts_amd import _native as Nn
-    import ctypes
-    first_steps = 1 + 13 + 32
-    t_begin = []
-    for _ in range(3):  # prefill + step 0 alone
+        for _ in range(warmup):
+            out = one()
         torch.cuda.synchronize()
-        a = time.perf_counter()
-        Nn.check(Nn.load().mtts_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()),
-                                               ctypes.c_void_p(mask_d.data_ptr()), args.batch, T, n_steps,
-                                               ctypes.byref(sp), ctypes.c_void_p(forced.data_ptr()), None), "begin")
-        Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
-        t_begin.append((time.perf_counter() - a) * 1e3)
-    t_begin = float(np.median(t_begin))
-    for _ in range(5):
+        if world > 1:
+            dist.barrier()
         torch.cuda.synchronize()
-        a = time.perf_counter()
-        Nn.check(Nn.load().mtts_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()),
-                                               ctypes.c_void_p(mask_d.data_ptr()), args.batch, T, n_steps,
-                                               ctypes.byref(sp), ctypes.c_void_p(forced.data_ptr()), None), "begin")
-        Nn.check(Nn.load().mtts_generate_decode(eng._h, first_steps - 1, None), "decode")
-        Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
-        lat.append((time.perf_counter() - a) * 1e3)
-    p50 = float(np.median(lat))
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = one()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        th = ctypes.c_int()
+        Nn.check(Nn.load().mtts_generate_stats(eng._h, ctypes.byref(th)), "stats")
+        # frames actually produced (de-delayed, non-pad rows after the assistant start)
+        g = out.cpu().numpy()
+        frames = [count_audio_frames(g[b], T, 32) for b in range(B)]
+        audio_s = sum(frames) / FRAME_RATE * steps
+        t = torch.tensor([dt, audio_s], dtype=torch.float64, device="cuda")
+        if world > 1:
+            tmax = t.clone()
+            dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+            dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+            t[0] = tmax[0]
+        t_begin, p50 = None, None
+        if latency:
+            # first-chunk latency: prefill + decode until the first 1 s of audio (13 frames) has
+            # all n_vq codebooks (frame f is complete n_vq steps after its first codebook)
+            first_steps = 1 + 13 + 32
+            begin = lambda: Nn.check(Nn.load().mtts_generate_begin(
+                eng._h, ctypes.c_void_p(ids_d.data_ptr()), ctypes.c_void_p(mask_d.data_ptr()), B, T, n_steps,
+                ctypes.byref(sp), ctypes.c_void_p(forced.data_ptr()), None), "begin")
+            tb, lat = [], []
+            for _ in range(3):  # prefill + step 0 alone
+                torch.cuda.synchronize()
+                a = time.perf_counter()
+                begin()
+                Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
+                tb.append((time.perf_counter() - a) * 1e3)
+            for _ in range(5):
+                torch.cuda.synchronize()
+                a = time.perf_counter()
+                begin()
+                Nn.check(Nn.load().mtts_generate_decode(eng._h, first_steps - 1, None), "decode")
+                Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
+                lat.append((time.perf_counter() - a) * 1e3)
+            t_begin, p50 = float(np.median(tb)), float(np.median(lat))
+        return float(t[0]), float(t[1]), T, frames[0], th.value, t_begin, p50
+
+    cfgd = dict(n_vq=32)
+    dt_max, audio_total, T, frames0, text_steps, t_begin, p50 = run_batch(args.batch, args.steps, args.warmup, True)
+    sweep = {}
+    for B in extra:
+        d, a_s, _, _, _, _, _ = run_batch(B, 1, 1)
+        sweep[str(B)] = {"audio_s_per_s_per_gpu": round(a_s / d / world, 3), "ms_per_utt_batch": round(d * 1e3, 2)}
 
     res = None
     if rank == 0:
@@ -260,7 +272,7 @@ def main():
                        "batch_per_gpu": args.batch, "prompt_tokens": int(T), "decode_steps": n_steps,
                        "layers": args.layers, "parallelism": f"dp{world}", "sampling": "greedy, forced text schedule"},
             "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
-            "audio_frames_per_utt": frames[0],
+            "audio_frames_per_utt": frames0,
             "p50_first_chunk_ms": round(p50, 2),
             "first_chunk_def": "prefill + 46 decode steps (first 1 s of audio codes complete), codec excluded",
             "decode_weight_bytes": wb,
@@ -269,9 +281,21 @@ def main():
         step_ms = (per_utt_ms - t_begin) / (n_steps - 1)
         res["prefill_ms"] = round(t_begin, 3)
         res["ms_per_decode_step"] = round(step_ms, 4)
-        res["decode_step_hbm_frac"] = round(wb / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        # algorithmic HBM bytes of an average decode step: every weight that step's logits need
+        # (the text head rows below the special ids only on steps that sample text freely:
+        # text_head_steps of n_steps), plus the KV cache read (36 x 2 x 8 x 128 x 2 B per
+        # cached position and row) and the KV append
+        text_skip = (min(151645, 151656, 151662) // 16) * 16 * 4096 * 2
+        kv_pos = 36 * 2 * 8 * 128 * 2
+        mean_ctx = T + n_steps / 2
+        step_bytes = (wb - text_skip * (1 - text_steps / n_steps)) + kv_pos * args.batch * (mean_ctx + 1)
+        res["text_head_steps"] = text_steps
+        res["decode_alg_bytes_per_step"] = int(step_bytes)
+        res["decode_step_hbm_frac"] = round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if sweep:
+            res["batch_sweep"] = sweep
         if not args.no_cpu_baseline and world == 1:
-            res["cpu_baseline"] = cpu_baseline(args, int(T), n_steps, frames[0])
+            res["cpu_baseline"] = cpu_baseline(args, int(T), n_steps, frames0)
         elif not args.no_cpu_baseline:
             res["cpu_baseline"] = None
     eng.close()

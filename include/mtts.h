@@ -3,8 +3,11 @@
  * Drop-in boundary.  The Python package `moss_tts_amd` binds these
  * entry points with ctypes; any other host (cgo, JNI, N-API) can bind them the same
  * way.  No torch types cross this boundary: plain pointers, sizes
- * and a hipStream_t (passed as void*).  All `*_dev` pointers are device memory owned
- * by the caller; the engine owns weights, KV cache and workspaces.
+ * and a hipStream_t (passed as void*; NULL = the legacy default stream).  Engine calls
+ * run on the engine's own stream, fenced by events after the caller's stream and before
+ * its later work, so results are ordered like any other work on the caller's stream.
+ * All `*_dev` pointers are device memory owned by the caller; the engine owns weights,
+ * KV cache and workspaces.
  *
  * Errors: every function returns 0 on success or a negative MTTS_E_* code;
  * mtts_last_error() returns a thread-local message.  Threading: one engine = one
@@ -96,6 +99,10 @@ int mtts_generate_decode(mtts_engine* eng, int n_steps, void* stream);
 /* synchronises the stream; *steps = sampled steps so far, *done_step = step at which
  * every row had emitted im_end (-1 if none) */
 int mtts_generate_poll(mtts_engine* eng, int* steps, int* done_step, void* stream);
+/* accounting: decode steps (step 0 included) whose logits needed the full text head, i.e.
+ * some row sampled the text channel outside audio mode.  Other steps evaluate only the
+ * 16-row text tiles holding the special ids plus the audio heads. */
+int mtts_generate_stats(mtts_engine* eng, int* text_head_steps);
 /* whole loop: begin + decode in chunks until every row stopped or max_new_tokens;
  * *n_rows = generated rows per sequence (reference generation_ids width - T) */
 int mtts_generate(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int T,
@@ -113,8 +120,9 @@ size_t mtts_k_packed_bytes(int rows, int K);
 int mtts_k_gemv(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                 int ldres, int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, void* stream);
 /* as mtts_k_gemv plus the fused RMSNorm prologue (ss_in: per-16-column sums of squares of x,
- * norm_w: RMSNorm weight; NULL = off), the residual epilogue's sums of squares (ss_out) and a
- * waves-per-block override (0 = automatic, 4/8/16) */
+ * norm_w: RMSNorm weight; NULL = off; needs (min(B,32)+1)*K*2 <= 48 KiB, the normalised rows
+ * are staged in LDS), the residual epilogue's sums of squares (ss_out) and a waves-per-block
+ * override (0 = automatic, 4/8/16) */
 int mtts_k_gemv_ex(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                    int ldres, int B, int N, int K, int epi, const float* ss_in, int ld_ss, int n_ss,
                    const uint16_t* norm_w, float eps, float* ss_out, int ld_ss_out, int force_nw, void* stream);
@@ -133,10 +141,15 @@ int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, 
                      int D, int Cmax, int CH, int n_split, void* stream);
 /* fused decode step of one layer's attention: q/k RMSNorm + RoPE of the new token (qkv
  * [B, (Hq+2Hkv)*D]), k/v appended to the cache at *pos_dev, attention over keys 0..pos
- * under mask [B, Cmax]; out [B, Hq*D] */
+ * under mask [B, Cmax] (Cmax % 64 == 0), split over the context in 128-key blocks;
+ * out [B, Hq*D].  workspace_dev: mtts_k_attn_decode_ws_bytes() bytes, zero-filled before
+ * the first call (the kernel leaves its arrival counters at zero).
+ * Replaces Qwen3Attention.forward for q_len == 1 (TF/models/qwen3/modeling_qwen3.py:241-280). */
+size_t mtts_k_attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, const uint16_t* kn_w, const uint16_t* cos_t,
                        const uint16_t* sin_t, uint16_t* kc, uint16_t* vc, const uint8_t* mask, const int32_t* pos_dev,
-                       uint16_t* out, int B, int Hq, int Hkv, int D, int Cmax, float eps, void* stream);
+                       uint16_t* out, void* workspace_dev, int B, int Hq, int Hkv, int D, int Cmax, float eps,
+                       void* stream);
 /* RoPE table exactly as the engine builds it: bf16 cos/sin [n_pos, D] on the host */
 int mtts_rope_table(float theta, int D, int n_pos, uint16_t* cos_host, uint16_t* sin_host);
 int mtts_k_fill_uniform(uint16_t* dst, size_t n, uint64_t seed, uint64_t tensor_id, float scale, float offset,

@@ -55,6 +55,7 @@ _SIGS = {
     "mtts_heads_ld": (I, [P]),
     "mtts_generate_begin": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, P]),
     "mtts_generate_decode": (I, [P, I, P]),
+    "mtts_generate_stats": (I, [P, P]),
     "mtts_generate_poll": (I, [P, ctypes.POINTER(I), ctypes.POINTER(I), P]),
     "mtts_generate": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, I, ctypes.POINTER(I), P]),
     "mtts_generate_fetch": (I, [P, P, I, P]),
@@ -67,7 +68,8 @@ _SIGS = {
     "mtts_k_qk_norm_rope": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P]),
     "mtts_k_attention_ws_bytes": (SZ, [I, I, I, I]),
     "mtts_k_attention": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
-    "mtts_k_attn_decode": (I, [P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
+    "mtts_k_attn_decode_ws_bytes": (SZ, [I, I, I, I, I]),
+    "mtts_k_attn_decode": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
     "mtts_rope_table": (I, [F, I, I, P, P]),
     "mtts_k_fill_uniform": (I, [P, SZ, U64, U64, F, F, P]),
 }

@@ -7,8 +7,10 @@
 //   Qwen3Model.forward          transformers/models/qwen3/modeling_qwen3.py:367-427
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <unordered_map>
@@ -64,6 +66,9 @@ struct mtts_engine {
   size_t part_floats = 0;
   bf16_t* logits = nullptr;
   int* d_pos = nullptr;  // pos_base for teacher-forced forwards / prefill
+  int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
+  int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
+  bool full_text_head = false;  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};
@@ -78,6 +83,8 @@ struct mtts_engine {
   std::vector<void*> allocs;      // weights
   std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)
   bool cap_mode = false;
+  bool unfused_norm = false;  // MTTS_UNFUSED_NORM=1: always run the separate RMSNorm kernel (A/B timing)
+  int nw[5] = {0, 0, 0, 0, 0};  // waves-per-block overrides (MTTS_NW="qkv,o,gu,down,heads"; 0 = auto)
   bf16_t* staging = nullptr;
   size_t staging_bytes = 0;
   uint64_t step_weight_bytes = 0;
@@ -176,6 +183,8 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->part, e->part_floats))) return rc;
   if ((rc = e->alloc(&e->logits, (size_t)c.max_batch * e->heads_ld))) return rc;
   if ((rc = e->alloc(&e->d_pos, 4))) return rc;
+  if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv))) return rc;
+  if (hipMemset(e->att_cnt, 0, (size_t)c.max_batch * Hkv * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   // generate state
   const int B = c.max_batch;
   if ((rc = e->alloc(&e->st, 1)) || (rc = e->alloc(&e->is_stopping, B)) || (rc = e->alloc(&e->is_audio, B)) ||
@@ -192,7 +201,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (!cfg || !out) return fail(MTTS_E_INVALID, "null argument");
   const mtts_config& c = *cfg;
   if (c.hidden % 32 || c.inter % 32 || c.head_dim % 8 || c.head_dim > 128 || c.n_heads % c.n_kv ||
-      (c.n_heads * c.head_dim) % 32 || c.max_batch <= 0 || c.max_batch > 256 || c.max_ctx <= 0 || c.n_vq < 1)
+      (c.n_heads * c.head_dim) % 32 || c.max_batch <= 0 || c.max_batch > 256 || c.max_ctx <= 0 || c.max_ctx > 32768 || c.n_vq < 1)
     return fail(MTTS_E_UNSUPPORTED, "unsupported model shape");
   const int G = c.n_heads / c.n_kv;
   if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MTTS_E_UNSUPPORTED, "GQA group must be 1/2/4/8");
@@ -204,6 +213,9 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   e->c.max_ctx = (c.max_ctx + 63) / 64 * 64;  // 16-byte V^T fragments, whole 64-key chunks
   if (e->c.max_prefill_tokens <= 0) e->c.max_prefill_tokens = 8192;
   e->device = device;
+  if (const char* v = getenv("MTTS_UNFUSED_NORM")) e->unfused_norm = v[0] == '1';
+  if (const char* v = getenv("MTTS_FULL_TEXT_HEAD")) e->full_text_head = v[0] == '1';
+  if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
     return rc;
@@ -216,6 +228,8 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   e->audio_rows = c.audio_vocab + 1;
   e->heads_rows = c.vocab + c.n_vq * e->audio_rows;
   e->heads_ld = e->heads_rows;
+  e->text_tile_lo = std::min({c.im_end_token_id, c.audio_assistant_gen_slot_token_id,
+                              c.audio_assistant_delay_slot_token_id, c.vocab}) / 16;
   int rc = 0;
   e->L.resize(c.layers);
   uint64_t wb = 0;
@@ -245,7 +259,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
 }
 
 extern "C" int mtts_engine_reserve(mtts_engine* e, int max_batch, int max_ctx, int max_prefill_tokens) {
-  if (!e || max_batch <= 0 || max_batch > 256 || max_ctx <= 0) return fail(MTTS_E_INVALID, "bad capacity");
+  if (!e || max_batch <= 0 || max_batch > 256 || max_ctx <= 0 || max_ctx > 32768) return fail(MTTS_E_INVALID, "bad capacity");
   hipSetDevice(e->device);
   HIPCHK(hipStreamSynchronize(e->stream));
   for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second.exec);
@@ -402,14 +416,31 @@ extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
 }
 
 // ---------------------------------------------------------------------------
+// The GEMV `g` reads Qwen3RMSNorm(h) with weight `nw`.  Small decode batches fold the norm
+// into the GEMV prologue (normalised rows staged in LDS per block, no extra launch); larger
+// ones run the single-pass rmsnorm_ss kernel into e->xn first.  Both read the residual
+// stream's per-16-column sums of squares e->ss.
+static int normed_input(mtts_engine* e, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s) {
+  const int H = e->c.hidden, NT = H / 16;
+  if (norm_lds_bytes(M, H) <= NORM_LDS_MAX && !e->unfused_norm) {
+    g.x = e->h; g.ldx = H;
+    g.ss_in = e->ss; g.ld_ss = NT; g.n_ss = NT; g.nw = nw; g.eps = e->c.rms_eps;
+    return 0;
+  }
+  HIPCHK(rmsnorm_ss(e->h, 0, H, e->ss, 0, NT, nw, e->xn, M, H, e->c.rms_eps, s));
+  g.x = e->xn; g.ldx = H;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
 // forward over rows [b0, b0+B) with S tokens each; pos_base device pointer.
-// Per layer: input RMSNorm (single pass, from the residual epilogue's sums of squares) ->
-// q|k|v GEMV -> attention (decode: one fused kernel incl. q/k norm, RoPE, KV append;
+// Per layer: input RMSNorm (from the residual epilogue's sums of squares; fused into the
+// GEMV prologue for small batches) -> q|k|v GEMV -> attention (decode: one fused kernel incl. q/k norm, RoPE, KV append;
 // prefill: norm/rope/append + split-K attention + combine) -> o_proj GEMV (+residual,
-// +sums of squares) -> post-attention RMSNorm -> gate|up GEMV (SwiGLU epilogue) -> down
+// +sums of squares) -> post-attention RMSNorm (fused as above) -> gate|up GEMV (SwiGLU epilogue) -> down
 // GEMV (+residual, +sums of squares).
 static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
-                        int n_split, bf16_t* logits_out, hipStream_t s) {
+                        int n_split, bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr) {
   const mtts_config& c = e->c;
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter, C = c.n_vq + 1;
   const int M = B * S;
@@ -420,13 +451,15 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     const LayerW& w = e->L[l];
     bf16_t* kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
     bf16_t* vc = e->vc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
-    HIPCHK(rmsnorm_ss(e->h, 0, H, e->ss, 0, NT, w.in_norm, e->xn, M, H, eps, s));
     GemvArgs g = gemv_args(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, M, e->qkv_rows, H);
+    normed_input(e, g, w.in_norm, M, s);
+    g.force_nw = e->nw[0];
     HIPCHK(gemv_ex(g, EPI_STORE, s));
     if (S == 1) {
       DecAttnArgs da;
       da.qkv = e->qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = e->cos_t; da.sin_t = e->sin_t;
       da.kc = kc; da.vc = vc; da.mask = e->mask + (size_t)b0 * c.max_ctx; da.pos = pos_base; da.out = e->attnb;
+      da.part = e->part; da.cnt = e->att_cnt;
       da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = c.max_ctx; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
       HIPCHK(attn_decode(da, B, s));
     } else {
@@ -443,13 +476,14 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
       HIPCHK(attention(aa, s));
     }
     g = gemv_args(w.o, e->attnb, Hq * D, e->h, H, M, H, Hq * D);
-    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT;
+    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
     HIPCHK(gemv_ex(g, EPI_RESADD, s));
-    HIPCHK(rmsnorm_ss(e->h, 0, H, e->ss, 0, NT, w.post_norm, e->xn, M, H, eps, s));
     g = gemv_args(w.gu, e->xn, H, e->act, I, M, I, H);
+    normed_input(e, g, w.post_norm, M, s);
+    g.force_nw = e->nw[2];
     HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
     g = gemv_args(w.down, e->act, I, e->h, H, M, H, I);
-    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT;
+    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
     HIPCHK(gemv_ex(g, EPI_RESADD, s));
   }
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
@@ -457,6 +491,17 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
                     e->final_norm, e->xn, B, H, eps, s));
   GemvArgs g = gemv_args(e->heads, e->xn, H, logits_out, e->heads_ld, B, e->heads_rows, H);
   g.pad_start = c.vocab; g.pad_period = e->audio_rows; g.pad_off = e->audio_rows - 1;
+  g.force_nw = e->nw[4];
+  if (text_gate && e->text_tile_lo > 0) {
+    // decode: text rows below the special ids only when some row samples text freely.
+    // Audio-mode rows see every text logit except gen_slot / delay_slot masked to -inf
+    // (modeling_moss_tts.py:459-460), so those are the only text logits they need.
+    GemvArgs gt = g;
+    gt.N = e->text_tile_lo * 16;
+    gt.gate = text_gate;
+    HIPCHK(gemv_ex(gt, EPI_LOGITS, s));
+    g.tile0 = e->text_tile_lo;
+  }
   HIPCHK(gemv_ex(g, EPI_LOGITS, s));
   return 0;
 }
@@ -478,19 +523,19 @@ static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int
   return 0;
 }
 
+// The engine works on its own non-blocking stream, ordered after / before the caller's
+// stream by events.  A NULL caller stream is the legacy default stream (what torch's
+// default `cuda_stream` handle is), which a non-blocking stream does NOT synchronise with
+// implicitly, so it gets the same event fences.
 static hipStream_t enter(mtts_engine* e, void* user) {
   hipSetDevice(e->device);
-  if (user) {
-    hipEventRecord(e->ev_in, (hipStream_t)user);
-    hipStreamWaitEvent(e->stream, e->ev_in, 0);
-  }
+  hipEventRecord(e->ev_in, (hipStream_t)user);
+  hipStreamWaitEvent(e->stream, e->ev_in, 0);
   return e->stream;
 }
 static void leave(mtts_engine* e, void* user) {
-  if (user) {
-    hipEventRecord(e->ev_out, e->stream);
-    hipStreamWaitEvent((hipStream_t)user, e->ev_out, 0);
-  }
+  hipEventRecord(e->ev_out, e->stream);
+  hipStreamWaitEvent((hipStream_t)user, e->ev_out, 0);
 }
 
 extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
@@ -509,7 +554,8 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
 static int decode_step_launch(mtts_engine* e, hipStream_t s) {
   const int B = e->gen_B;
   const int n_split = (e->c.max_ctx + CH_DECODE - 1) / CH_DECODE;
-  int rc = forward_rows(e, e->cur_ids, 0, B, 1, &e->st->fwd_pos, CH_DECODE, n_split, e->logits, s);
+  int rc = forward_rows(e, e->cur_ids, 0, B, 1, &e->st->fwd_pos, CH_DECODE, n_split, e->logits, s,
+                        e->full_text_head ? nullptr : &e->st->need_text);
   if (rc) return rc;
   HIPCHK(sample_step(e->bufs(), B, e->c.n_vq, TEXT_PARTS, s));
   return 0;
@@ -597,6 +643,16 @@ extern "C" int mtts_generate_poll(mtts_engine* e, int* steps, int* done_step, vo
   if (steps) *steps = g.step;
   if (done_step) *done_step = g.done_step;
   (void)stream;
+  return 0;
+}
+
+extern "C" int mtts_generate_stats(mtts_engine* e, int* text_head_steps) {
+  if (!e || !text_head_steps) return fail(MTTS_E_INVALID, "null argument");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  GenDev g;
+  HIPCHK(hipMemcpy(&g, e->st, sizeof(g), hipMemcpyDeviceToHost));
+  *text_head_steps = g.text_head_steps;
   return 0;
 }
 
@@ -728,13 +784,19 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
   return 0;
 }
 
+extern "C" size_t mtts_k_attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax) {
+  return attn_decode_ws_bytes(B, Hq, Hkv, D, Cmax);
+}
 extern "C" int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, const uint16_t* kn_w, const uint16_t* cos_t,
                                   const uint16_t* sin_t, uint16_t* kc, uint16_t* vc, const uint8_t* mask,
-                                  const int32_t* pos, uint16_t* out, int B, int Hq, int Hkv, int D, int Cmax, float eps,
-                                  void* stream) {
+                                  const int32_t* pos, uint16_t* out, void* ws, int B, int Hq, int Hkv, int D, int Cmax,
+                                  float eps, void* stream) {
+  if (!ws) return fail(MTTS_E_INVALID, "workspace required");
   DecAttnArgs a;
   a.qkv = qkv; a.qn_w = qn_w; a.kn_w = kn_w; a.cos_t = cos_t; a.sin_t = sin_t; a.kc = kc; a.vc = vc; a.mask = mask;
   a.pos = pos; a.out = out; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.eps = eps;
+  a.cnt = reinterpret_cast<int*>(ws);
+  a.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + ((size_t)B * Hkv * sizeof(int) + 255) / 256 * 256);
   a.scale = 1.0f / std::sqrt((float)D);
   HIPCHK(attn_decode(a, B, (hipStream_t)stream));
   return 0;

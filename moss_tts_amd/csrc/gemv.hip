@@ -16,13 +16,19 @@
 // reduced through LDS in a fixed order (deterministic).  NW is picked per matrix so
 // that every CU holds enough waves (bytes in flight) even for 4096-row matrices.
 //
-// Fusions: the RMSNorm that precedes q|k|v, gate|up and the heads runs in the prologue
-// (x is normalised per fragment from per-tile sums of squares), and the op that follows
-// the matmul runs in the epilogue (residual add + its sums of squares, SwiGLU, the
-// audio-head pad column mask).
+// Fusions: for small decode batches (B <= 4 at K = 4096) the RMSNorm that precedes q|k|v
+// and gate|up runs in the prologue: the block stages the normalised rows in LDS once, from
+// the per-16-column sums of squares its producer wrote, while its first weight batch is
+// already in flight.  The op that follows the matmul runs in the epilogue (residual add +
+// its sums of squares, SwiGLU, the audio-head pad column mask).
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.h"
 
 namespace mtts {
+
+size_t norm_lds_bytes(int B, int K) { return (size_t)(B + 1) * K * 2; }
 
 // bf16(nw * bf16(x * r)) for 8 packed elements (Qwen3RMSNorm rounding points)
 __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
@@ -36,12 +42,15 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
   return o;
 }
 
-template <int NB, int RT, int EPI, bool NORM, int NW>
+template <int NB, int RT, int EPI, bool NORM, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
-  constexpr int U = 8;  // k-tiles in flight per wave
+  // k-tiles per load batch (one batch in flight per wave); the U4 variant (PIPE) trades
+  // bytes in flight per wave for more resident waves
+  constexpr int U = PIPE ? 4 : 8;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int bt = blockIdx.x;  // output row tile
+  if (a.gate && *a.gate == 0) return;
+  const int bt = blockIdx.x + a.tile0;  // output row tile
   const int KT = a.KT;
   const int per = (KT + NW - 1) / NW;
   const int kt0 = wave * per;
@@ -61,43 +70,38 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
   // B operand: x rows (b = lane&15 + 16 nb), 8 consecutive k at 8*(lane>>4)
   const u32x4* xbase[NB];
   bool xok[NB];
-  float rr[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int b = (lane & 15) + 16 * nb;
     xok[nb] = b < a.B;
     xbase[nb] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
-    rr[nb] = 0.f;
   }
-  const u32x4* nwbase = NORM ? reinterpret_cast<const u32x4*>(a.nw + (lane >> 4) * 8) : nullptr;
-
-  // all loads of the first k-batch (weights, x fragments, norm weights) go out before the
-  // latency-bound norm prologue, so that prologue overlaps the first HBM round trip
+  // all weight loads of the first k-batch go out before the (latency-bound) norm prologue
   int kt = kt0;
   u32x4 wa[RT][U];
   u32x4 xb[NB][U];
-  u32x4 wn[U];
-  auto issue = [&](int k) {
+  auto issue_w = [&](int k) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < RT; ++r) wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)(k + u) * 64);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        xb[nb][u] = xok[nb] ? xbase[nb][(k + u) * 4] : (u32x4){0u, 0u, 0u, 0u};
-    if constexpr (NORM) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) wn[u] = nwbase[(k + u) * 4];
-    }
   };
-  if (kt + U <= kt1) issue(kt);
+  if (kt + U <= kt1) issue_w(kt);
+
+  // NORM: the block stages bf16(nw * bf16(x * r_b)) for all its B rows in LDS once
+  // (r_b from the producer's per-16-column sums of squares); the MFMA B fragments are then
+  // LDS reads.  Without NORM the fragments come straight from x (L2).
+  extern __shared__ u32x4 xs_dyn[];
+  const int K8 = KT * 4;  // 16-byte chunks per row
   if constexpr (NORM) {
-    // r_b = rsqrt(mean(x_b^2) + eps) from the producer's per-16-column sums of squares:
-    // one coalesced float4 per lane per row, a wave reduction, lanes keep their own rows
-    const int nrow = min(a.B, 16 * NB);
-    for (int b = 0; b < nrow; ++b) {
+    __shared__ float r_s[32];
+    const int n8x = a.B * K8;
+    for (int i = threadIdx.x; i < n8x + K8; i += NW * 64) {
+      const int b = i / K8, c = i - b * K8;
+      xs_dyn[i] = i < n8x ? reinterpret_cast<const u32x4*>(a.x + (size_t)b * a.ldx)[c]
+                          : reinterpret_cast<const u32x4*>(a.nw)[c];
+    }
+    for (int b = wave; b < a.B; b += NW) {
       const float* sp = a.ss_in + (size_t)b * a.ld_ss;
       float ss = 0.f;
       for (int t4 = lane * 4; t4 < a.n_ss; t4 += 256) {
@@ -105,21 +109,26 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
         ss += (v.x + v.y) + (v.z + v.w);
       }
       ss = wave_sum(ss);
-      const float r = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        if ((lane & 15) + 16 * nb == b) rr[nb] = r;
+      if (lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n8x; i += NW * 64) {
+      const int b = i / K8;
+      xs_dyn[i] = norm8(xs_dyn[i], xs_dyn[n8x + i - b * K8], r_s[b]);
+    }
+    __syncthreads();
   }
+  auto load_x = [&](int k, int nb) -> u32x4 {
+    if (!xok[nb]) return (u32x4){0u, 0u, 0u, 0u};
+    if constexpr (NORM) return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
+    return xbase[nb][k * 4];
+  };
 
-  for (; kt + U <= kt1; kt += U) {
-    if (kt != kt0) issue(kt);
-    if constexpr (NORM) {
+  auto compute = [&](u32x4 (&w)[RT][U], int k) {
 #pragma unroll
-      for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u)
 #pragma unroll
-        for (int nb = 0; nb < NB; ++nb) xb[nb][u] = norm8(xb[nb][u], wn[u], rr[nb]);
-    }
+      for (int nb = 0; nb < NB; ++nb) xb[nb][u] = load_x(k + u, nb);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -127,15 +136,18 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
           acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, wa[r][u]), __builtin_bit_cast(bf16x8, xb[nb][u]), acc[r][nb], 0, 0, 0);
+              __builtin_bit_cast(bf16x8, w[r][u]), __builtin_bit_cast(bf16x8, xb[nb][u]), acc[r][nb], 0, 0, 0);
+  };
+  {
+    for (; kt + U <= kt1; kt += U) {
+      if (kt != kt0) issue_w(kt);
+      compute(wa, kt);
+    }
   }
   for (; kt < kt1; ++kt) {
     u32x4 xv[NB];
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      xv[nb] = xok[nb] ? xbase[nb][kt * 4] : (u32x4){0u, 0u, 0u, 0u};
-      if constexpr (NORM) xv[nb] = norm8(xv[nb], nwbase[kt * 4], rr[nb]);
-    }
+    for (int nb = 0; nb < NB; ++nb) xv[nb] = load_x(kt, nb);
 #pragma unroll
     for (int r = 0; r < RT; ++r) {
       const u32x4 wv = __builtin_nontemporal_load(wbase[r] + (size_t)kt * 64);
@@ -236,18 +248,19 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
-  if (a.force_nw == 4 || a.force_nw == 8 || a.force_nw == 16) {
-    if (a.force_nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4>), dim3(n_tiles), dim3(256), 0, s, a);
-    if (a.force_nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8>), dim3(n_tiles), dim3(512), 0, s, a);
-    if (a.force_nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16>), dim3(n_tiles), dim3(1024), 0, s, a);
+  const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : 0;
+  int nw = a.force_nw;
+  if (nw != 4 && nw != 8 && nw != 16) nw = a.KT < 64 ? 4 : ((rows >= 8192 || a.KT < 128) ? 8 : 16);
+  static const bool pipe = getenv("MTTS_GEMV_PIPE") && getenv("MTTS_GEMV_PIPE")[0] == '1';
+  if (NB == 1 && pipe) {
+    if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
+    if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8, true>), dim3(n_tiles), dim3(512), lds, s, a);
+    if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16, true>), dim3(n_tiles), dim3(1024), lds, s, a);
     return;
   }
-  if (a.KT < 64)
-    hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4>), dim3(n_tiles), dim3(256), 0, s, a);
-  else if (rows >= 8192 || a.KT < 128)
-    hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8>), dim3(n_tiles), dim3(512), 0, s, a);
-  else
-    hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16>), dim3(n_tiles), dim3(1024), 0, s, a);
+  if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4>), dim3(n_tiles), dim3(256), lds, s, a);
+  if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8>), dim3(n_tiles), dim3(512), lds, s, a);
+  if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16>), dim3(n_tiles), dim3(1024), lds, s, a);
 }
 
 template <int RT, int EPI>
@@ -260,6 +273,8 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
 
 hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   if (a0.K % 32 != 0 || a0.B <= 0 || a0.N <= 0) return hipErrorInvalidValue;
+  if (a0.ss_in && (a0.n_ss % 4 || a0.ld_ss % 4 || a0.ldx % 8 || norm_lds_bytes(std::min(a0.B, 32), a0.K) > NORM_LDS_MAX))
+    return hipErrorInvalidValue;
   for (int b0 = 0; b0 < a0.B; b0 += 32) {
     GemvArgs a = a0;
     a.x = a0.x + (size_t)b0 * a0.ldx;
@@ -270,7 +285,8 @@ hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
     a.B = min(32, a0.B - b0);
     a.KT = a0.K / 32;
     if (a.pad_period <= 0) a.pad_period = 1;
-    const int n_tiles = (a0.N + 15) / 16;
+    const int n_tiles = (a0.N + 15) / 16 - a0.tile0;
+    if (n_tiles <= 0) continue;
     switch (epi) {
       case EPI_STORE: launch_epi<1, EPI_STORE>(a, n_tiles, s); break;
       case EPI_LOGITS: launch_epi<1, EPI_LOGITS>(a, n_tiles, s); break;

@@ -32,6 +32,8 @@ struct GemvArgs {
   float* ss_out;       // [B, ld_ss_out] (nullptr: skip)
   int ld_ss_out;
   int force_nw;        // 0: automatic waves-per-block choice; 4/8/16: forced (tuning)
+  int tile0;           // first output row tile of this launch (row ranges of one matrix)
+  const int* gate;     // device flag: the launch does nothing when *gate == 0 (nullptr: always on)
 };
 
 inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {
@@ -83,8 +85,13 @@ struct DecAttnArgs {
   const uint8_t* mask;  // [Bmax][Cmax]
   const int* pos;       // device: absolute position of the new token
   bf16_t* out;          // [B, Hq * D]
+  float* part;          // split partials [B][Hkv][ns][G*(D+2)]
+  int* cnt;             // arrival tickets [B][Hkv], zero between launches
   int Hq, Hkv, D, Cmax;
+  int ns;               // splits per head (set by attn_decode)
+  int nwv;              // waves per block (32 keys each; set by attn_decode)
   float eps, scale;
+  int probe;            // timing probe (MTTS_ATTN_PROBE): 0 full; 1 exit after pos; 2 after loads + prologue; 3 no combine
 };
 
 struct GenDev {
@@ -93,6 +100,8 @@ struct GenDev {
   int step;        // time_step of the logits being sampled
   int fwd_pos;     // absolute position of the token fed to the next forward
   int done_step;   // first step at which every row had stopped, -1 if none yet
+  int need_text;   // some row samples the text channel freely at `step` (full text head needed)
+  int text_head_steps;  // decode steps that evaluated the full text head (accounting)
   int B, n_vq, C, Ltot, Cmax;
   int vocab, audio_rows;  // text vocab, 1025
   int heads_ld;           // row stride of the logits buffer
@@ -125,7 +134,10 @@ struct GenBufs {
 // gemv.hip
 hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int ldy, const bf16_t* res, int ldres,
                 int B, int N, int K, int epi, int pad_start, int pad_period, int pad_off, hipStream_t s);
-// full-control form (fused norm prologue / sum-of-squares epilogue); rows > 32 are chunked
+// full-control form (fused norm prologue / sum-of-squares epilogue); rows > 32 are chunked.
+// The fused norm stages the B normalised rows + the norm weight in LDS: (B+1)*K*2 bytes
+constexpr size_t NORM_LDS_MAX = 48 * 1024;
+size_t norm_lds_bytes(int B, int K);
 hipError_t gemv_ex(const GemvArgs& a, int epi, hipStream_t s);
 hipError_t pack_weight(const bf16_t* src, bf16_t* dst, int rows, int K, int row_offset, int interleave, int which,
                        hipStream_t s);
@@ -141,6 +153,9 @@ hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s);
 size_t attn_smem_bytes(int G, int D, int CH);
 hipError_t attention(const AttnArgs& a, hipStream_t s);
 hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s);
+int attn_decode_splits(int Cmax);
+// workspace of attn_decode: ticket counters (zero-filled once by the owner) + partials
+size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);

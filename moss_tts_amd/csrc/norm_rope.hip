@@ -5,36 +5,54 @@ namespace mtts {
 
 // ---------------------------------------------------------------------------
 // h[m, :] = E_text[ids[m,0]] + E_0[ids[m,1]] + ... + E_{n-1}[ids[m,n]], each add rounded to
-// bf16 left to right (moss_tts_delay/modeling_moss_tts.py:196-213).  One block per token.
-// Grid (M, H/2048): each thread owns one 8-wide chunk; it also emits the sum of squares of
-// every 16-column tile (pairs of chunks) for the fused RMSNorm of the first q|k|v GEMV.
+// bf16 left to right (moss_tts_delay/modeling_moss_tts.py:196-213).
+// Grid (M, H/256): a block gathers the C embedding slices of its 256 columns into LDS with
+// every 16-byte load in flight at once, then each thread sums one column in channel order.
+// It also emits the sum of squares of every 16-column tile for the next RMSNorm.
+constexpr int EMB_COLS = 256, EMB_MAXC = 64;
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int C, const bf16_t* __restrict__ emb_text,
                                                     const bf16_t* __restrict__ emb_audio, int audio_rows, int H,
                                                     bf16_t* __restrict__ h, float* __restrict__ ss_out, int ld_ss) {
-  const int m = blockIdx.x;
-  const int64_t* id = ids + (size_t)m * C;
-  const int nchunk = H >> 3;
-  const int c = blockIdx.y * 256 + threadIdx.x;
-  const bool ok = c < nchunk;
-  float e[8];
-  for (int i = 0; i < 8; ++i) e[i] = 0.f;
-  if (ok) {
-    unpack8(*reinterpret_cast<const uint4*>(emb_text + (size_t)id[0] * H + c * 8), e);
-    for (int j = 1; j < C; ++j) {
-      float a[8];
-      unpack8(*reinterpret_cast<const uint4*>(emb_audio + ((size_t)(j - 1) * audio_rows + id[j]) * H + c * 8), a);
+  constexpr int LPT = (EMB_MAXC * EMB_COLS / 8 + 255) / 256;  // 16-byte loads per thread (max)
+  __shared__ __attribute__((aligned(16))) bf16_t rows_s[EMB_MAXC][EMB_COLS];
+  __shared__ int64_t id_s[EMB_MAXC];
+  const int m = blockIdx.x, c0 = blockIdx.y * EMB_COLS, t = threadIdx.x;
+  if (t < C) id_s[t] = ids[(size_t)m * C + t];
+  __syncthreads();
+  const int ncols = min(EMB_COLS, H - c0);
+  const int cpr = ncols >> 3;
+  const int n = C * cpr;
+  uint4 v[LPT];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) e[i] = rbf(e[i] + a[i]);
+  for (int u = 0; u < LPT; ++u) {
+    const int i = t + u * 256;
+    if (i < n) {
+      const int j = i / cpr, cc = i - j * cpr;
+      const bf16_t* src = j == 0 ? emb_text + (size_t)id_s[0] * H : emb_audio + ((size_t)(j - 1) * audio_rows + id_s[j]) * H;
+      v[u] = *reinterpret_cast<const uint4*>(src + c0 + cc * 8);
     }
-    uint4 o;
-    o.x = pack2(e[0], e[1]); o.y = pack2(e[2], e[3]); o.z = pack2(e[4], e[5]); o.w = pack2(e[6], e[7]);
-    *reinterpret_cast<uint4*>(h + (size_t)m * H + c * 8) = o;
   }
-  float ss = 0.f;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) ss += e[i] * e[i];
+  for (int u = 0; u < LPT; ++u) {
+    const int i = t + u * 256;
+    if (i < n) {
+      const int j = i / cpr, cc = i - j * cpr;
+      *reinterpret_cast<uint4*>(&rows_s[j][cc * 8]) = v[u];
+    }
+  }
+  __syncthreads();
+  float e = 0.f;
+  if (t < ncols) {
+    e = bf2f(rows_s[0][t]);
+    for (int j = 1; j < C; ++j) e = rbf(e + bf2f(rows_s[j][t]));
+    h[(size_t)m * H + c0 + t] = f2bf(e);
+  }
+  float ss = e * e;
   ss += __shfl_xor(ss, 1, 64);
-  if (ss_out && ok && (c & 1) == 0) ss_out[(size_t)m * ld_ss + (c >> 1)] = ss;
+  ss += __shfl_xor(ss, 2, 64);
+  ss += __shfl_xor(ss, 4, 64);
+  ss += __shfl_xor(ss, 8, 64);
+  if (ss_out && t < ncols && (t & 15) == 0) ss_out[(size_t)m * ld_ss + ((c0 + t) >> 4)] = ss;
 }
 
 // ---------------------------------------------------------------------------
@@ -199,9 +217,8 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
 
 hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
                  bf16_t* h, int M, hipStream_t s, float* ss_out, int ld_ss) {
-  if (H % 16) return hipErrorInvalidValue;
-  const int nchunk = H / 8;
-  hipLaunchKernelGGL(embed_kernel, dim3(M, (nchunk + 255) / 256), dim3(256), 0, s, ids, C, emb_text, emb_audio,
+  if (H % 16 || C < 1 || C > EMB_MAXC) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(embed_kernel, dim3(M, (H + EMB_COLS - 1) / EMB_COLS), dim3(256), 0, s, ids, C, emb_text, emb_audio,
                      audio_rows, H, h, ss_out, ld_ss);
   return hipGetLastError();
 }

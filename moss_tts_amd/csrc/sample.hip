@@ -63,6 +63,7 @@ __device__ __forceinline__ float scaled(bf16_t v, float temp) { return rbf(bf2f(
 // top-K of one text vocab slice (special ids excluded), K = 1 when greedy
 __global__ __launch_bounds__(256) void text_partial_kernel(GenBufs g) {
   const GenDev& st = *g.st;
+  if (!st.need_text) return;  // every sampling row is in audio mode: partials unused
   const int b = blockIdx.x, p = blockIdx.y;
   const int K = st.text_sample ? min(st.text_top_k > 0 ? st.text_top_k : MAXK, MAXK) : 1;
   const int lo = p * st.part_len, hi = min(st.vocab, lo + st.part_len);
@@ -230,8 +231,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
   const MttsIds& d = st.ids;
   const int n_vq = st.n_vq;
   const int step = st.step;
-  __shared__ int n_stop;
-  if (threadIdx.x == 0) n_stop = 0;
+  __shared__ int n_stop, any_text;
+  if (threadIdx.x == 0) n_stop = any_text = 0;
   __syncthreads();
   for (int b = threadIdx.x; b < st.B; b += blockDim.x) {
     bool stop = g.is_stopping[b] != 0;
@@ -272,9 +273,13 @@ __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
     for (int c = 0; c < st.C; ++c) gr[c] = cur[c];
     g.mask[(size_t)b * st.Cmax + col] = stop ? 0 : 1;
     if (stop) atomicAdd(&n_stop, 1);
+    // next step samples this row's text channel over the full vocab (:453-471)
+    if (!stop && dl > n_vq && !isa) atomicOr(&any_text, 1);
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (st.need_text) st.text_head_steps += 1;
+    st.need_text = any_text;
     if (n_stop == st.B && st.done_step < 0) st.done_step = step;
     st.fwd_pos = st.T0 + step;
     st.step = step + 1;
@@ -318,6 +323,8 @@ __global__ __launch_bounds__(256) void gen_init_kernel(GenBufs g, const int64_t*
     st.step = 0;
     st.done_step = -1;
     st.fwd_pos = 0;
+    st.need_text = 1;  // step 0 samples from the prefill's full logits
+    st.text_head_steps = 0;
   }
 }
 

@@ -12,7 +12,7 @@ rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -5 gpurun_out/bench.
 if [ $rc -ne 0 ]; then exit $rc; fi
 if [ "${PROFILE:-1}" = "1" ]; then
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- \
-      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
+      python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --extra-batches "" > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
   rc=$?; echo "rocprof rc=$rc"; tail -3 gpurun_out/prof.err
   find gpurun_out/prof -name "*stats*" | head
 fi

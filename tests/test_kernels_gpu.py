@@ -112,6 +112,42 @@ def test_gemv_epilogues(N):
     assert fin.sum() == B * (Nr - 3)
 
 
+@pytest.mark.parametrize("B,Nr,K,epi", [(1, 4096, 4096, 0), (4, 6144, 4096, 0), (2, 512, 4096, 2), (5, 96, 1024, 0),
+                                        (3, 4100, 512, 0)])
+def test_gemv_fused_norm(N, B, Nr, K, epi):
+    """Qwen3RMSNorm folded into the GEMV prologue (small decode batches): y = linear(rmsnorm(x)),
+    r from per-16-column sums of squares as the residual epilogue writes them."""
+    rng = np.random.default_rng(B * 7 + Nr + K)
+    ctx = O._Ctx("bf16")
+    x = rand_bf16(rng, (B, K), 2.0)
+    nw = B16.rnd(1 + 0.25 * rng.standard_normal(K).astype(np.float32))
+    ss = (x.astype(np.float32) ** 2).reshape(B, K // 16, 16).sum(-1).astype(np.float32)
+    rows = 2 * Nr if epi == 2 else Nr
+    W = rand_bf16(rng, (rows, K), K ** -0.5)
+    packed = torch.zeros(N.load().mtts_k_packed_bytes(rows, K) // 2, dtype=torch.bfloat16, device="cuda")
+    wd = dev_bf16(W)
+    if epi == 2:
+        wg, wu = dev_bf16(W[:Nr]), dev_bf16(W[Nr:])
+        N.call("mtts_k_pack", P(wg), P(packed), Nr, K, 0, 1, 0, None)
+        N.call("mtts_k_pack", P(wu), P(packed), Nr, K, 0, 1, 1, None)
+    else:
+        N.call("mtts_k_pack", P(wd), P(packed), Nr, K, 0, 0, 0, None)
+    xd, nwd = dev_bf16(x), dev_bf16(nw)
+    ssd = torch.from_numpy(ss).cuda()
+    y = torch.zeros(B, Nr, dtype=torch.bfloat16, device="cuda")
+    N.call("mtts_k_gemv_ex", P(packed), P(xd), K, P(y), Nr, None, 0, B, Nr, K, epi, P(ssd), K // 16, K // 16,
+           P(nwd), ctypes.c_float(1e-6), None, 0, 0, None)
+    torch.cuda.synchronize()
+    xn = O.rmsnorm(ctx, x, nw, 1e-6)
+    if epi == 2:
+        want = ctx.r(ctx.r(O.silu(O.linear(ctx, xn, W[:Nr]))) * O.linear(ctx, xn, W[Nr:]))
+    else:
+        want = O.linear(ctx, xn, W)
+    got = host(y)
+    rowscale = np.abs(want).max(axis=1, keepdims=True)
+    assert within_band(got, want, 2.0, scale=np.maximum(np.abs(want), rowscale / 4)).all(), np.abs(got - want).max()
+
+
 @pytest.mark.parametrize("M,H", [(1, 64), (7, 4096), (3, 12288)])
 def test_rmsnorm(N, M, H):
     rng = np.random.default_rng(M + H)
@@ -127,10 +163,10 @@ def test_rmsnorm(N, M, H):
     assert np.mean(got == want) > 0.99
 
 
-def test_embed_exact(N):
-    cfg = O.tiny_cfg(n_vq=4)
-    rng = np.random.default_rng(1)
-    H = 64
+@pytest.mark.parametrize("H,n_vq", [(64, 4), (320, 32), (4096, 32)])
+def test_embed_exact(N, H, n_vq):
+    cfg = O.tiny_cfg(n_vq=n_vq)
+    rng = np.random.default_rng(H + n_vq)
     et = rand_bf16(rng, (cfg.vocab, H))
     ea = rand_bf16(rng, (cfg.n_vq, 1025, H))
     ids = np.concatenate([rng.integers(0, cfg.vocab, (6, 1)), rng.integers(0, 1025, (6, cfg.n_vq))], 1).astype(np.int64)
@@ -222,7 +258,9 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
         assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), (CH, err.max())
 
 
-@pytest.mark.parametrize("past,D,Hq,Hkv,B", [(10, 128, 32, 8, 1), (0, 16, 4, 2, 3), (300, 128, 8, 2, 2), (700, 64, 4, 1, 2)])
+@pytest.mark.parametrize("past,D,Hq,Hkv,B", [(10, 128, 32, 8, 1), (0, 16, 4, 2, 3), (300, 128, 8, 2, 2), (700, 64, 4, 1, 2),
+                                             (127, 128, 32, 8, 1), (128, 128, 32, 8, 2), (1023, 16, 8, 1, 1),
+                                             (389, 128, 32, 8, 4)])
 def test_attn_decode_fused(N, past, D, Hq, Hkv, B):
     """Fused decode step (norm + rope + append + attention) against the oracle ops."""
     rng = np.random.default_rng(past + D)
@@ -243,8 +281,9 @@ def test_attn_decode_fused(N, past, D, Hq, Hkv, B):
     pos = torch.tensor([past], dtype=torch.int32, device="cuda")
     out = torch.zeros(B, Hq * D, dtype=torch.bfloat16, device="cuda")
     keep = [dev_bf16(a) for a in (qkv, qn, kn, cos, sin)]
+    ws = torch.zeros(N.load().mtts_k_attn_decode_ws_bytes(B, Hq, Hkv, D, Cmax), dtype=torch.uint8, device="cuda")
     N.call("mtts_k_attn_decode", P(keep[0]), P(keep[1]), P(keep[2]), P(keep[3]), P(keep[4]), P(kc), P(vc), P(md),
-           P(pos), P(out), B, Hq, Hkv, D, Cmax, ctypes.c_float(1e-6), None)
+           P(pos), P(out), P(ws), B, Hq, Hkv, D, Cmax, ctypes.c_float(1e-6), None)
     torch.cuda.synchronize()
     x = qkv.reshape(B, 1, heads, D)
     q = O.apply_rope(ctx, O.rmsnorm(ctx, x[:, :, :Hq], qn, 1e-6).transpose(0, 2, 1, 3), cos[past:past + 1], sin[past:past + 1])
