@@ -126,6 +126,10 @@ int mtts_k_gemv(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y
 int mtts_k_gemv_ex(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                    int ldres, int B, int N, int K, int epi, const float* ss_in, int ld_ss, int n_ss,
                    const uint16_t* norm_w, float eps, float* ss_out, int ld_ss_out, int force_nw, void* stream);
+/* prefill form: y[M,N] = epi(x[M,K] . W^T) for any token count M (epi 0 store, 1 residual
+ * add + per-16-column sums of squares into ss_out when non-NULL, 2 swiglu) */
+int mtts_k_gemm(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                int ldres, int M, int N, int K, int epi, float* ss_out, int ld_ss_out, void* stream);
 int mtts_k_rmsnorm(const uint16_t* x, size_t x_off, size_t x_stride, const uint16_t* w, uint16_t* y, int M, int H,
                    float eps, void* stream);
 int mtts_k_embed(const int64_t* ids, int C, const uint16_t* emb_text, const uint16_t* emb_audio, int audio_rows,

@@ -68,7 +68,8 @@ struct mtts_engine {
   int* d_pos = nullptr;  // pos_base for teacher-forced forwards / prefill
   int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
   int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
-  bool full_text_head = false;  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
+  bool full_text_head = false;
+  bool gemv_prefill = false;    // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};
@@ -215,6 +216,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   e->device = device;
   if (const char* v = getenv("MTTS_UNFUSED_NORM")) e->unfused_norm = v[0] == '1';
   if (const char* v = getenv("MTTS_FULL_TEXT_HEAD")) e->full_text_head = v[0] == '1';
+  if (const char* v = getenv("MTTS_GEMV_PREFILL")) e->gemv_prefill = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -439,6 +441,14 @@ static int normed_input(mtts_engine* e, GemvArgs& g, const bf16_t* nw, int M, hi
 // prefill: norm/rope/append + split-K attention + combine) -> o_proj GEMV (+residual,
 // +sums of squares) -> post-attention RMSNorm (fused as above) -> gate|up GEMV (SwiGLU epilogue) -> down
 // GEMV (+residual, +sums of squares).
+// token-parallel projections: the decode GEMV for a handful of rows, the prefill GEMM
+// (weights read once per 256 tokens instead of once per 32) beyond that
+constexpr int GEMM_MIN_ROWS = 33;
+static hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
+  if (g.B >= GEMM_MIN_ROWS && !g.ss_in && !e->gemv_prefill) return gemm_ex(g, epi, s);
+  return gemv_ex(g, epi, s);
+}
+
 static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
                         int n_split, bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr) {
   const mtts_config& c = e->c;
@@ -454,7 +464,7 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     GemvArgs g = gemv_args(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, M, e->qkv_rows, H);
     normed_input(e, g, w.in_norm, M, s);
     g.force_nw = e->nw[0];
-    HIPCHK(gemv_ex(g, EPI_STORE, s));
+    HIPCHK(proj(e, g, EPI_STORE, s));
     if (S == 1) {
       DecAttnArgs da;
       da.qkv = e->qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = e->cos_t; da.sin_t = e->sin_t;
@@ -477,14 +487,14 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     }
     g = gemv_args(w.o, e->attnb, Hq * D, e->h, H, M, H, Hq * D);
     g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
-    HIPCHK(gemv_ex(g, EPI_RESADD, s));
+    HIPCHK(proj(e, g, EPI_RESADD, s));
     g = gemv_args(w.gu, e->xn, H, e->act, I, M, I, H);
     normed_input(e, g, w.post_norm, M, s);
     g.force_nw = e->nw[2];
-    HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
+    HIPCHK(proj(e, g, EPI_SWIGLU, s));
     g = gemv_args(w.down, e->act, I, e->h, H, M, H, I);
     g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
-    HIPCHK(gemv_ex(g, EPI_RESADD, s));
+    HIPCHK(proj(e, g, EPI_RESADD, s));
   }
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
   HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
@@ -799,6 +809,16 @@ extern "C" int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, con
   a.part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + ((size_t)B * Hkv * sizeof(int) + 255) / 256 * 256);
   a.scale = 1.0f / std::sqrt((float)D);
   HIPCHK(attn_decode(a, B, (hipStream_t)stream));
+  return 0;
+}
+
+extern "C" int mtts_k_gemm(const uint16_t* w, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                           int ldres, int M, int N, int K, int epi, float* ss_out, int ld_ss_out, void* stream) {
+  if (K % 32) return fail(MTTS_E_INVALID, "K must be a multiple of 32");
+  if (epi != EPI_STORE && epi != EPI_RESADD && epi != EPI_SWIGLU) return fail(MTTS_E_INVALID, "epi 0/1/2 only");
+  GemvArgs a = gemv_args(w, x, ldx, y, ldy, M, N, K);
+  a.res = res; a.ldres = ldres; a.ss_out = ss_out; a.ld_ss_out = ld_ss_out;
+  HIPCHK(gemm_ex(a, epi, (hipStream_t)stream));
   return 0;
 }
 

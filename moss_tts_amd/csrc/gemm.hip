@@ -1,0 +1,271 @@
+// Prefill GEMM: y[M,N] = epi(x[M,K] . W[N,K]^T) for M = rows x prompt tokens.
+//
+// Same weights, same MFMA-tile packed layout and same epilogues as the decode GEMV
+// (gemv.hip), for the prompt's projections (TF/models/qwen3/modeling_qwen3.py:241-280
+// q/k/v/o_proj, :81-83 gate/up/down_proj).  The GEMV streams every weight tile once per
+// 32 tokens; here a block holds RT weight tiles (16*RT output columns) against up to
+// 4 * NBW * 16 tokens, so a 181-token prompt reads each weight byte once from HBM.
+//
+// Block = 4 waves; wave w owns token tiles [tb0 + w*NBW, +NBW) and runs the whole K loop
+// for them (no cross-wave reduction): per 32-deep k-step it loads the RT weight tiles (one
+// 1 KiB wave-load each, A operands; the 4 waves of a block share them through L1/L2) and
+// its NBW activation fragments (B operands), then issues RT x NBW
+// v_mfma_f32_16x16x32_bf16.  The epilogue runs from registers: lane holds 4 consecutive
+// output columns of one token (MFMA C layout), so stores are 8-byte row segments.
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace mtts {
+
+template <int RT, int NBW, int EPI>
+__global__ __launch_bounds__(256) void gemm_kernel(GemvArgs a) {
+  constexpr int U = 4;  // k-tiles in flight per wave
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int bt = blockIdx.x;                            // output tile (pair for SwiGLU)
+  const int tt0 = (blockIdx.y * 4 + wave) * NBW;        // first token tile of this wave
+  if (tt0 * 16 >= a.B) return;
+  const int KT = a.KT;
+  const int g4 = lane >> 4, c16 = lane & 15;
+
+  f32x4 acc[RT][NBW];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int j = 0; j < NBW; ++j) acc[r][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const u32x4* wbase[RT];
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+    wbase[r] = reinterpret_cast<const u32x4*>(a.w) + ((size_t)(bt * RT + r) * KT) * 64 + lane;
+  const u32x4* xbase[NBW];
+  bool xok[NBW];
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    const int m = (tt0 + j) * 16 + c16;
+    xok[j] = m < a.B;
+    xbase[j] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[j] ? m : 0) * a.ldx + g4 * 8);
+  }
+
+  int kt = 0;
+  for (; kt + U <= KT; kt += U) {
+    u32x4 wa[RT][U], xb[NBW][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int r = 0; r < RT; ++r) wa[r][u] = wbase[r][(size_t)(kt + u) * 64];
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) xb[j][u] = xok[j] ? xbase[j][(kt + u) * 4] : (u32x4){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < RT; ++r)
+#pragma unroll
+        for (int j = 0; j < NBW; ++j)
+          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[r][u]),
+                                                             __builtin_bit_cast(bf16x8, xb[j][u]), acc[r][j], 0, 0, 0);
+  }
+  for (; kt < KT; ++kt) {
+#pragma unroll
+    for (int r = 0; r < RT; ++r) {
+      const u32x4 wv = wbase[r][(size_t)kt * 64];
+#pragma unroll
+      for (int j = 0; j < NBW; ++j) {
+        const u32x4 xv = xok[j] ? xbase[j][kt * 4] : (u32x4){0u, 0u, 0u, 0u};
+        acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wv),
+                                                           __builtin_bit_cast(bf16x8, xv), acc[r][j], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: lane -> token m = tile*16 + c16, columns n0 .. n0+3 ----
+  const int n0 = bt * 16 + g4 * 4;
+#pragma unroll
+  for (int j = 0; j < NBW; ++j) {
+    const int m = (tt0 + j) * 16 + c16;
+    const bool mok = m < a.B;
+    float o[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = n0 + i;
+      if constexpr (EPI == EPI_STORE) {
+        o[i] = rbf(acc[0][j][i]);
+      } else if constexpr (EPI == EPI_RESADD) {
+        // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
+        o[i] = (mok && n < a.N) ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(acc[0][j][i])) : 0.f;
+      } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
+        const float g = rbf(acc[0][j][i]);
+        const float u = rbf(acc[RT - 1][j][i]);
+        o[i] = rbf(rbf(g / (1.0f + expf(-g))) * u);
+      }
+    }
+    if (mok) {
+      bf16_t* yr = a.y + (size_t)m * a.ldy;
+      if (n0 + 3 < a.N && (a.ldy % 4) == 0) {
+        uint2 pk;
+        pk.x = pack2(o[0], o[1]);
+        pk.y = pack2(o[2], o[3]);
+        *reinterpret_cast<uint2*>(yr + n0) = pk;
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (n0 + i < a.N) yr[n0 + i] = f2bf(o[i]);
+      }
+    }
+    if constexpr (EPI == EPI_RESADD) {
+      // sum of squares of this token's 16 new columns (for the next RMSNorm)
+      float ss = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+      ss += __shfl_xor(ss, 16, 64);
+      ss += __shfl_xor(ss, 32, 64);
+      if (a.ss_out && mok && g4 == 0) a.ss_out[(size_t)m * a.ld_ss_out + bt] = ss;
+    }
+  }
+}
+
+// Large-M form: 2 x 2 waves, each a WR x WN grid of 16 x 16 MFMA tiles (WR weight row tiles
+// x WN token tiles), so a 256-thread block covers 32*WR rows x 32*WN tokens and every
+// 16-byte fragment a wave loads feeds WN (weights) or WR (activations) MFMAs.  The two
+// waves that share a weight (or token) stripe read it through the CU's L1.  SwiGLU takes
+// WR/2 gate|up tile pairs per wave.
+template <int WR, int WN, int EPI>
+__global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
+  constexpr int U = 2;  // k-tiles in flight per wave
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave & 1, wm = wave >> 1;
+  const int rt0 = (blockIdx.x * 2 + wr) * WR;  // first packed row tile of this wave
+  const int tt0 = (blockIdx.y * 2 + wm) * WN;  // first token tile of this wave
+  const int KT = a.KT;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int n_rt = a.n_row_tiles;
+  if (tt0 * 16 >= a.B || rt0 >= n_rt) return;
+
+  f32x4 acc[WR][WN];
+#pragma unroll
+  for (int r = 0; r < WR; ++r)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[r][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const u32x4* wbase[WR];
+#pragma unroll
+  for (int r = 0; r < WR; ++r)
+    wbase[r] = reinterpret_cast<const u32x4*>(a.w) + ((size_t)min(rt0 + r, n_rt - 1) * KT) * 64 + lane;
+  const u32x4* xbase[WN];
+  bool xok[WN];
+#pragma unroll
+  for (int j = 0; j < WN; ++j) {
+    const int m = (tt0 + j) * 16 + c16;
+    xok[j] = m < a.B;
+    xbase[j] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[j] ? m : 0) * a.ldx + g4 * 8);
+  }
+  for (int kt = 0; kt < KT; kt += U) {  // KT % U == 0 (K % 64 == 0 checked by the launcher)
+    u32x4 wa[WR][U], xb[WN][U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int r = 0; r < WR; ++r) wa[r][u] = wbase[r][(size_t)(kt + u) * 64];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) xb[j][u] = xok[j] ? xbase[j][(kt + u) * 4] : (u32x4){0u, 0u, 0u, 0u};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int r = 0; r < WR; ++r)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[r][u]),
+                                                             __builtin_bit_cast(bf16x8, xb[j][u]), acc[r][j], 0, 0, 0);
+  }
+  constexpr int OT = EPI == EPI_SWIGLU ? WR / 2 : WR;  // output column tiles per wave
+#pragma unroll
+  for (int q = 0; q < OT; ++q) {
+    const int ot = EPI == EPI_SWIGLU ? rt0 / 2 + q : rt0 + q;  // output 16-column tile
+    const int n0 = ot * 16 + g4 * 4;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int m = (tt0 + j) * 16 + c16;
+      const bool mok = m < a.B && n0 < a.N;
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + i;
+        if constexpr (EPI == EPI_STORE) {
+          o[i] = rbf(acc[q][j][i]);
+        } else if constexpr (EPI == EPI_RESADD) {
+          o[i] = (mok && n < a.N) ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(acc[q][j][i])) : 0.f;
+        } else {
+          const float g = rbf(acc[2 * q][j][i]);
+          const float u = rbf(acc[2 * q + 1][j][i]);
+          o[i] = rbf(rbf(g / (1.0f + expf(-g))) * u);
+        }
+      }
+      if (mok) {
+        bf16_t* yr = a.y + (size_t)m * a.ldy;
+        if (n0 + 3 < a.N && (a.ldy % 4) == 0) {
+          uint2 pk;
+          pk.x = pack2(o[0], o[1]);
+          pk.y = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(yr + n0) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n0 + i < a.N) yr[n0 + i] = f2bf(o[i]);
+        }
+      }
+      if constexpr (EPI == EPI_RESADD) {
+        float ss = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (a.ss_out && mok && g4 == 0) a.ss_out[(size_t)m * a.ld_ss_out + ot] = ss;
+      }
+    }
+  }
+}
+
+template <int RT, int EPI>
+static void gemm_launch(const GemvArgs& a, int n_tiles, hipStream_t s) {
+  const int mt = (a.B + 15) / 16;  // token tiles
+  const int nbw = mt >= 16 ? 4 : (mt + 3) / 4;  // tiles per wave: one block covers short prompts
+  const dim3 grid(n_tiles, (mt + 4 * nbw - 1) / (4 * nbw));
+  switch (nbw) {
+    case 1: hipLaunchKernelGGL((gemm_kernel<RT, 1, EPI>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((gemm_kernel<RT, 2, EPI>), grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((gemm_kernel<RT, 3, EPI>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((gemm_kernel<RT, 4, EPI>), grid, dim3(256), 0, s, a); break;
+  }
+}
+
+template <int WR, int WN, int EPI>
+static void gemm2_launch(GemvArgs a, hipStream_t s) {
+  a.n_row_tiles = (EPI == EPI_SWIGLU ? 2 : 1) * ((a.N + 15) / 16);
+  const int mt = (a.B + 15) / 16;
+  const dim3 grid((a.n_row_tiles + 2 * WR - 1) / (2 * WR), (mt + 2 * WN - 1) / (2 * WN));
+  hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI>), grid, dim3(256), 0, s, a);
+}
+
+hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
+  if (a0.K % 32 != 0 || a0.B <= 0 || a0.N <= 0 || a0.ss_in || a0.gate || a0.tile0) return hipErrorInvalidValue;
+  GemvArgs a = a0;
+  a.KT = a0.K / 32;
+  const int n_tiles = (a0.N + 15) / 16;
+  static const int big = getenv("MTTS_GEMM_SMALL") && getenv("MTTS_GEMM_SMALL")[0] == '1' ? 1 << 30 : 128;
+  if (a.B >= big && a.K % 64 == 0) {  // 128 x 128 block tiles
+    switch (epi) {
+      case EPI_STORE: gemm2_launch<4, 4, EPI_STORE>(a, s); break;
+      case EPI_RESADD: gemm2_launch<4, 4, EPI_RESADD>(a, s); break;
+      case EPI_SWIGLU: gemm2_launch<4, 4, EPI_SWIGLU>(a, s); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  switch (epi) {
+    case EPI_STORE: gemm_launch<1, EPI_STORE>(a, n_tiles, s); break;
+    case EPI_RESADD: gemm_launch<1, EPI_RESADD>(a, n_tiles, s); break;
+    case EPI_SWIGLU: gemm_launch<2, EPI_SWIGLU>(a, n_tiles, s); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mtts

@@ -34,6 +34,7 @@ struct GemvArgs {
   int force_nw;        // 0: automatic waves-per-block choice; 4/8/16: forced (tuning)
   int tile0;           // first output row tile of this launch (row ranges of one matrix)
   const int* gate;     // device flag: the launch does nothing when *gate == 0 (nullptr: always on)
+  int n_row_tiles;     // packed 16-row weight tiles (set by the GEMM launcher)
 };
 
 inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {
@@ -139,6 +140,9 @@ hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int 
 constexpr size_t NORM_LDS_MAX = 48 * 1024;
 size_t norm_lds_bytes(int B, int K);
 hipError_t gemv_ex(const GemvArgs& a, int epi, hipStream_t s);
+// gemm.hip: prefill form of gemv_ex (B = tokens, any count; EPI_STORE / RESADD / SWIGLU;
+// no fused norm prologue, no gate)
+hipError_t gemm_ex(const GemvArgs& a, int epi, hipStream_t s);
 hipError_t pack_weight(const bf16_t* src, bf16_t* dst, int rows, int K, int row_offset, int interleave, int which,
                        hipStream_t s);
 // norm_rope.hip

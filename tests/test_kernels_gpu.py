@@ -148,6 +148,47 @@ def test_gemv_fused_norm(N, B, Nr, K, epi):
     assert within_band(got, want, 2.0, scale=np.maximum(np.abs(want), rowscale / 4)).all(), np.abs(got - want).max()
 
 
+@pytest.mark.parametrize("M,Nr,K,epi", [(181, 4100, 512, 0), (33, 96, 4096, 0), (300, 512, 256, 1), (181, 384, 1024, 2),
+                                        (1000, 64, 128, 1)])
+def test_gemm_prefill(N, M, Nr, K, epi):
+    """Prefill GEMM (any token count) against the oracle linear + epilogues, including the
+    residual epilogue's per-16-column sums of squares."""
+    rng = np.random.default_rng(M + Nr + K + epi)
+    ctx = O._Ctx("bf16")
+    x = rand_bf16(rng, (M, K))
+    rows = 2 * Nr if epi == 2 else Nr
+    W = rand_bf16(rng, (rows, K), K ** -0.5)
+    packed = torch.zeros(N.load().mtts_k_packed_bytes(rows, K) // 2, dtype=torch.bfloat16, device="cuda")
+    keep = [dev_bf16(W[:Nr]), dev_bf16(W[Nr:]) if epi == 2 else None]
+    if epi == 2:
+        N.call("mtts_k_pack", P(keep[0]), P(packed), Nr, K, 0, 1, 0, None)
+        N.call("mtts_k_pack", P(keep[1]), P(packed), Nr, K, 0, 1, 1, None)
+    else:
+        N.call("mtts_k_pack", P(keep[0]), P(packed), Nr, K, 0, 0, 0, None)
+    xd = dev_bf16(x)
+    res = rand_bf16(rng, (M, Nr))
+    y = dev_bf16(res) if epi == 1 else torch.zeros(M, Nr, dtype=torch.bfloat16, device="cuda")
+    nt = (Nr + 15) // 16
+    ss = torch.zeros(M, nt, dtype=torch.float32, device="cuda")
+    N.call("mtts_k_gemm", P(packed), P(xd), K, P(y), Nr, P(y) if epi == 1 else None, Nr, M, Nr, K, epi,
+           P(ss) if epi == 1 else None, nt, None)
+    torch.cuda.synchronize()
+    lin = O.linear(ctx, x, W[:Nr])
+    if epi == 0:
+        want = lin
+    elif epi == 1:
+        want = ctx.r(res + lin)
+    else:
+        want = ctx.r(ctx.r(O.silu(lin)) * O.linear(ctx, x, W[Nr:]))
+    got = host(y)
+    rowscale = np.abs(want).max(axis=1, keepdims=True)
+    assert within_band(got, want, 2.0, scale=np.maximum(np.abs(want), rowscale / 4)).all(), np.abs(got - want).max()
+    if epi == 1:
+        g2 = np.pad(got, ((0, 0), (0, nt * 16 - Nr))).reshape(M, nt, 16)
+        want_ss = (g2.astype(np.float64) ** 2).sum(-1)
+        assert np.allclose(ss.cpu().numpy(), want_ss, rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("M,H", [(1, 64), (7, 4096), (3, 12288)])
 def test_rmsnorm(N, M, H):
     rng = np.random.default_rng(M + H)
