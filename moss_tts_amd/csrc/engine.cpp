@@ -462,7 +462,7 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     bf16_t* kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
     bf16_t* vc = e->vc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
     GemvArgs g = gemv_args(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, M, e->qkv_rows, H);
-    normed_input(e, g, w.in_norm, M, s);
+    if (int rc = normed_input(e, g, w.in_norm, M, s)) return rc;
     g.force_nw = e->nw[0];
     HIPCHK(proj(e, g, EPI_STORE, s));
     if (S == 1) {
@@ -489,7 +489,7 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
     HIPCHK(proj(e, g, EPI_RESADD, s));
     g = gemv_args(w.gu, e->xn, H, e->act, I, M, I, H);
-    normed_input(e, g, w.post_norm, M, s);
+    if (int rc = normed_input(e, g, w.post_norm, M, s)) return rc;
     g.force_nw = e->nw[2];
     HIPCHK(proj(e, g, EPI_SWIGLU, s));
     g = gemv_args(w.down, e->act, I, e->h, H, M, H, I);
@@ -497,9 +497,13 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     HIPCHK(proj(e, g, EPI_RESADD, s));
   }
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
-  HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
-                    e->final_norm, e->xn, B, H, eps, s));
   GemvArgs g = gemv_args(e->heads, e->xn, H, logits_out, e->heads_ld, B, e->heads_rows, H);
+  if (S == 1) {
+    if (int rc = normed_input(e, g, e->final_norm, B, s)) return rc;
+  } else {
+    HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
+                      e->final_norm, e->xn, B, H, eps, s));
+  }
   g.pad_start = c.vocab; g.pad_period = e->audio_rows; g.pad_off = e->audio_rows - 1;
   g.force_nw = e->nw[4];
   if (text_gate && e->text_tile_lo > 0) {

@@ -44,8 +44,8 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
 
 template <int NB, int RT, int EPI, bool NORM, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
-  // k-tiles per load batch (one batch in flight per wave); the U4 variant (PIPE) trades
-  // bytes in flight per wave for more resident waves
+  // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
+  // bytes in flight per wave for more resident waves (the default for 17-32 rows)
   constexpr int U = PIPE ? 4 : 8;
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -249,10 +249,15 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
   const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : 0;
+  // 17-32 rows (NB = 2): 4 waves of 4-deep batches (in-context B=32 sweep: 5.62 vs 6.03 ms/step)
   int nw = a.force_nw;
-  if (nw != 4 && nw != 8 && nw != 16) nw = a.KT < 64 ? 4 : ((rows >= 8192 || a.KT < 128) ? 8 : 16);
-  static const bool pipe = getenv("MTTS_GEMV_PIPE") && getenv("MTTS_GEMV_PIPE")[0] == '1';
-  if (NB == 1 && pipe) {
+  // fused-norm launches stage (B+1)*K*2 bytes of LDS per block: 8 waves keep 2 blocks per CU
+  // (q|k|v: 3.46 vs 3.53 ms/step with 16)
+  if (nw != 4 && nw != 8 && nw != 16)
+    nw = (a.KT < 64 || NB == 2) ? 4 : ((rows >= 8192 || a.KT < 128 || NORM) ? 8 : 16);
+  // MTTS_GEMV_PIPE bit 0 / bit 1 flips the batch depth (8 <-> 4 k-tiles) for <= 16 / > 16 rows
+  static const int pipe = getenv("MTTS_GEMV_PIPE") ? atoi(getenv("MTTS_GEMV_PIPE")) : 0;
+  if ((NB == 1 && (pipe & 1)) || (NB == 2 && !(pipe & 2))) {
     if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
     if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8, true>), dim3(n_tiles), dim3(512), lds, s, a);
     if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16, true>), dim3(n_tiles), dim3(1024), lds, s, a);

@@ -8,8 +8,10 @@
 // (moss_tts_delay/inference_utils.py:19-145).
 //
 // Per step:
-//   text_partial  (B, P blocks)   top-K (K = 1 for greedy) of each vocab slice, special ids excluded
-//   audio_select  (B, n_vq)       temperature, repetition penalty, top-k/top-p, argmax | draw
+//   score         (B, P + n_vq)   blocks y < P: top-K (K = 1 for greedy) of each text vocab slice,
+//                                 special ids excluded (skipped when no row samples text freely);
+//                                 y >= P: audio channel y-P: temperature, repetition penalty,
+//                                 top-k/top-p, argmax | draw
 //   text_select   (B)            merge partials + allowed special ids under the step's masks
 //   finalize      (1 block)      state update, next input ids, generation buffer, mask, stop
 #include "kernels.h"
@@ -61,10 +63,9 @@ __device__ __forceinline__ float scaled(bf16_t v, float temp) { return rbf(bf2f(
 
 // ---------------------------------------------------------------------------
 // top-K of one text vocab slice (special ids excluded), K = 1 when greedy
-__global__ __launch_bounds__(256) void text_partial_kernel(GenBufs g) {
+__device__ void text_partial_body(const GenBufs& g, int b, int p) {
   const GenDev& st = *g.st;
   if (!st.need_text) return;  // every sampling row is in audio mode: partials unused
-  const int b = blockIdx.x, p = blockIdx.y;
   const int K = st.text_sample ? min(st.text_top_k > 0 ? st.text_top_k : MAXK, MAXK) : 1;
   const int lo = p * st.part_len, hi = min(st.vocab, lo + st.part_len);
   const bf16_t* row = g.logits + (size_t)b * st.heads_ld;
@@ -186,9 +187,8 @@ __global__ __launch_bounds__(256) void text_select_kernel(GenBufs g) {
 }
 
 // audio channel j of row b: candidates over 1025 codes (modeling_moss_tts.py:483-503)
-__global__ __launch_bounds__(256) void audio_select_kernel(GenBufs g) {
+__device__ void audio_select_body(const GenBufs& g, int b, int j) {
   const GenDev& st = *g.st;
-  const int b = blockIdx.x, j = blockIdx.y;
   const int V = st.audio_rows;
   const bf16_t* row = g.logits + (size_t)b * st.heads_ld + st.vocab + (size_t)j * V;
   const uint8_t* seen = g.seen + (j == 0 ? 0 : V);
@@ -225,13 +225,19 @@ __global__ __launch_bounds__(256) void audio_select_kernel(GenBufs g) {
   }
 }
 
-// state update (one block, one thread per row) -- modeling_moss_tts.py:453-516
+// state update (one block) -- modeling_moss_tts.py:453-516.  Phase 1: one thread per row
+// updates the row's scalars; phase 2: one thread per (row, channel) writes the next input
+// ids, the generation buffer and the repetition-penalty history.
+constexpr int FIN_MAXB = 256;
 __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
   GenDev& st = *g.st;
   const MttsIds& d = st.ids;
-  const int n_vq = st.n_vq;
+  const int n_vq = st.n_vq, C = st.C;
   const int step = st.step;
+  const int col = st.T0 + step;
   __shared__ int n_stop, any_text;
+  __shared__ int s_nt[FIN_MAXB];
+  __shared__ int64_t s_al[FIN_MAXB], s_dl[FIN_MAXB];
   if (threadIdx.x == 0) n_stop = any_text = 0;
   __syncthreads();
   for (int b = threadIdx.x; b < st.B; b += blockDim.x) {
@@ -239,6 +245,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
     int64_t dl = g.delayed[b];
     int64_t al = g.audio_len[b];
     bool isa = g.is_audio[b] != 0;
+    s_al[b] = al;  // channel masks use the counters before this step's update (:477-480)
+    s_dl[b] = dl;
     int nt = d.pad;
     if (!stop && dl < n_vq) nt = d.delay_slot;
     const bool eos = !stop && dl == n_vq;
@@ -250,15 +258,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
     }
     if (nt == d.audio_start) isa = true;
     if (nt == d.im_end) stop = true;
-    int64_t* cur = g.cur_ids + (size_t)b * st.C;
-    cur[0] = nt;
-    for (int j = 0; j < n_vq; ++j) {
-      const bool pre = al > j;
-      const bool post = (dl == I64MAX) || ((int64_t)j > dl - 1);
-      const int tok = (pre && post) ? g.audio_cand[(size_t)b * n_vq + j] : d.audio_pad;
-      cur[1 + j] = tok;
-      g.seen[(j == 0 ? 0 : st.audio_rows) + tok] = 1;
-    }
+    s_nt[b] = nt;
     if (nt == d.audio_start || nt == d.gen_slot || nt == d.delay_slot) al += 1;
     if (nt == d.audio_end) al = 0;
     if (dl == I64MAX && nt == d.delay_slot) dl = 0;
@@ -268,15 +268,27 @@ __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
     g.is_audio[b] = isa;
     g.audio_len[b] = al;
     g.delayed[b] = dl;
-    const int col = st.T0 + step;
-    int64_t* gr = g.gen_ids + ((size_t)b * st.Ltot + col) * st.C;
-    for (int c = 0; c < st.C; ++c) gr[c] = cur[c];
     g.mask[(size_t)b * st.Cmax + col] = stop ? 0 : 1;
     if (stop) atomicAdd(&n_stop, 1);
     // next step samples this row's text channel over the full vocab (:453-471)
     if (!stop && dl > n_vq && !isa) atomicOr(&any_text, 1);
   }
   __syncthreads();
+  for (int i = threadIdx.x; i < st.B * C; i += blockDim.x) {
+    const int b = i / C, c = i - b * C;
+    int tok;
+    if (c == 0) {
+      tok = s_nt[b];
+    } else {
+      const int j = c - 1;
+      const bool pre = s_al[b] > j;
+      const bool post = (s_dl[b] == I64MAX) || ((int64_t)j > s_dl[b] - 1);
+      tok = (pre && post) ? g.audio_cand[(size_t)b * n_vq + j] : d.audio_pad;
+      g.seen[(j == 0 ? 0 : st.audio_rows) + tok] = 1;
+    }
+    g.cur_ids[(size_t)b * C + c] = tok;
+    g.gen_ids[((size_t)b * st.Ltot + col) * C + c] = tok;
+  }
   if (threadIdx.x == 0) {
     if (st.need_text) st.text_head_steps += 1;
     st.need_text = any_text;
@@ -333,9 +345,15 @@ hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, h
   return hipGetLastError();
 }
 
+// one launch for the text vocab partials (blockIdx.y < P) and the n_vq audio channels
+__global__ __launch_bounds__(256) void score_kernel(GenBufs g, int P) {
+  if ((int)blockIdx.y < P) text_partial_body(g, blockIdx.x, blockIdx.y);
+  else audio_select_body(g, blockIdx.x, blockIdx.y - P);
+}
+
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s) {
-  hipLaunchKernelGGL(text_partial_kernel, dim3(B, P), dim3(256), 0, s, g);
-  hipLaunchKernelGGL(audio_select_kernel, dim3(B, n_vq), dim3(256), 0, s, g);
+  if (B > FIN_MAXB) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(score_kernel, dim3(B, P + n_vq), dim3(256), 0, s, g, P);
   hipLaunchKernelGGL(text_select_kernel, dim3(B), dim3(256), 0, s, g);
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, g);
   return hipGetLastError();
