@@ -450,7 +450,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(DecAttnArgs a) {
 
   // ---- merge the 16 wave partials (fixed order) into the block's result / partial ----
   const int t = threadIdx.x;
-  const bool single = nact == 1;
+  const bool single = nact == 1 && !a.publish_only;
   float* part = a.part + (((size_t)b * a.Hkv + kvh) * a.ns + sp) * (G * (D + 2));
   for (int e = t; e < G * D; e += NWV * 64) {
     const int h = e / D, d = e % D;
@@ -475,7 +475,7 @@ __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(DecAttnArgs a) {
       }
     }
   }
-  if (single || a.probe == 3) return;
+  if (single || a.publish_only || a.probe == 3) return;
 
   // ---- publish + arrival ticket (agent-scope release / acquire) ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -544,6 +544,8 @@ static int decode_waves() {
   static const int nwv = getenv("MTTS_ATTN_NWV") ? atoi(getenv("MTTS_ATTN_NWV")) : 8;
   return (nwv == 8 || nwv == 16) ? nwv : 4;
 }
+
+int attn_decode_keys_per_block() { return DEC_KW * decode_waves(); }
 
 int attn_decode_splits(int Cmax) { return (Cmax + DEC_KW * decode_waves() - 1) / (DEC_KW * decode_waves()); }
 

@@ -69,7 +69,8 @@ struct mtts_engine {
   int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
   int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
   bool full_text_head = false;
-  bool gemv_prefill = false;    // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
+  bool gemv_prefill = false;
+  bool unfused_attn = false;    // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)    // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};
@@ -217,6 +218,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_UNFUSED_NORM")) e->unfused_norm = v[0] == '1';
   if (const char* v = getenv("MTTS_FULL_TEXT_HEAD")) e->full_text_head = v[0] == '1';
   if (const char* v = getenv("MTTS_GEMV_PREFILL")) e->gemv_prefill = v[0] == '1';
+  if (const char* v = getenv("MTTS_UNFUSED_ATTN")) e->unfused_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -457,6 +459,7 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
   const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
   HIPCHK(embed(ids, C, e->emb_text, e->emb_audio, e->audio_rows, H, e->h, M, s, e->ss, NT));
   const float eps = c.rms_eps;
+  const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn;
   for (int l = 0; l < c.layers; ++l) {
     const LayerW& w = e->L[l];
     bf16_t* kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
@@ -466,10 +469,12 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     g.force_nw = e->nw[0];
     HIPCHK(proj(e, g, EPI_STORE, s));
     if (S == 1) {
-      DecAttnArgs da;
+      DecAttnArgs da{};
       da.qkv = e->qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = e->cos_t; da.sin_t = e->sin_t;
       da.kc = kc; da.vc = vc; da.mask = e->mask + (size_t)b0 * c.max_ctx; da.pos = pos_base; da.out = e->attnb;
       da.part = e->part; da.cnt = e->att_cnt;
+      // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
+      da.publish_only = fuse_attn ? 1 : 0;
       da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = c.max_ctx; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
       HIPCHK(attn_decode(da, B, s));
     } else {
@@ -487,6 +492,10 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     }
     g = gemv_args(w.o, e->attnb, Hq * D, e->h, H, M, H, Hq * D);
     g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
+    if (fuse_attn) {
+      g.attn.part = e->part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
+      g.attn.ns = attn_decode_splits(c.max_ctx); g.attn.kb = attn_decode_keys_per_block();
+    }
     HIPCHK(proj(e, g, EPI_RESADD, s));
     g = gemv_args(w.gu, e->xn, H, e->act, I, M, I, H);
     if (int rc = normed_input(e, g, w.post_norm, M, s)) return rc;
@@ -806,7 +815,7 @@ extern "C" int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, con
                                   const int32_t* pos, uint16_t* out, void* ws, int B, int Hq, int Hkv, int D, int Cmax,
                                   float eps, void* stream) {
   if (!ws) return fail(MTTS_E_INVALID, "workspace required");
-  DecAttnArgs a;
+  DecAttnArgs a{};
   a.qkv = qkv; a.qn_w = qn_w; a.kn_w = kn_w; a.cos_t = cos_t; a.sin_t = sin_t; a.kc = kc; a.vc = vc; a.mask = mask;
   a.pos = pos; a.out = out; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.eps = eps;
   a.cnt = reinterpret_cast<int*>(ws);

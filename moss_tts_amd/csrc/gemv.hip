@@ -42,7 +42,7 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
   return o;
 }
 
-template <int NB, int RT, int EPI, bool NORM, int NW, bool PIPE = false>
+template <int NB, int RT, int EPI, int PRO, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
   // bytes in flight per wave for more resident waves (the default for 17-32 rows)
@@ -88,12 +88,16 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
   };
   if (kt + U <= kt1) issue_w(kt);
 
-  // NORM: the block stages bf16(nw * bf16(x * r_b)) for all its B rows in LDS once
-  // (r_b from the producer's per-16-column sums of squares); the MFMA B fragments are then
-  // LDS reads.  Without NORM the fragments come straight from x (L2).
+  // Prologues (PRO) stage the block's B activation rows in LDS once; the MFMA B fragments
+  // are then LDS reads.  PRO_NONE reads the fragments straight from x (L2).
+  //   PRO_NORM:  bf16(nw * bf16(x * r_b)), r_b from the producer's per-16-column sums of
+  //              squares (Qwen3RMSNorm, TF/models/qwen3/modeling_qwen3.py:59-64)
+  //   PRO_ATTN:  the decode attention output, merged here from its per-split (m, l, o)
+  //              partials in split order: x = bf16(sum_s f_s o_s / sum_s f_s l_s),
+  //              f_s = exp(m_s - max m) -- the cross-block combine of attn_decode
   extern __shared__ u32x4 xs_dyn[];
   const int K8 = KT * 4;  // 16-byte chunks per row
-  if constexpr (NORM) {
+  if constexpr (PRO == PRO_NORM) {
     __shared__ float r_s[32];
     const int n8x = a.B * K8;
     for (int i = threadIdx.x; i < n8x + K8; i += NW * 64) {
@@ -117,10 +121,37 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
       xs_dyn[i] = norm8(xs_dyn[i], xs_dyn[n8x + i - b * K8], r_s[b]);
     }
     __syncthreads();
+  } else if constexpr (PRO == PRO_ATTN) {
+    const AttnPartView& v = a.attn;
+    const int nact = *v.pos / v.kb + 1;
+    const int G = v.G, D = v.D, PS = G * (D + 2);
+    for (int i = threadIdx.x; i < a.B * K8; i += NW * 64) {
+      const int b = i / K8, k0 = (i - b * K8) * 8;
+      const int h = k0 / D, d0 = k0 - h * D, kvh = h / G, hg = h - kvh * G;
+      const float* pp = v.part + ((size_t)b * v.Hkv + kvh) * v.ns * PS;
+      float M = -INFINITY;
+      for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, pp[(size_t)s2 * PS + G * D + 2 * hg]);
+      float L = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < nact; ++s2) {
+        const float* q = pp + (size_t)s2 * PS;
+        const float ms = q[G * D + 2 * hg];
+        const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
+        L += f * q[G * D + 2 * hg + 1];
+        const float4 o0 = *reinterpret_cast<const float4*>(q + hg * D + d0);
+        const float4 o1 = *reinterpret_cast<const float4*>(q + hg * D + d0 + 4);
+        o[0] += f * o0.x; o[1] += f * o0.y; o[2] += f * o0.z; o[3] += f * o0.w;
+        o[4] += f * o1.x; o[5] += f * o1.y; o[6] += f * o1.z; o[7] += f * o1.w;
+      }
+      u32x4 r;
+#pragma unroll
+      for (int q2 = 0; q2 < 4; ++q2) r[q2] = L > 0.f ? pack2(o[2 * q2] / L, o[2 * q2 + 1] / L) : 0u;
+      xs_dyn[i] = r;
+    }
+    __syncthreads();
   }
   auto load_x = [&](int k, int nb) -> u32x4 {
     if (!xok[nb]) return (u32x4){0u, 0u, 0u, 0u};
-    if constexpr (NORM) return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
+    if constexpr (PRO != PRO_NONE) return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
     return xbase[nb][k * 4];
   };
 
@@ -243,12 +274,13 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-template <int NB, int RT, int EPI, bool NORM>
+template <int NB, int RT, int EPI, int PRO>
 static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
+  constexpr bool NORM = PRO == PRO_NORM;
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
-  const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : 0;
+  const size_t lds = PRO == PRO_NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN ? (size_t)a.B * a.K * 2 : 0);
   // 17-32 rows (NB = 2): 4 waves of 4-deep batches (in-context B=32 sweep: 5.62 vs 6.03 ms/step)
   int nw = a.force_nw;
   // fused-norm launches stage (B+1)*K*2 bytes of LDS per block: 8 waves keep 2 blocks per CU
@@ -258,27 +290,36 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // MTTS_GEMV_PIPE bit 0 / bit 1 flips the batch depth (8 <-> 4 k-tiles) for <= 16 / > 16 rows
   static const int pipe = getenv("MTTS_GEMV_PIPE") ? atoi(getenv("MTTS_GEMV_PIPE")) : 0;
   if ((NB == 1 && (pipe & 1)) || (NB == 2 && !(pipe & 2))) {
-    if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
-    if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8, true>), dim3(n_tiles), dim3(512), lds, s, a);
-    if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16, true>), dim3(n_tiles), dim3(1024), lds, s, a);
+    if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
+    if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8, true>), dim3(n_tiles), dim3(512), lds, s, a);
+    if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16, true>), dim3(n_tiles), dim3(1024), lds, s, a);
     return;
   }
-  if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 4>), dim3(n_tiles), dim3(256), lds, s, a);
-  if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 8>), dim3(n_tiles), dim3(512), lds, s, a);
-  if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, NORM, 16>), dim3(n_tiles), dim3(1024), lds, s, a);
+  if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4>), dim3(n_tiles), dim3(256), lds, s, a);
+  if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8>), dim3(n_tiles), dim3(512), lds, s, a);
+  if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16>), dim3(n_tiles), dim3(1024), lds, s, a);
 }
 
 template <int RT, int EPI>
 static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
   const bool two = a.B > 16;
+  if constexpr (EPI == EPI_RESADD) {
+    if (a.attn.part) {  // o_proj reading the attention partials (B <= 16)
+      launch_nw<1, RT, EPI, PRO_ATTN>(a, n_tiles, s);
+      return;
+    }
+  }
   const bool norm = a.ss_in != nullptr;
-  if (two) norm ? launch_nw<2, RT, EPI, true>(a, n_tiles, s) : launch_nw<2, RT, EPI, false>(a, n_tiles, s);
-  else norm ? launch_nw<1, RT, EPI, true>(a, n_tiles, s) : launch_nw<1, RT, EPI, false>(a, n_tiles, s);
+  if (two) norm ? launch_nw<2, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<2, RT, EPI, PRO_NONE>(a, n_tiles, s);
+  else norm ? launch_nw<1, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<1, RT, EPI, PRO_NONE>(a, n_tiles, s);
 }
 
 hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   if (a0.K % 32 != 0 || a0.B <= 0 || a0.N <= 0) return hipErrorInvalidValue;
   if (a0.ss_in && (a0.n_ss % 4 || a0.ld_ss % 4 || a0.ldx % 8 || norm_lds_bytes(std::min(a0.B, 32), a0.K) > NORM_LDS_MAX))
+    return hipErrorInvalidValue;
+  if (a0.attn.part && (epi != EPI_RESADD || a0.B > 16 || (size_t)a0.B * a0.K * 2 > NORM_LDS_MAX || a0.attn.D % 8 ||
+                       a0.K != a0.attn.Hkv * a0.attn.G * a0.attn.D))
     return hipErrorInvalidValue;
   for (int b0 = 0; b0 < a0.B; b0 += 32) {
     GemvArgs a = a0;

@@ -9,6 +9,15 @@ constexpr int MAXK = 64;  // largest top-k handled on device
 
 enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 
+enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2 };
+
+// decode-attention split partials as read by the o_proj prologue (PRO_ATTN)
+struct AttnPartView {
+  const float* part;   // [B][Hkv][ns][G*(D+2)]: o[G][D], then (m, l) per head
+  const int* pos;      // device: position of the new token
+  int Hkv, G, D, ns, kb;  // kb = keys per attention block
+};
+
 struct GemvArgs {
   const bf16_t* w;     // packed tiles
   const bf16_t* x;     // [B, ldx] activations (bf16)
@@ -35,6 +44,7 @@ struct GemvArgs {
   int tile0;           // first output row tile of this launch (row ranges of one matrix)
   const int* gate;     // device flag: the launch does nothing when *gate == 0 (nullptr: always on)
   int n_row_tiles;     // packed 16-row weight tiles (set by the GEMM launcher)
+  AttnPartView attn;   // PRO_ATTN (o_proj): x is merged from these partials; attn.part == nullptr: off
 };
 
 inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {
@@ -92,6 +102,7 @@ struct DecAttnArgs {
   int ns;               // splits per head (set by attn_decode)
   int nwv;              // waves per block (32 keys each; set by attn_decode)
   float eps, scale;
+  int publish_only;     // 1: every block writes its (m, l, o) partial; the o_proj GEMV merges them
   int probe;            // timing probe (MTTS_ATTN_PROBE): 0 full; 1 exit after pos; 2 after loads + prologue; 3 no combine
 };
 
@@ -158,6 +169,7 @@ size_t attn_smem_bytes(int G, int D, int CH);
 hipError_t attention(const AttnArgs& a, hipStream_t s);
 hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s);
 int attn_decode_splits(int Cmax);
+int attn_decode_keys_per_block();
 // workspace of attn_decode: ticket counters (zero-filled once by the owner) + partials
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 // sample.hip
