@@ -452,7 +452,8 @@ static hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s
 }
 
 static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
-                        int n_split, bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr) {
+                        int n_split, bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr,
+                        bool heads = true) {
   const mtts_config& c = e->c;
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter, C = c.n_vq + 1;
   const int M = B * S;
@@ -505,6 +506,7 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
     g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
     HIPCHK(proj(e, g, EPI_RESADD, s));
   }
+  if (!heads) return 0;  // a leading chunk of a position-chunked prefill: KV cache only
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
   GemvArgs g = gemv_args(e->heads, e->xn, H, logits_out, e->heads_ld, B, e->heads_rows, H);
   if (S == 1) {
@@ -529,17 +531,34 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
   return 0;
 }
 
-// prefill / teacher-forced forward of S tokens at position `past` (host int), rows chunked
+// prefill / teacher-forced forward of S tokens at position `past` (host int).  Rows are
+// chunked so that rows x S <= max_prefill_tokens; a prompt longer than that is prefilled one
+// row at a time in position chunks of max_prefill_tokens (each chunk attends to the cache the
+// previous ones wrote; only the last chunk evaluates the heads) -- the long-form (TTSD) path.
 static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s) {
   const mtts_config& c = e->c;
-  if (S > e->Mmax) return fail(MTTS_E_UNSUPPORTED, "prompt longer than max_prefill_tokens");
+  const int C = c.n_vq + 1;
+  const int CH = S == 1 ? CH_DECODE : CH_PREFILL;
+  if (S > e->Mmax) {
+    const int P = e->Mmax;
+    for (int b = 0; b < B; ++b) {
+      for (int s0 = 0; s0 < S; s0 += P) {
+        const int len = std::min(P, S - s0);
+        HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->d_pos), past + s0, 1, s));
+        const int n_split = (past + s0 + len + CH - 1) / CH;
+        int rc = forward_rows(e, ids + ((size_t)b * S + s0) * C, b, 1, len, e->d_pos, CH, n_split,
+                              logits_out + (size_t)b * e->heads_ld, s, nullptr, s0 + len == S);
+        if (rc) return rc;
+      }
+    }
+    return 0;
+  }
   HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->d_pos), past, 1, s));
   const int rows_per = std::max(1, e->Mmax / S);
-  const int CH = S == 1 ? CH_DECODE : CH_PREFILL;
   const int n_split = (past + S + CH - 1) / CH;
   for (int b0 = 0; b0 < B; b0 += rows_per) {
     const int nb = std::min(rows_per, B - b0);
-    int rc = forward_rows(e, ids + (size_t)b0 * S * (c.n_vq + 1), b0, nb, S, e->d_pos, CH, n_split,
+    int rc = forward_rows(e, ids + (size_t)b0 * S * C, b0, nb, S, e->d_pos, CH, n_split,
                           logits_out + (size_t)b0 * e->heads_ld, s);
     if (rc) return rc;
   }

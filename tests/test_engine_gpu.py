@@ -13,12 +13,12 @@ torch = pytest.importorskip("torch")
 CASES = ["g_nvq4_fp32", "g_nvq4_stop_fp32", "g_nvq16_bf16", "g_nvq32_bf16", "g_nvq4_pen_fp32", "g_nvq4_b1_fp32"]
 
 
-def make_engine(cfg, W, max_batch=4, max_ctx=256):
+def make_engine(cfg, W, max_batch=4, max_ctx=256, max_prefill_tokens=512):
     from moss_tts_amd.engine import Engine, EngineConfig
     e = Engine(EngineConfig(hidden=cfg.hidden, layers=cfg.layers, n_heads=cfg.n_heads, n_kv=cfg.n_kv,
                             head_dim=cfg.head_dim, inter=cfg.inter, vocab=cfg.vocab, n_vq=cfg.n_vq,
                             rope_theta=cfg.rope_theta, max_batch=max_batch, max_ctx=max_ctx,
-                            max_prefill_tokens=512), 0)
+                            max_prefill_tokens=max_prefill_tokens), 0)
     e.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
     return e
 
@@ -48,15 +48,17 @@ def gpu():
         pytest.skip("no GPU")
 
 
-@pytest.mark.parametrize("name", CASES)
-def test_generate_matches_oracle(gpu, golden, name):
+@pytest.mark.parametrize("name,prefill_cap", [(n, 512) for n in CASES] + [("g_nvq16_bf16", 8), ("g_nvq4_b1_fp32", 8)])
+def test_generate_matches_oracle(gpu, golden, name, prefill_cap):
+    """prefill_cap < prompt length exercises the position-chunked prefill (long-form path)."""
     from moss_tts_amd.engine import sampling_params
     g, c, cfg, W = case(golden, name)
     ids, mask = g[name + "/input_ids"], g[name + "/mask"]
     tr = O.StepTrace()
     ref = O.generate(W, cfg, ids, mask, max_new_tokens=c["steps"], text_temperature=0, audio_temperature=0,
                      audio_repetition_penalty=c["penalty"], dtype="bf16", trace=tr)
-    eng = make_engine(cfg, W)
+    eng = make_engine(cfg, W, max_prefill_tokens=prefill_cap)
+    assert prefill_cap >= 512 or ids.shape[1] > max(prefill_cap, 4), "case must exceed the chunk"
     out = eng.generate_ids(torch.from_numpy(ids), torch.from_numpy(mask), c["steps"],
                            sampling_params(text_temperature=0, audio_temperature=0,
                                            audio_repetition_penalty=c["penalty"]))

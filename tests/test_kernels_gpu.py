@@ -301,12 +301,13 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
 
 @pytest.mark.parametrize("past,D,Hq,Hkv,B", [(10, 128, 32, 8, 1), (0, 16, 4, 2, 3), (300, 128, 8, 2, 2), (700, 64, 4, 1, 2),
                                              (127, 128, 32, 8, 1), (128, 128, 32, 8, 2), (1023, 16, 8, 1, 1),
-                                             (389, 128, 32, 8, 4)])
+                                             (389, 128, 32, 8, 4), (3000, 128, 32, 8, 1), (8100, 64, 8, 2, 1)])
 def test_attn_decode_fused(N, past, D, Hq, Hkv, B):
-    """Fused decode step (norm + rope + append + attention) against the oracle ops."""
+    """Fused decode step (norm + rope + append + attention) against the oracle ops; long
+    contexts exercise the multi-block split and its combine."""
     rng = np.random.default_rng(past + D)
     ctx = O._Ctx("bf16")
-    Cmax = 1024
+    Cmax = max(1024, (past + 1 + 63) // 64 * 64)
     heads = Hq + 2 * Hkv
     qkv = rand_bf16(rng, (B, heads * D), 2.0)
     qn = B16.rnd(1 + 0.25 * rng.standard_normal(D).astype(np.float32))
