@@ -144,6 +144,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--extra-batches", default="4,32", help="extra per-GPU batch sizes reported in batch_sweep")
+    ap.add_argument("--config", choices=["clone", "ttsd"], default="clone",
+                    help="clone: configs[1] (default); ttsd: configs[4], MOSS-TTSD long form (n_vq 16, a "
+                         "2,000-token script, 10 min = 7,500 frames of audio, position-chunked prefill)")
     args = ap.parse_args()
 
     import torch
@@ -159,22 +162,30 @@ def main():
     from moss_tts_amd.engine import Engine, EngineConfig, sampling_params
     from moss_tts_amd import _native as Nn
     import ctypes
+    n_vq = 32
+    text_tokens = 48
+    if args.config == "ttsd":
+        n_vq, text_tokens = 16, 2000
+        if args.decode_steps == 208:
+            args.decode_steps = 7500 + n_vq + 3
+        args.extra_batches = ""
     n_steps = args.decode_steps
-    gen_frames = n_steps - 35
+    gen_frames = n_steps - (n_vq + 3)
     extra = [int(x) for x in args.extra_batches.split(",") if x] if args.extra_batches else []
     max_b = max([args.batch] + extra)
-    ecfg = EngineConfig(layers=args.layers, max_batch=max_b, max_ctx=256 + n_steps + 16,
-                        max_prefill_tokens=max(256 * max_b, 256))
+    prompt_cap = 64 + text_tokens + 2 * n_vq + 64
+    ecfg = EngineConfig(layers=args.layers, n_vq=n_vq, max_batch=max_b, max_ctx=prompt_cap + n_steps + 16,
+                        max_prefill_tokens=max(256 * max_b, 256) if args.config == "clone" else 1024)
     eng = Engine(ecfg, local)
     eng.init_random(seed=0)
-    forced = torch.from_numpy(forced_schedule(n_steps, 32, gen_frames)).cuda()
+    forced = torch.from_numpy(forced_schedule(n_steps, n_vq, gen_frames)).cuda()
     sp = sampling_params(text_temperature=0, audio_temperature=0)
 
     def run_batch(B, steps, warmup, latency=False):
         """steps x generate() of B utterances; returns (wall s max over ranks, audio s summed
         over ranks, T, frames of row 0, text-head steps, prefill ms, p50 first-chunk ms)"""
         rng = np.random.default_rng(1 + rank)
-        prompts = [synthetic_prompt(cfgd, rng) for _ in range(B)]
+        prompts = [synthetic_prompt(cfgd, rng, text_tokens=text_tokens) for _ in range(B)]
         from moss_tts_amd.processing_moss_tts import left_pad
         padded = left_pad([torch.from_numpy(p) for p in prompts], 151643, 1024)
         ids, mask = padded["input_ids"].numpy(), padded["attention_mask"].numpy()
@@ -203,7 +214,7 @@ def main():
         Nn.check(Nn.load().mtts_generate_stats(eng._h, ctypes.byref(th)), "stats")
         # frames actually produced (de-delayed, non-pad rows after the assistant start)
         g = out.cpu().numpy()
-        frames = [count_audio_frames(g[b], T, 32) for b in range(B)]
+        frames = [count_audio_frames(g[b], T, n_vq) for b in range(B)]
         audio_s = sum(frames) / FRAME_RATE * steps
         t = torch.tensor([dt, audio_s], dtype=torch.float64, device="cuda")
         if world > 1:
@@ -215,7 +226,7 @@ def main():
         if latency:
             # first-chunk latency: prefill + decode until the first 1 s of audio (13 frames) has
             # all n_vq codebooks (frame f is complete n_vq steps after its first codebook)
-            first_steps = 1 + 13 + 32
+            first_steps = 1 + 13 + n_vq
             begin = lambda: Nn.check(Nn.load().mtts_generate_begin(
                 eng._h, ctypes.c_void_p(ids_d.data_ptr()), ctypes.c_void_p(mask_d.data_ptr()), B, T, n_steps,
                 ctypes.byref(sp), ctypes.c_void_p(forced.data_ptr()), None), "begin")
@@ -236,7 +247,7 @@ def main():
             t_begin, p50 = float(np.median(tb)), float(np.median(lat))
         return float(t[0]), float(t[1]), T, frames[0], th.value, t_begin, p50
 
-    cfgd = dict(n_vq=32)
+    cfgd = dict(n_vq=n_vq)
     dt_max, audio_total, T, frames0, text_steps, t_begin, p50 = run_batch(args.batch, args.steps, args.warmup, True)
     sweep = {}
     for B in extra:
@@ -267,14 +278,17 @@ def main():
             "ms_per_step": round(per_utt_ms, 3), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init bf16 weights at the MossTTSDelay-8B shape; synthetic clone prompts)",
-            "config": {"workload": "MossTTSDelay bf16 batch=1 zero-shot clone (3s prompt audio) on 1xMI355X, hipGraph "
-                                   "decode" if args.batch == 1 else f"MossTTSDelay bf16 batch={args.batch}/GPU",
+            "config": {"workload": (("MOSS-TTSD long form (n_vq 16, 2000-token script, 7500 frames) bf16 batch="
+                                    f"{args.batch}/GPU, chunked prefill, hipGraph decode") if args.config == "ttsd" else
+                                   "MossTTSDelay bf16 batch=1 zero-shot clone (3s prompt audio) on 1xMI355X, hipGraph "
+                                   "decode" if args.batch == 1 else f"MossTTSDelay bf16 batch={args.batch}/GPU"),
+                       "n_vq": n_vq,
                        "batch_per_gpu": args.batch, "prompt_tokens": int(T), "decode_steps": n_steps,
                        "layers": args.layers, "parallelism": f"dp{world}", "sampling": "greedy, forced text schedule"},
             "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
             "audio_frames_per_utt": frames0,
             "p50_first_chunk_ms": round(p50, 2),
-            "first_chunk_def": "prefill + 46 decode steps (first 1 s of audio codes complete), codec excluded",
+            "first_chunk_def": f"prefill + {13 + n_vq + 1} decode steps (first 1 s of audio codes complete), codec excluded",
             "decode_weight_bytes": wb,
             "roofline": roof,
         }

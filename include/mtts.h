@@ -143,6 +143,11 @@ size_t mtts_k_attention_ws_bytes(int M, int Hq, int D, int n_split);
 int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
                      const int32_t* pos_base_dev, uint16_t* out, void* workspace_dev, int M, int S, int Hq, int Hkv,
                      int D, int Cmax, int CH, int n_split, void* stream);
+/* flash-form prefill attention (no workspace): q [M = B*S, Hq*D] (normed + roped), caches
+ * already holding the S new tokens at *pos_dev .. +S-1; out [M, Hq*D]; D in {16, 32, 64, 128} */
+int mtts_k_attention_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
+                             const int32_t* pos_dev, uint16_t* out, int M, int S, int Hq, int Hkv, int D, int Cmax,
+                             void* stream);
 /* fused decode step of one layer's attention: q/k RMSNorm + RoPE of the new token (qkv
  * [B, (Hq+2Hkv)*D]), k/v appended to the cache at *pos_dev, attention over keys 0..pos
  * under mask [B, Cmax] (Cmax % 64 == 0), split over the context in 128-key blocks;

@@ -69,6 +69,7 @@ _SIGS = {
     "mtts_k_qk_norm_rope": (I, [P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, F, P]),
     "mtts_k_attention_ws_bytes": (SZ, [I, I, I, I]),
     "mtts_k_attention": (I, [P, P, P, P, P, P, P, I, I, I, I, I, I, I, I, P]),
+    "mtts_k_attention_prefill": (I, [P, P, P, P, P, P, I, I, I, I, I, I, P]),
     "mtts_k_attn_decode_ws_bytes": (SZ, [I, I, I, I, I]),
     "mtts_k_attn_decode": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
     "mtts_rope_table": (I, [F, I, I, P, P]),

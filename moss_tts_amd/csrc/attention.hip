@@ -158,6 +158,165 @@ __global__ __launch_bounds__(256) void attn_combine_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Prefill attention, flash form on MFMA.  Grid (16-token query tile, KV head, row b); one
+// wave per query head of the GQA group, so the G waves of a block read the same K / V^T
+// tiles (through L1).  Per 32-key chunk a wave computes
+//   S[16 tokens][32 keys] = Q[16 x D] . K^T          (v_mfma_f32_16x16x32_bf16, B = K rows)
+// with the causal + padding mask, an online softmax per token row (probabilities rounded
+// to bf16 before P.V, fp32 statistics), and
+//   O[16 tokens][D] = O * alpha + P[16 x 32] . V[32 x D]  (P through LDS, V^T from the cache)
+// so each K/V byte is read once per 16 tokens x G heads instead of once per token.
+template <int G, int D>
+__global__ __launch_bounds__(G * 64) void attn_prefill_kernel(AttnArgs a) {
+  constexpr int QS = (D + 31) / 32, DT = (D + 15) / 16;  // dims beyond D are zero-filled
+  const int qt = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int hq = kvh * G + wave;
+  const int s0 = qt * 16;                       // first token of the tile (within the row)
+  const int pos0 = *a.pos_base + s0;            // its absolute position
+  const int last = min(a.S - 1, s0 + 15);
+  const int kend = *a.pos_base + last;          // last key any token of the tile sees
+  const int Cmax = a.Cmax;
+  __shared__ __attribute__((aligned(16))) bf16_t p_s[G][16][32];
+  const bf16_t* kbase = a.kc + ((size_t)b * a.Hkv + kvh) * Cmax * D;
+  const bf16_t* vbase = a.vc + ((size_t)b * a.Hkv + kvh) * D * Cmax;
+  const uint8_t* mrow = a.mask + (size_t)b * Cmax;
+
+  // Q A-operand fragments: token s0 + (lane & 15), dims st*32 + 8*(lane>>4) .. +7
+  bf16x8 qf[QS];
+  {
+    const int tq = min(s0 + c16, a.S - 1);
+    const bf16_t* qrow = a.q + ((size_t)b * a.S + tq) * a.Hq * D + (size_t)hq * D;
+#pragma unroll
+    for (int st = 0; st < QS; ++st)
+      qf[st] = st * 32 + 8 * g4 < D ? *reinterpret_cast<const bf16x8*>(qrow + st * 32 + 8 * g4)
+                                    : __builtin_bit_cast(bf16x8, (u32x4){0u, 0u, 0u, 0u});
+  }
+  // this lane's output rows: tokens s0 + g4*4 + i
+  float m_run[4], l_run[4];
+  f32x4 o_run[DT];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { m_run[i] = -INFINITY; l_run[i] = 0.f; }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o_run[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  for (int k0 = 0; k0 <= kend; k0 += 32) {
+    // ---- S = Q . K^T for keys k0 .. k0+31 (two 16-key tiles) ----
+    f32x4 sacc[2];
+    uint32_t mk[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = k0 + t * 16 + c16;
+      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      mk[t] = key <= kend ? mrow[key] : 0u;
+#pragma unroll
+      for (int st = 0; st < QS; ++st) {
+        const u32x4 kf = (key <= kend && st * 32 + 8 * g4 < D)
+                             ? *reinterpret_cast<const u32x4*>(kbase + (size_t)key * D + st * 32 + 8 * g4)
+                             : (u32x4){0u, 0u, 0u, 0u};
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[st], __builtin_bit_cast(bf16x8, kf), sacc[t], 0, 0, 0);
+      }
+    }
+    // V^T B-operand fragments: dim dt*16 + c16, keys k0 + 8*g4 .. +7 (zero beyond kend)
+    u32x4 vt[DT];
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int kb = k0 + 8 * g4;
+      vt[dt] = kb <= kend ? *reinterpret_cast<const u32x4*>(vbase + (size_t)(dt * 16 + c16) * Cmax + kb)
+                          : (u32x4){0u, 0u, 0u, 0u};
+      if (kb <= kend && kb + 7 > kend) {
+        u32x4 v = vt[dt];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t lo = kb + 2 * i <= kend ? (v[i] & 0xffffu) : 0u;
+          const uint32_t hi = kb + 2 * i + 1 <= kend ? (v[i] >> 16) : 0u;
+          v[i] = lo | (hi << 16);
+        }
+        vt[dt] = v;
+      }
+    }
+    // ---- online softmax per token row (row = g4*4 + i, keys over the 16-lane group) ----
+    float alpha[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int pq = pos0 + g4 * 4 + i;
+      float sv[2];
+      float mc = -INFINITY;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int key = k0 + t * 16 + c16;
+        sv[t] = (key <= pq && mk[t]) ? sacc[t][i] * a.scale : -INFINITY;
+        mc = fmaxf(mc, sv[t]);
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) mc = fmaxf(mc, __shfl_xor(mc, o, 64));
+      const float mn = fmaxf(m_run[i], mc);
+      alpha[i] = (m_run[i] == -INFINITY) ? (mn == -INFINITY ? 1.f : 0.f) : expf(m_run[i] - mn);
+      float lc = 0.f;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const float p = (mn == -INFINITY || sv[t] == -INFINITY) ? 0.f : expf(sv[t] - mn);
+        lc += p;
+        p_s[wave][g4 * 4 + i][t * 16 + c16] = f2bf(p);  // bf16-rounded probabilities
+      }
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) lc += __shfl_xor(lc, o, 64);
+      l_run[i] = l_run[i] * alpha[i] + lc;
+      m_run[i] = mn;
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    // ---- O = O * alpha + P . V ----
+    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[wave][c16][8 * g4]);
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
+                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) o_run[dt][i] = o_run[dt][i] * alpha[i] + oc[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+  // ---- normalise and store: token s0 + g4*4 + i, dims dt*16 + c16 ----
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int tq = s0 + g4 * 4 + i;
+    if (tq >= a.S) continue;
+    bf16_t* dst = a.out + ((size_t)b * a.S + tq) * a.Hq * D + (size_t)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) dst[dt * 16 + c16] = f2bf(l_run[i] > 0.f ? o_run[dt][i] / l_run[i] : 0.f);
+  }
+}
+
+template <int D>
+static hipError_t attn_prefill_d(const AttnArgs& a, int G, hipStream_t st) {
+  const int B = a.M / a.S;
+  dim3 grid((a.S + 15) / 16, a.Hkv, B);
+  switch (G) {
+    case 1: hipLaunchKernelGGL((attn_prefill_kernel<1, D>), grid, dim3(64), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((attn_prefill_kernel<2, D>), grid, dim3(128), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((attn_prefill_kernel<4, D>), grid, dim3(256), 0, st, a); break;
+    case 8: hipLaunchKernelGGL((attn_prefill_kernel<8, D>), grid, dim3(512), 0, st, a); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t attention_prefill(const AttnArgs& a, hipStream_t st) {
+  const int G = a.Hq / a.Hkv;
+  if (a.Hq % a.Hkv || a.M % a.S || a.Cmax % 64) return hipErrorInvalidValue;
+  switch (a.D) {
+    case 128: return attn_prefill_d<128>(a, G, st);
+    case 64: return attn_prefill_d<64>(a, G, st);
+    case 32: return attn_prefill_d<32>(a, G, st);
+    case 16: return attn_prefill_d<16>(a, G, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 size_t attn_smem_bytes(int G, int D, int CH) {
   const int LPK = D / 8;
   const int slots = 256 / LPK;

@@ -70,7 +70,8 @@ struct mtts_engine {
   int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
   bool full_text_head = false;
   bool gemv_prefill = false;
-  bool unfused_attn = false;    // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)    // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
+  bool unfused_attn = false;
+  bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)    // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)    // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};
@@ -219,6 +220,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_FULL_TEXT_HEAD")) e->full_text_head = v[0] == '1';
   if (const char* v = getenv("MTTS_GEMV_PREFILL")) e->gemv_prefill = v[0] == '1';
   if (const char* v = getenv("MTTS_UNFUSED_ATTN")) e->unfused_attn = v[0] == '1';
+  if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -489,7 +491,8 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
       aa.part_o = e->part; aa.part_ml = e->part + (size_t)M * n_split * Hq * D; aa.out = e->attnb;
       aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = c.max_ctx; aa.CH = CH; aa.n_split = n_split; aa.M = M;
       aa.scale = 1.0f / std::sqrt((float)D);
-      HIPCHK(attention(aa, s));
+      if (e->old_prefill_attn) HIPCHK(attention(aa, s));
+      else HIPCHK(attention_prefill(aa, s));
     }
     g = gemv_args(w.o, e->attnb, Hq * D, e->h, H, M, H, Hq * D);
     g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
@@ -773,6 +776,16 @@ extern "C" int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uin
   a.out = out; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.CH = CH; a.n_split = n_split; a.M = M;
   a.scale = 1.0f / std::sqrt((float)D);
   HIPCHK(attention(a, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_attention_prefill(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
+                                        const int32_t* pos, uint16_t* out, int M, int S, int Hq, int Hkv, int D, int Cmax,
+                                        void* stream) {
+  AttnArgs a{};
+  a.q = q; a.kc = kc; a.vc = vc; a.mask = mask; a.pos_base = pos; a.out = out;
+  a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.M = M;
+  a.scale = 1.0f / std::sqrt((float)D);
+  HIPCHK(attention_prefill(a, (hipStream_t)stream));
   return 0;
 }
 extern "C" int mtts_k_fill_uniform(uint16_t* dst, size_t n, uint64_t seed, uint64_t tid, float scale, float offset,

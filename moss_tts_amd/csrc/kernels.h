@@ -167,6 +167,8 @@ hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s);
 // attention.hip
 size_t attn_smem_bytes(int G, int D, int CH);
 hipError_t attention(const AttnArgs& a, hipStream_t s);
+// flash-form prefill attention (no workspace, no combine); D in {32, 64, 128}
+hipError_t attention_prefill(const AttnArgs& a, hipStream_t s);
 hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s);
 int attn_decode_splits(int Cmax);
 int attn_decode_keys_per_block();

@@ -245,7 +245,8 @@ def test_rope_table_matches_oracle():
     assert np.abs(B16.from_bits(cs) - c).max() <= 2 ** -8
 
 
-@pytest.mark.parametrize("S,past,D,Hq,Hkv", [(1, 10, 128, 32, 8), (5, 0, 16, 4, 2), (3, 300, 128, 8, 8)])
+@pytest.mark.parametrize("S,past,D,Hq,Hkv", [(1, 10, 128, 32, 8), (5, 0, 16, 4, 2), (3, 300, 128, 8, 8), (40, 0, 128, 32, 8),
+                                             (181, 0, 128, 32, 8), (100, 350, 64, 8, 2), (33, 17, 16, 8, 1)])
 def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
     rng = np.random.default_rng(S * 7 + past)
     ctx = O._Ctx("bf16")
@@ -274,7 +275,14 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
     q = O.apply_rope(ctx, q, cos[past:past + S], sin[past:past + S])
     k = O.apply_rope(ctx, k, cos[past:past + S], sin[past:past + S])
     gq = host(qo).reshape(B, S, Hq, D).transpose(0, 2, 1, 3)
-    assert within_band(gq, q, 1.0).all() and np.mean(gq == q) > 0.98
+    # r = rsqrt(mean(x^2)) sums in a different order than numpy, so a normed value can round
+    # across a bf16 boundary before the rotation; the rotation (a difference of two products)
+    # can cancel, so the band is taken against the head's scale (rare; > 98 % bit-equal)
+    hscale = np.maximum(np.abs(q), np.abs(q).max(axis=-1, keepdims=True))
+    ok = within_band(gq, q, 1.0, scale=hscale)
+    bad = np.argwhere(~ok)
+    assert ok.all() and np.mean(gq == q) > 0.98, (np.mean(gq == q), len(bad), bad[:4].tolist(),
+                                                  [(float(gq[tuple(i)]), float(q[tuple(i)])) for i in bad[:4]])
     kcg, vcg = host(kc), host(vc).transpose(0, 1, 3, 2)
     assert within_band(kcg[:, :, past:past + S], k, 1.0).all()
     assert (vcg[:, :, past:past + S] == v).all()
@@ -283,13 +291,17 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
     mask = np.ones((B, Cmax), np.uint8)
     mask[1, :3] = 0
     ctxlen = past + S
-    for CH, n_split in ((64, (ctxlen + 63) // 64), (256, (ctxlen + 255) // 256)):
-        ws = torch.zeros(N.load().mtts_k_attention_ws_bytes(M, Hq, D, n_split) // 4 + 1, dtype=torch.float32,
-                         device="cuda")
+    for CH, n_split in ((64, (ctxlen + 63) // 64), (256, (ctxlen + 255) // 256), ("flash", 0)):
         out = torch.zeros(M, Hq * D, dtype=torch.bfloat16, device="cuda")
         md = torch.from_numpy(mask).cuda()
-        N.call("mtts_k_attention", P(qo), P(kc), P(vc), P(md), P(pos), P(out), P(ws),
-               M, S, Hq, Hkv, D, Cmax, CH, n_split, None)
+        if CH == "flash":  # the prefill path's MFMA flash kernel
+            N.call("mtts_k_attention_prefill", P(qo), P(kc), P(vc), P(md), P(pos), P(out), M, S, Hq, Hkv, D, Cmax,
+                   None)
+        else:
+            ws = torch.zeros(N.load().mtts_k_attention_ws_bytes(M, Hq, D, n_split) // 4 + 1, dtype=torch.float32,
+                             device="cuda")
+            N.call("mtts_k_attention", P(qo), P(kc), P(vc), P(md), P(pos), P(out), P(ws),
+                   M, S, Hq, Hkv, D, Cmax, CH, n_split, None)
         torch.cuda.synchronize()
         K = kcg[:, :, :ctxlen]
         V = vcg[:, :, :ctxlen]
