@@ -144,6 +144,10 @@ class Engine:
         V, A = self.cfg.vocab, self.cfg.audio_vocab + 1
         return [logits[:, :V]] + [logits[:, V + j * A: V + (j + 1) * A] for j in range(self.cfg.n_vq)]
 
+    def session(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor], max_new_tokens: int,
+                sampling: N.MttsSampling, forced_text: Optional[torch.Tensor] = None) -> "GenerateSession":
+        return GenerateSession(self, input_ids, attention_mask, max_new_tokens, sampling, forced_text)
+
     def generate_ids(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor], max_new_tokens: int,
                      sampling: N.MttsSampling, forced_text: Optional[torch.Tensor] = None, chunk: int = 16):
         """Runs the whole device loop; returns generation_ids [B, T + n, 1+n_vq] (prompt included)."""
@@ -159,6 +163,53 @@ class Engine:
                                        _ptr(forced), chunk, ctypes.byref(n), _stream_ptr(self.device)), "generate")
         out = torch.empty(B, T + n.value, C, dtype=torch.int64, device=self.device)
         N.check(N.load().mtts_generate_fetch(self._h, _ptr(out), n.value, _stream_ptr(self.device)), "fetch")
+        return out
+
+
+class GenerateSession:
+    """Step-wise form of Engine.generate_ids for streaming: begin (prefill + step 0), then
+    decode chunks of hipGraph steps, polling and fetching the generation rows in between."""
+
+    def __init__(self, eng: "Engine", input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor],
+                 max_new_tokens: int, sampling: N.MttsSampling, forced_text: Optional[torch.Tensor] = None):
+        self.eng = eng
+        self.B, self.T, self.C = input_ids.shape
+        self.max_new = max_new_tokens
+        self._ids = input_ids.to(eng.device, torch.int64).contiguous()
+        self._mask = None if attention_mask is None else attention_mask.to(eng.device, torch.uint8).contiguous()
+        self._forced = None if forced_text is None else forced_text.to(eng.device, torch.int32).contiguous()
+        self._sp = sampling
+        N.check(N.load().mtts_generate_begin(eng._h, _ptr(self._ids), _ptr(self._mask), self.B, self.T,
+                                             max_new_tokens, ctypes.byref(self._sp), _ptr(self._forced),
+                                             _stream_ptr(eng.device)), "generate_begin")
+        self.steps, self.done_step = 1, -1
+
+    def poll(self):
+        st, dn = ctypes.c_int(), ctypes.c_int()
+        N.check(N.load().mtts_generate_poll(self.eng._h, ctypes.byref(st), ctypes.byref(dn), None), "poll")
+        self.steps, self.done_step = st.value, dn.value
+        return self.steps, self.done_step
+
+    @property
+    def finished(self) -> bool:
+        return self.done_step >= 0 or self.steps >= self.max_new
+
+    @property
+    def n_rows(self) -> int:
+        """generated rows the reference's generation_ids would hold so far"""
+        return self.done_step + 1 if self.done_step >= 0 else self.steps
+
+    def decode(self, n_steps: int):
+        n = min(n_steps, self.max_new - self.steps)
+        if n > 0 and self.done_step < 0:
+            N.check(N.load().mtts_generate_decode(self.eng._h, n, _stream_ptr(self.eng.device)), "generate_decode")
+        return self.poll()
+
+    def fetch(self) -> torch.Tensor:
+        """generation_ids [B, T + n_rows, 1 + n_vq] (prompt included) so far"""
+        out = torch.empty(self.B, self.T + self.n_rows, self.C, dtype=torch.int64, device=self.eng.device)
+        N.check(N.load().mtts_generate_fetch(self.eng._h, _ptr(out), self.n_rows, _stream_ptr(self.eng.device)),
+                "fetch")
         return out
 
 

@@ -102,7 +102,7 @@ class MossTTSDelayModel(MossTTSDelayPreTrainedModel):
         want_c = max(ctx, int(os.environ.get("MTTS_MAX_CTX", "4096")))
         if self._engine is None:
             ecfg = EngineConfig.from_hf(self.config, max_batch=want_b, max_ctx=want_c,
-                                        max_prefill_tokens=max(8192, want_c))
+                                        max_prefill_tokens=int(os.environ.get("MTTS_MAX_PREFILL", max(8192, want_c))))
             eng = Engine(ecfg, self._device_index())
             for name, p in self.state_dict().items():
                 if "rotary_emb" in name:
@@ -170,3 +170,48 @@ class MossTTSDelayModel(MossTTSDelayPreTrainedModel):
         starts = find_last_equal_C(input_ids[..., 0], self.config.im_start_token_id) + 3
         lengths = T - starts
         return [(lengths[b], gen[b, int(starts[b]):]) for b in range(B)]
+
+    @torch.inference_mode()
+    def generate_stream(self, input_ids: torch.LongTensor, attention_mask: Optional[torch.Tensor] = None,
+                        max_new_tokens: int = 1000, chunk_steps: int = 16, text_temperature: float = 1.5,
+                        text_top_p: float = 1.0, text_top_k: int = 50, audio_temperature: float = 1.7,
+                        audio_top_p: float = 0.8, audio_top_k: int = 25, audio_repetition_penalty: float = 1.0,
+                        forced_text: Optional[torch.Tensor] = None):
+        """Streaming form of `generate` (the reference has none).  Decodes in
+        chunks of `chunk_steps` hipGraph steps and yields, after each chunk, the audio frames
+        that became complete: frame f of the delay pattern is final once generated row
+        f + n_vq - 1 exists (`processing_moss_tts.py:515-537`).  Yields lists (one per batch
+        row) of LongTensor [n_new_frames, n_vq] (de-delayed, all-pad frames dropped, on the
+        device); concatenated per row they equal `split_audio_segments` of the generate()
+        output.  A codec decoder can consume each chunk as it arrives."""
+        from .processing_moss_tts import apply_de_delay_pattern
+        if input_ids.dim() != 3 or input_ids.shape[-1] != self.config.n_vq + 1:
+            raise ValueError("`Input_ids`'s shape should be exactly (batch_size, sequence_length, 1 + n_vq).")
+        B, T, _ = input_ids.shape
+        n_vq, pad = self.config.n_vq, self.config.audio_pad_code
+        eng = self.engine(B, T + max_new_tokens)
+        seed = int(torch.randint(0, 2 ** 62, (1,)).item())
+        sp = sampling_params(text_temperature=text_temperature, text_top_p=text_top_p, text_top_k=text_top_k,
+                             audio_temperature=audio_temperature, audio_top_p=audio_top_p, audio_top_k=audio_top_k,
+                             audio_repetition_penalty=audio_repetition_penalty, seed=seed)
+        starts = (find_last_equal_C(input_ids[..., 0], self.config.im_start_token_id) + 3).tolist()
+        sess = eng.session(input_ids, attention_mask, max_new_tokens, sp, forced_text=forced_text)
+        sess.poll()
+        emitted = [0] * B  # complete frames (pad frames included) already examined per row
+        while True:
+            final = sess.finished
+            gen = sess.fetch()
+            out = []
+            for b in range(B):
+                a = gen[b, int(starts[b]):, 1:]
+                n_complete = a.shape[0] - n_vq + 1
+                if n_complete <= emitted[b]:
+                    out.append(a.new_zeros((0, n_vq)))
+                    continue
+                frames = apply_de_delay_pattern(a[: n_complete + n_vq - 1])[emitted[b]:n_complete]
+                emitted[b] = n_complete
+                out.append(frames[~(frames == pad).all(dim=1)])
+            yield out
+            if final:
+                return
+            sess.decode(chunk_steps)
