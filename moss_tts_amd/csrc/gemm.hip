@@ -129,9 +129,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemvArgs a) {
 // 16-byte fragment a wave loads feeds WN (weights) or WR (activations) MFMAs.  The two
 // waves that share a weight (or token) stripe read it through the CU's L1.  SwiGLU takes
 // WR/2 gate|up tile pairs per wave.
-template <int WR, int WN, int EPI>
+template <int WR, int WN, int EPI, int U>
 __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
-  constexpr int U = 2;  // k-tiles in flight per wave
+  // U: k-tiles in flight per wave (the k loop is latency-bound for short prompts)
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int wr = wave & 1, wm = wave >> 1;
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
     xok[j] = m < a.B;
     xbase[j] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[j] ? m : 0) * a.ldx + g4 * 8);
   }
-  for (int kt = 0; kt < KT; kt += U) {  // KT % U == 0 (K % 64 == 0 checked by the launcher)
+  for (int kt = 0; kt < KT; kt += U) {  // KT % U == 0 (checked by the launcher)
     u32x4 wa[WR][U], xb[WN][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -241,7 +241,10 @@ static void gemm2_launch(GemvArgs a, hipStream_t s) {
   a.n_row_tiles = (EPI == EPI_SWIGLU ? 2 : 1) * ((a.N + 15) / 16);
   const int mt = (a.B + 15) / 16;
   const dim3 grid((a.n_row_tiles + 2 * WR - 1) / (2 * WR), (mt + 2 * WN - 1) / (2 * WN));
-  hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI>), grid, dim3(256), 0, s, a);
+  static const int u = getenv("MTTS_GEMM_U") ? atoi(getenv("MTTS_GEMM_U")) : 4;
+  if (u == 8 && a.KT % 8 == 0) hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 8>), grid, dim3(256), 0, s, a);
+  else if (u >= 4 && a.KT % 4 == 0) hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 2>), grid, dim3(256), 0, s, a);
 }
 
 hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
