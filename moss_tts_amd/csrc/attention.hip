@@ -412,8 +412,10 @@ __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(DecAttnArgs a) {
       pr[jj] = *reinterpret_cast<const uint32_t*>(row + (size_t)hd * D + 2 * lane);
       if (j <= G) {
         pw[jj] = *reinterpret_cast<const uint32_t*>((j < G ? a.qn_w : a.kn_w) + 2 * lane);
-        pc[jj] = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
-        ps[jj] = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
+        if (a.cos_t) {
+          pc[jj] = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
+          ps[jj] = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
+        }
       }
     }
   }
@@ -473,8 +475,10 @@ __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(DecAttnArgs a) {
     const int partner = lo ? lane + q4 : lane - q4;
     const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
     const float sg = lo ? -1.f : 1.f;
-    const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
-    const float o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+    // no cos table: attention without positional embedding (MossTTSLocal's depth
+    // transformer, moss_tts_local/modeling_moss_tts.py:126-176)
+    const float o0 = a.cos_t ? rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)) : n0;
+    const float o1 = a.cos_t ? rbf(rbf(n1 * c1) + rbf(sg * p1 * s1)) : n1;
     if (act) {
       if (j < G) {
         q_s[j][2 * lane] = f2bf(o0);

@@ -5,111 +5,13 @@
 //   MossTTSDelayModel.forward   moss_tts_delay/modeling_moss_tts.py:225-300
 //   MossTTSDelayModel.generate  moss_tts_delay/modeling_moss_tts.py:392-525
 //   Qwen3Model.forward          transformers/models/qwen3/modeling_qwen3.py:367-427
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <cmath>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <string>
-#include <unordered_map>
-#include <vector>
-
-#include "../../include/mtts.h"
-#include "kernels.h"
-
-using namespace mtts;
+#include "engine_internal.h"
 
 static thread_local std::string g_err;
-static int fail(int code, const std::string& msg) {
+int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
-#define HIPCHK(x)                                                                              \
-  do {                                                                                         \
-    hipError_t e_ = (x);                                                                       \
-    if (e_ != hipSuccess) return fail(MTTS_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
-  } while (0)
-
-namespace {
-
-constexpr int CH_DECODE = 64;
-constexpr int CH_PREFILL = 256;
-constexpr int TEXT_PARTS = 64;
-
-struct LayerW {
-  bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
-};
-
-size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
-
-}  // namespace
-
-struct mtts_engine {
-  mtts_config c{};
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  int qkv_rows = 0, audio_rows = 0, heads_rows = 0, heads_ld = 0;
-  std::vector<LayerW> L;
-  bf16_t *emb_text = nullptr, *emb_audio = nullptr, *final_norm = nullptr, *heads = nullptr;
-  bf16_t *kc = nullptr, *vc = nullptr;
-  size_t layer_kv = 0;  // elements per layer in kc / vc
-  bf16_t *cos_t = nullptr, *sin_t = nullptr;
-  uint8_t* mask = nullptr;
-  // workspace
-  int Mmax = 0;
-  float* ss = nullptr;  // [Mmax, H/16] per-tile sums of squares of the residual stream
-  bf16_t *h = nullptr, *xn = nullptr, *qkvb = nullptr, *qb = nullptr, *attnb = nullptr, *act = nullptr;
-  float* part = nullptr;
-  size_t part_floats = 0;
-  bf16_t* logits = nullptr;
-  int* d_pos = nullptr;  // pos_base for teacher-forced forwards / prefill
-  int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
-  int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
-  bool full_text_head = false;
-  bool gemv_prefill = false;
-  bool unfused_attn = false;
-  bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)    // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)    // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)  // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
-  // generate state
-  GenDev* st = nullptr;
-  GenDev hst{};
-  int *is_stopping = nullptr, *is_audio = nullptr, *text_cand = nullptr, *audio_cand = nullptr, *part_idx = nullptr;
-  int64_t *audio_len = nullptr, *delayed = nullptr, *cur_ids = nullptr, *gen_ids = nullptr;
-  uint8_t* seen = nullptr;
-  float* part_val = nullptr;
-  const int* forced = nullptr;
-  int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
-  struct Graph { hipGraphExec_t exec; const int* forced; };
-  std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
-  std::vector<void*> allocs;      // weights
-  std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)
-  bool cap_mode = false;
-  bool unfused_norm = false;  // MTTS_UNFUSED_NORM=1: always run the separate RMSNorm kernel (A/B timing)
-  int nw[5] = {0, 0, 0, 0, 0};  // waves-per-block overrides (MTTS_NW="qkv,o,gu,down,heads"; 0 = auto)
-  bf16_t* staging = nullptr;
-  size_t staging_bytes = 0;
-  uint64_t step_weight_bytes = 0;
-
-  template <class T>
-  int alloc(T** p, size_t n) {
-    void* q = nullptr;
-    if (n == 0) n = 1;
-    if (hipMalloc(&q, n * sizeof(T)) != hipSuccess) return fail(MTTS_E_OOM, "hipMalloc failed (" + std::to_string(n * sizeof(T)) + " B)");
-    (cap_mode ? cap_allocs : allocs).push_back(q);
-    *p = reinterpret_cast<T*>(q);
-    return 0;
-  }
-  GenBufs bufs() const {
-    GenBufs g;
-    g.st = st; g.logits = logits; g.is_stopping = is_stopping; g.is_audio = is_audio;
-    g.audio_len = audio_len; g.delayed = delayed; g.cur_ids = cur_ids; g.gen_ids = gen_ids; g.mask = mask;
-    g.seen = seen; g.part_val = part_val; g.part_idx = part_idx; g.text_cand = text_cand; g.audio_cand = audio_cand;
-    g.forced = forced;
-    return g;
-  }
-};
 
 // ---------------------------------------------------------------------------
 // RoPE table (TF/.../modeling_qwen3.py:106-137): inv_freq = 1/theta^(2i/D) with the power
@@ -291,7 +193,7 @@ extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0;
 
 // ---------------------------------------------------------------------------
 // weight loading by reference state_dict name
-static int ensure_staging(mtts_engine* e, size_t bytes) {
+int ensure_staging(mtts_engine* e, size_t bytes) {
   if (e->staging_bytes >= bytes) return 0;
   if (e->staging) hipFree(e->staging);
   e->staging = nullptr;
@@ -301,7 +203,7 @@ static int ensure_staging(mtts_engine* e, size_t bytes) {
   return 0;
 }
 
-static bool parse_layer(const char* name, int* layer, std::string* rest) {
+bool parse_layer(const char* name, int* layer, std::string* rest) {
   const char* p = "language_model.layers.";
   if (std::strncmp(name, p, std::strlen(p)) != 0) return false;
   const char* q = name + std::strlen(p);
@@ -426,16 +328,28 @@ extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
 // into the GEMV prologue (normalised rows staged in LDS per block, no extra launch); larger
 // ones run the single-pass rmsnorm_ss kernel into e->xn first.  Both read the residual
 // stream's per-16-column sums of squares e->ss.
-static int normed_input(mtts_engine* e, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s) {
-  const int H = e->c.hidden, NT = H / 16;
+int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s) {
+  const int H = st.H, NT = H / 16;
   if (norm_lds_bytes(M, H) <= NORM_LDS_MAX && !e->unfused_norm) {
-    g.x = e->h; g.ldx = H;
-    g.ss_in = e->ss; g.ld_ss = NT; g.n_ss = NT; g.nw = nw; g.eps = e->c.rms_eps;
+    g.x = st.h; g.ldx = H;
+    g.ss_in = st.ss; g.ld_ss = NT; g.n_ss = NT; g.nw = nw; g.eps = e->c.rms_eps;
     return 0;
   }
-  HIPCHK(rmsnorm_ss(e->h, 0, H, e->ss, 0, NT, nw, e->xn, M, H, e->c.rms_eps, s));
-  g.x = e->xn; g.ldx = H;
+  HIPCHK(rmsnorm_ss(st.h, 0, H, st.ss, 0, NT, nw, st.xn, M, H, e->c.rms_eps, s));
+  g.x = st.xn; g.ldx = H;
   return 0;
+}
+
+Stack backbone_stack(mtts_engine* e) {
+  const mtts_config& c = e->c;
+  Stack st;
+  st.L = e->L.data(); st.layers = c.layers; st.H = c.hidden; st.Hq = c.n_heads; st.Hkv = c.n_kv; st.D = c.head_dim;
+  st.I = c.inter; st.qkv_rows = e->qkv_rows;
+  st.kc = e->kc; st.vc = e->vc; st.layer_kv = e->layer_kv; st.Cmax = c.max_ctx;
+  st.cos_t = e->cos_t; st.sin_t = e->sin_t; st.mask = e->mask;
+  st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
+  st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt;
+  return st;
 }
 
 // ---------------------------------------------------------------------------
@@ -448,72 +362,91 @@ static int normed_input(mtts_engine* e, GemvArgs& g, const bf16_t* nw, int M, hi
 // token-parallel projections: the decode GEMV for a handful of rows, the prefill GEMM
 // (weights read once per 256 tokens instead of once per 32) beyond that
 constexpr int GEMM_MIN_ROWS = 33;
-static hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
+hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
   if (g.B >= GEMM_MIN_ROWS && !g.ss_in && !e->gemv_prefill) return gemm_ex(g, epi, s);
   return gemv_ex(g, epi, s);
 }
 
-static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
-                        int n_split, bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr,
-                        bool heads = true) {
-  const mtts_config& c = e->c;
-  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter, C = c.n_vq + 1;
+// the decoder layers of a stack over rows [b0, b0+B), S tokens each, token s of a row at
+// position *pos_base + s
+int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int* pos_base, int CH, int n_split,
+               hipStream_t s) {
+  const int H = st.H, D = st.D, Hq = st.Hq, Hkv = st.Hkv, I = st.I;
   const int M = B * S;
   const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
-  HIPCHK(embed(ids, C, e->emb_text, e->emb_audio, e->audio_rows, H, e->h, M, s, e->ss, NT));
-  const float eps = c.rms_eps;
+  const float eps = e->c.rms_eps;
   const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn;
-  for (int l = 0; l < c.layers; ++l) {
-    const LayerW& w = e->L[l];
-    bf16_t* kc = e->kc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
-    bf16_t* vc = e->vc + l * e->layer_kv + (size_t)b0 * Hkv * c.max_ctx * D;
-    GemvArgs g = gemv_args(w.qkv, e->xn, H, e->qkvb, e->qkv_rows, M, e->qkv_rows, H);
-    if (int rc = normed_input(e, g, w.in_norm, M, s)) return rc;
+  for (int l = 0; l < st.layers; ++l) {
+    const LayerW& w = st.L[l];
+    bf16_t* kc = st.kc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
+    bf16_t* vc = st.vc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
+    GemvArgs g = gemv_args(w.qkv, st.xn, H, st.qkvb, st.qkv_rows, M, st.qkv_rows, H);
+    if (int rc = normed_input(e, st, g, w.in_norm, M, s)) return rc;
     g.force_nw = e->nw[0];
     HIPCHK(proj(e, g, EPI_STORE, s));
     if (S == 1) {
       DecAttnArgs da{};
-      da.qkv = e->qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = e->cos_t; da.sin_t = e->sin_t;
-      da.kc = kc; da.vc = vc; da.mask = e->mask + (size_t)b0 * c.max_ctx; da.pos = pos_base; da.out = e->attnb;
-      da.part = e->part; da.cnt = e->att_cnt;
+      da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
+      da.kc = kc; da.vc = vc; da.mask = st.mask + (size_t)b0 * st.Cmax; da.pos = pos_base; da.out = st.attnb;
+      da.part = st.part; da.cnt = st.att_cnt;
       // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
       da.publish_only = fuse_attn ? 1 : 0;
-      da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = c.max_ctx; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
+      da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
       HIPCHK(attn_decode(da, B, s));
     } else {
+      if (!st.cos_t) return fail(MTTS_E_UNSUPPORTED, "multi-token forward of a stack without positions");
       QKRopeArgs qa;
-      qa.qkv = e->qkvb; qa.q_out = e->qb; qa.kc = kc; qa.vc = vc;
-      qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = e->cos_t; qa.sin_t = e->sin_t;
-      qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = c.max_ctx; qa.eps = eps; qa.M = M;
+      qa.qkv = st.qkvb; qa.q_out = st.qb; qa.kc = kc; qa.vc = vc;
+      qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = st.cos_t; qa.sin_t = st.sin_t;
+      qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = st.Cmax; qa.eps = eps; qa.M = M;
       HIPCHK(qk_norm_rope(qa, s));
       AttnArgs aa;
-      aa.q = e->qb; aa.kc = kc; aa.vc = vc; aa.mask = e->mask + (size_t)b0 * c.max_ctx; aa.pos_base = pos_base;
-      aa.part_o = e->part; aa.part_ml = e->part + (size_t)M * n_split * Hq * D; aa.out = e->attnb;
-      aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = c.max_ctx; aa.CH = CH; aa.n_split = n_split; aa.M = M;
+      aa.q = st.qb; aa.kc = kc; aa.vc = vc; aa.mask = st.mask + (size_t)b0 * st.Cmax; aa.pos_base = pos_base;
+      aa.part_o = st.part; aa.part_ml = st.part + (size_t)M * n_split * Hq * D; aa.out = st.attnb;
+      aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = st.Cmax; aa.CH = CH; aa.n_split = n_split; aa.M = M;
       aa.scale = 1.0f / std::sqrt((float)D);
       if (e->old_prefill_attn) HIPCHK(attention(aa, s));
       else HIPCHK(attention_prefill(aa, s));
     }
-    g = gemv_args(w.o, e->attnb, Hq * D, e->h, H, M, H, Hq * D);
-    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
+    g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
+    g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
     if (fuse_attn) {
-      g.attn.part = e->part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
-      g.attn.ns = attn_decode_splits(c.max_ctx); g.attn.kb = attn_decode_keys_per_block();
+      g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
+      g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
     }
     HIPCHK(proj(e, g, EPI_RESADD, s));
-    g = gemv_args(w.gu, e->xn, H, e->act, I, M, I, H);
-    if (int rc = normed_input(e, g, w.post_norm, M, s)) return rc;
+    g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
+    if (int rc = normed_input(e, st, g, w.post_norm, M, s)) return rc;
     g.force_nw = e->nw[2];
     HIPCHK(proj(e, g, EPI_SWIGLU, s));
-    g = gemv_args(w.down, e->act, I, e->h, H, M, H, I);
-    g.res = e->h; g.ldres = H; g.ss_out = e->ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
+    g = gemv_args(w.down, st.act, I, st.h, H, M, H, I);
+    g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
     HIPCHK(proj(e, g, EPI_RESADD, s));
+  }
+  return 0;
+}
+
+int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH,
+                 int n_split, bf16_t* logits_out, hipStream_t s, const int* text_gate, bool heads, bf16_t* hidden,
+                 int n_embed) {
+  const mtts_config& c = e->c;
+  const int H = c.hidden, C = c.n_vq + 1;
+  const int M = B * S;
+  const int NT = H / 16;
+  const float eps = c.rms_eps;
+  const Stack st = backbone_stack(e);
+  HIPCHK(embed(ids, n_embed > 0 ? n_embed : C, e->emb_text, e->emb_audio, e->audio_rows, H, e->h, M, s, e->ss, NT, C));
+  if (int rc = run_layers(e, st, b0, B, S, pos_base, CH, n_split, s)) return rc;
+  if (!heads && hidden) {  // final-normed hidden state of each row's last token (MossTTSLocal)
+    HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
+                      e->final_norm, hidden, B, H, eps, s));
+    return 0;
   }
   if (!heads) return 0;  // a leading chunk of a position-chunked prefill: KV cache only
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
   GemvArgs g = gemv_args(e->heads, e->xn, H, logits_out, e->heads_ld, B, e->heads_rows, H);
   if (S == 1) {
-    if (int rc = normed_input(e, g, e->final_norm, B, s)) return rc;
+    if (int rc = normed_input(e, st, g, e->final_norm, B, s)) return rc;
   } else {
     HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
                       e->final_norm, e->xn, B, H, eps, s));
@@ -538,7 +471,8 @@ static int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S
 // chunked so that rows x S <= max_prefill_tokens; a prompt longer than that is prefilled one
 // row at a time in position chunks of max_prefill_tokens (each chunk attends to the cache the
 // previous ones wrote; only the last chunk evaluates the heads) -- the long-form (TTSD) path.
-static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s) {
+int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s,
+                    bf16_t* hidden, int n_embed) {
   const mtts_config& c = e->c;
   const int C = c.n_vq + 1;
   const int CH = S == 1 ? CH_DECODE : CH_PREFILL;
@@ -549,8 +483,10 @@ static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int
         const int len = std::min(P, S - s0);
         HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->d_pos), past + s0, 1, s));
         const int n_split = (past + s0 + len + CH - 1) / CH;
+        const bool last = s0 + len == S;
         int rc = forward_rows(e, ids + ((size_t)b * S + s0) * C, b, 1, len, e->d_pos, CH, n_split,
-                              logits_out + (size_t)b * e->heads_ld, s, nullptr, s0 + len == S);
+                              logits_out ? logits_out + (size_t)b * e->heads_ld : nullptr, s, nullptr,
+                              last && !hidden, last && hidden ? hidden + (size_t)b * c.hidden : nullptr, n_embed);
         if (rc) return rc;
       }
     }
@@ -562,7 +498,8 @@ static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int
   for (int b0 = 0; b0 < B; b0 += rows_per) {
     const int nb = std::min(rows_per, B - b0);
     int rc = forward_rows(e, ids + (size_t)b0 * S * C, b0, nb, S, e->d_pos, CH, n_split,
-                          logits_out + (size_t)b0 * e->heads_ld, s);
+                          logits_out ? logits_out + (size_t)b0 * e->heads_ld : nullptr, s, nullptr, !hidden,
+                          hidden ? hidden + (size_t)b0 * c.hidden : nullptr, n_embed);
     if (rc) return rc;
   }
   return 0;
@@ -572,13 +509,13 @@ static int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int
 // stream by events.  A NULL caller stream is the legacy default stream (what torch's
 // default `cuda_stream` handle is), which a non-blocking stream does NOT synchronise with
 // implicitly, so it gets the same event fences.
-static hipStream_t enter(mtts_engine* e, void* user) {
+hipStream_t enter(mtts_engine* e, void* user) {
   hipSetDevice(e->device);
   hipEventRecord(e->ev_in, (hipStream_t)user);
   hipStreamWaitEvent(e->stream, e->ev_in, 0);
   return e->stream;
 }
-static void leave(mtts_engine* e, void* user) {
+void leave(mtts_engine* e, void* user) {
   hipEventRecord(e->ev_out, e->stream);
   hipStreamWaitEvent((hipStream_t)user, e->ev_out, 0);
 }

@@ -1,0 +1,142 @@
+// Engine internals shared by engine.cpp (MossTTSDelay) and local.cpp (MossTTSLocal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mtts.h"
+#include "kernels.h"
+
+using namespace mtts;
+
+int fail(int code, const std::string& msg);
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess) return fail(MTTS_E_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int CH_DECODE = 64;
+constexpr int CH_PREFILL = 256;
+constexpr int TEXT_PARTS = 64;
+
+struct LayerW {
+  bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
+};
+
+// A stack of Qwen3 decoder layers with its KV cache and activation buffers: the backbone,
+// or MossTTSLocal's depth transformer (no positional embedding: cos_t == nullptr).
+struct Stack {
+  const LayerW* L = nullptr;
+  int layers = 0, H = 0, Hq = 0, Hkv = 0, D = 0, I = 0, qkv_rows = 0;
+  bf16_t *kc = nullptr, *vc = nullptr;
+  size_t layer_kv = 0;
+  int Cmax = 0;
+  const bf16_t *cos_t = nullptr, *sin_t = nullptr;
+  uint8_t* mask = nullptr;  // [Bmax][Cmax]
+  bf16_t *h = nullptr, *xn = nullptr, *qkvb = nullptr, *qb = nullptr, *attnb = nullptr, *act = nullptr;
+  float* ss = nullptr;      // per-16-column sums of squares of h
+  float* part = nullptr;
+  int* att_cnt = nullptr;
+};
+
+inline size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
+
+struct LocalParts;  // MossTTSLocal depth stage (local.cpp)
+
+struct mtts_engine {
+  mtts_config c{};
+  LocalParts* lp = nullptr;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  int qkv_rows = 0, audio_rows = 0, heads_rows = 0, heads_ld = 0;
+  std::vector<LayerW> L;
+  bf16_t *emb_text = nullptr, *emb_audio = nullptr, *final_norm = nullptr, *heads = nullptr;
+  bf16_t *kc = nullptr, *vc = nullptr;
+  size_t layer_kv = 0;  // elements per layer in kc / vc
+  bf16_t *cos_t = nullptr, *sin_t = nullptr;
+  uint8_t* mask = nullptr;
+  // workspace
+  int Mmax = 0;
+  float* ss = nullptr;  // [Mmax, H/16] per-tile sums of squares of the residual stream
+  bf16_t *h = nullptr, *xn = nullptr, *qkvb = nullptr, *qb = nullptr, *attnb = nullptr, *act = nullptr;
+  float* part = nullptr;
+  size_t part_floats = 0;
+  bf16_t* logits = nullptr;
+  int* d_pos = nullptr;  // pos_base for teacher-forced forwards / prefill
+  int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
+  int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
+  bool full_text_head = false;    // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
+  bool gemv_prefill = false;      // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)
+  bool unfused_attn = false;      // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)
+  bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)
+  // generate state
+  GenDev* st = nullptr;
+  GenDev hst{};
+  int *is_stopping = nullptr, *is_audio = nullptr, *text_cand = nullptr, *audio_cand = nullptr, *part_idx = nullptr;
+  int64_t *audio_len = nullptr, *delayed = nullptr, *cur_ids = nullptr, *gen_ids = nullptr;
+  uint8_t* seen = nullptr;
+  float* part_val = nullptr;
+  const int* forced = nullptr;
+  int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
+  struct Graph { hipGraphExec_t exec; const int* forced; };
+  std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
+  std::vector<void*> allocs;      // weights
+  std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)
+  bool cap_mode = false;
+  bool unfused_norm = false;  // MTTS_UNFUSED_NORM=1: always run the separate RMSNorm kernel (A/B timing)
+  int nw[5] = {0, 0, 0, 0, 0};  // waves-per-block overrides (MTTS_NW="qkv,o,gu,down,heads"; 0 = auto)
+  bf16_t* staging = nullptr;
+  size_t staging_bytes = 0;
+  uint64_t step_weight_bytes = 0;
+
+  template <class T>
+  int alloc(T** p, size_t n) {
+    void* q = nullptr;
+    if (n == 0) n = 1;
+    if (hipMalloc(&q, n * sizeof(T)) != hipSuccess) return fail(MTTS_E_OOM, "hipMalloc failed (" + std::to_string(n * sizeof(T)) + " B)");
+    (cap_mode ? cap_allocs : allocs).push_back(q);
+    *p = reinterpret_cast<T*>(q);
+    return 0;
+  }
+  GenBufs bufs() const {
+    GenBufs g;
+    g.st = st; g.logits = logits; g.is_stopping = is_stopping; g.is_audio = is_audio;
+    g.audio_len = audio_len; g.delayed = delayed; g.cur_ids = cur_ids; g.gen_ids = gen_ids; g.mask = mask;
+    g.seen = seen; g.part_val = part_val; g.part_idx = part_idx; g.text_cand = text_cand; g.audio_cand = audio_cand;
+    g.forced = forced;
+    return g;
+  }
+};
+
+// ---- shared engine internals (engine.cpp) ----
+int ensure_staging(mtts_engine* e, size_t bytes);
+bool parse_layer(const char* name, int* layer, std::string* rest);
+int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s);
+Stack backbone_stack(mtts_engine* e);
+hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s);
+int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int* pos_base, int CH, int n_split,
+               hipStream_t s);
+// backbone forward; heads == false: KV cache only, or (hidden != nullptr) the final-normed
+// hidden state of each row's last token into hidden [B, H]; n_embed: channels summed (0 = all)
+int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH, int n_split,
+                 bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr, bool heads = true,
+                 bf16_t* hidden = nullptr, int n_embed = 0);
+int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s,
+                    bf16_t* hidden = nullptr, int n_embed = 0);
+hipStream_t enter(mtts_engine* e, void* user);
+void leave(mtts_engine* e, void* user);
+// local.cpp (MossTTSLocal)
+int local_create(mtts_engine* e);
+int local_alloc_capacity(mtts_engine* e);
+void local_destroy(mtts_engine* e);
+// 1: the name belongs to the local stage and was loaded (or failed: *rc set); 0: not a local name
+int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev, int* rc);

@@ -157,8 +157,10 @@ hipError_t gemm_ex(const GemvArgs& a, int epi, hipStream_t s);
 hipError_t pack_weight(const bf16_t* src, bf16_t* dst, int rows, int K, int row_offset, int interleave, int which,
                        hipStream_t s);
 // norm_rope.hip
+// sum of the embeddings of channels 0..C-1 (channel 0 from emb_text, j >= 1 from table j-1 of
+// emb_audio); ids row stride ld_ids (0: C)
 hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
-                 bf16_t* h, int M, hipStream_t s, float* ss_out = nullptr, int ld_ss = 0);
+                 bf16_t* h, int M, hipStream_t s, float* ss_out = nullptr, int ld_ss = 0, int ld_ids = 0);
 hipError_t rmsnorm(const bf16_t* x, size_t x_off, size_t x_stride, const bf16_t* w, bf16_t* y, int M, int H, float eps,
                    hipStream_t s);
 hipError_t rmsnorm_ss(const bf16_t* x, size_t x_off, size_t x_stride, const float* ss, size_t ss_off, size_t ss_stride,

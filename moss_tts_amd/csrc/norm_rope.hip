@@ -12,12 +12,13 @@ namespace mtts {
 constexpr int EMB_COLS = 256, EMB_MAXC = 64;
 __global__ __launch_bounds__(256) void embed_kernel(const int64_t* __restrict__ ids, int C, const bf16_t* __restrict__ emb_text,
                                                     const bf16_t* __restrict__ emb_audio, int audio_rows, int H,
-                                                    bf16_t* __restrict__ h, float* __restrict__ ss_out, int ld_ss) {
+                                                    bf16_t* __restrict__ h, float* __restrict__ ss_out, int ld_ss,
+                                                    int ld_ids) {
   constexpr int LPT = (EMB_MAXC * EMB_COLS / 8 + 255) / 256;  // 16-byte loads per thread (max)
   __shared__ __attribute__((aligned(16))) bf16_t rows_s[EMB_MAXC][EMB_COLS];
   __shared__ int64_t id_s[EMB_MAXC];
   const int m = blockIdx.x, c0 = blockIdx.y * EMB_COLS, t = threadIdx.x;
-  if (t < C) id_s[t] = ids[(size_t)m * C + t];
+  if (t < C) id_s[t] = ids[(size_t)m * ld_ids + t];
   __syncthreads();
   const int ncols = min(EMB_COLS, H - c0);
   const int cpr = ncols >> 3;
@@ -216,10 +217,11 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
 }
 
 hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t* emb_audio, int audio_rows, int H,
-                 bf16_t* h, int M, hipStream_t s, float* ss_out, int ld_ss) {
+                 bf16_t* h, int M, hipStream_t s, float* ss_out, int ld_ss, int ld_ids) {
   if (H % 16 || C < 1 || C > EMB_MAXC) return hipErrorInvalidValue;
+  if (ld_ids <= 0) ld_ids = C;
   hipLaunchKernelGGL(embed_kernel, dim3(M, (H + EMB_COLS - 1) / EMB_COLS), dim3(256), 0, s, ids, C, emb_text, emb_audio,
-                     audio_rows, H, h, ss_out, ld_ss);
+                     audio_rows, H, h, ss_out, ld_ss, ld_ids);
   return hipGetLastError();
 }
 

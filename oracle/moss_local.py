@@ -61,7 +61,7 @@ class LCfg:
 
 def tiny_lcfg(n_vq=4, **kw):
     c = LCfg(hidden=64, layers=2, n_heads=4, n_kv=2, head_dim=16, inter=128, n_vq=n_vq, rope_theta=10000.0,
-             local_hidden=48, local_layers=2, local_inter=96, mlp_ffn=80)
+             local_hidden=64, local_layers=2, local_inter=128, mlp_ffn=96)
     for k, v in kw.items():
         setattr(c, k, v)
     return c
@@ -114,7 +114,7 @@ def _scale(kind, shape):
         return 1.0, 0.0
     if kind == "norm":
         return 0.25, 1.0
-    return float(shape[-1]) ** -0.5 * 1.7, 0.0  # uniform(-1,1) * s: var ~ 1/K
+    return float(np.sqrt(3.0 / shape[-1])), 0.0  # uniform(-1,1) * s: var = 1/K (as oracle.moss_delay)
 
 
 def make_weights(cfg: LCfg, seed: int, dtype="bf16", eos_boost=0.0) -> Dict[str, np.ndarray]:
