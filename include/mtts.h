@@ -44,7 +44,16 @@ typedef struct mtts_config {
   int max_batch;          /* rows per generate() call */
   int max_ctx;            /* prompt + max_new_tokens */
   int max_prefill_tokens; /* rows x prompt tokens processed per prefill chunk */
+  /* model family: MTTS_MODEL_DELAY (MossTTSDelay) or MTTS_MODEL_LOCAL (MossTTSLocal:
+   * backbone + depth transformer, moss_tts_local/configuration_moss_tts.py:60-110) */
+  int model_kind;
+  int local_hidden, local_layers, local_inter; /* depth transformer (local_*_size) */
+  int local_mlp_ffn;                           /* additional_mlp_ffn_hidden_size of the adapters */
+  int eos_token_id;                            /* generation_config.eos_token_id (Local stop id) */
 } mtts_config;
+
+#define MTTS_MODEL_DELAY 0
+#define MTTS_MODEL_LOCAL 1
 
 /* generate() keyword arguments (modeling_moss_tts.py:393-405); temperature <= 0 = greedy */
 typedef struct mtts_sampling {
@@ -110,6 +119,31 @@ int mtts_generate(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_
                   int* n_rows, void* stream);
 /* copy generation_ids [B, T + n_rows, 1+n_vq] (prompt included) to out_dev */
 int mtts_generate_fetch(mtts_engine* eng, int64_t* out_dev, int n_rows, void* stream);
+
+/* ---- MossTTSLocal (model_kind == MTTS_MODEL_LOCAL) -------------------------------------
+ * Weights load by the reference names of moss_tts_local/modeling_moss_tts.py
+ * (model.embedding_list.{i}, model.language_model.*, local_transformer.*,
+ * speech_embedding_to_local_mlp.*, local_to_speech_embedding_mlps.{i}.*,
+ * layer_norm_before_lm_heads.{i}, lm_heads.{i}).  Poll and fetch are mtts_generate_poll /
+ * mtts_generate_fetch.  n_vq_for_inference < 0: all channels.
+ * Replaces CustomMixin._sample (moss_tts_local/modeling_moss_tts.py:315-477), greedy
+ * (do_samples all False); a positive temperature is rejected with MTTS_E_UNSUPPORTED. */
+int mtts_local_generate_begin(mtts_engine* eng, const int64_t* input_ids_dev, const uint8_t* attention_mask_dev, int B,
+                              int T, int max_new_tokens, int n_vq_for_inference, const mtts_sampling* sampling,
+                              void* stream);
+int mtts_local_generate_decode(mtts_engine* eng, int n_steps, void* stream);
+int mtts_local_generate(mtts_engine* eng, const int64_t* input_ids_dev, const uint8_t* attention_mask_dev, int B, int T,
+                        int max_new_tokens, int n_vq_for_inference, const mtts_sampling* sampling, int chunk_steps,
+                        int* n_rows, void* stream);
+/* Teacher-forced frame: backbone over S tokens at `past` (mask [B, past+S]), then the depth
+ * loop feeding forced_dev[b, i] ([B, 1+n_vq] int64) to channel i+1.  logits_dev receives
+ * channel i's logits at + i*B*ld (bf16 [n_ch][B][ld], ld >= vocab; audio pad column -inf). */
+int mtts_local_forward(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int S, int past,
+                       int n_vq_for_inference, const int64_t* forced_dev, uint16_t* logits_dev, int ld, void* stream);
+/* weight bytes one frame streams (backbone + n_ch x depth stage + heads) */
+int mtts_local_frame_bytes(const mtts_engine* eng, int n_vq_for_inference, uint64_t* bytes);
+/* bf16 MossTTSRMSNorm (no fp32 upcast, modeling_moss_tts.py:34-44), x/y [M, H] */
+int mtts_k_moss_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int H, float eps, void* stream);
 
 /* ---- kernel-level entry points (unit parity; device pointers, explicit shapes) ---- */
 /* pack W [rows,K] bf16 into MFMA tiles; interleave=1 places gate/up tile pairs */

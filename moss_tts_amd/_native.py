@@ -25,7 +25,9 @@ class MttsConfig(ctypes.Structure):
                                             "audio_start_token_id", "audio_end_token_id",
                                             "audio_user_slot_token_id", "audio_assistant_gen_slot_token_id",
                                             "audio_assistant_delay_slot_token_id", "audio_pad_code",
-                                            "max_batch", "max_ctx", "max_prefill_tokens")]
+                                            "max_batch", "max_ctx", "max_prefill_tokens", "model_kind",
+                                            "local_hidden", "local_layers", "local_inter", "local_mlp_ffn",
+                                            "eos_token_id")]
 
 
 class MttsSampling(ctypes.Structure):
@@ -58,6 +60,12 @@ _SIGS = {
     "mtts_generate_stats": (I, [P, P]),
     "mtts_generate_poll": (I, [P, ctypes.POINTER(I), ctypes.POINTER(I), P]),
     "mtts_generate": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, I, ctypes.POINTER(I), P]),
+    "mtts_local_generate_begin": (I, [P, P, P, I, I, I, I, ctypes.POINTER(MttsSampling), P]),
+    "mtts_local_generate_decode": (I, [P, I, P]),
+    "mtts_local_generate": (I, [P, P, P, I, I, I, I, ctypes.POINTER(MttsSampling), I, ctypes.POINTER(I), P]),
+    "mtts_local_forward": (I, [P, P, P, I, I, I, I, P, P, I, P]),
+    "mtts_local_frame_bytes": (I, [P, I, ctypes.POINTER(U64)]),
+    "mtts_k_moss_rmsnorm": (I, [P, P, P, I, I, F, P]),
     "mtts_generate_fetch": (I, [P, P, I, P]),
     "mtts_k_pack": (I, [P, P, I, I, I, I, I, P]),
     "mtts_k_packed_bytes": (SZ, [I, I]),

@@ -48,6 +48,7 @@ extern "C" int mtts_engine_destroy(mtts_engine* e) {
   if (!e) return 0;
   hipSetDevice(e->device);
   for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second.exec);
+  local_destroy(e);
   for (void* p : e->allocs) hipFree(p);
   for (void* p : e->cap_allocs) hipFree(p);
   if (e->staging) hipFree(e->staging);
@@ -112,6 +113,11 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MTTS_E_UNSUPPORTED, "GQA group must be 1/2/4/8");
   if ((c.vocab + TEXT_PARTS - 1) / TEXT_PARTS > 4096) return fail(MTTS_E_UNSUPPORTED, "text vocab too large");
   if (c.audio_vocab + 1 > 1040) return fail(MTTS_E_UNSUPPORTED, "audio vocab too large");
+  if (c.model_kind != MTTS_MODEL_DELAY && c.model_kind != MTTS_MODEL_LOCAL) return fail(MTTS_E_UNSUPPORTED, "model_kind");
+  if (c.model_kind == MTTS_MODEL_LOCAL &&
+      (c.local_hidden <= 0 || c.local_hidden % 64 || c.local_hidden > 4096 || c.local_inter <= 0 || c.local_inter % 32 ||
+       c.local_mlp_ffn <= 0 || c.local_mlp_ffn % 32 || c.local_layers <= 0 || c.n_vq + 1 > 64 || c.hidden % 64))
+    return fail(MTTS_E_UNSUPPORTED, "unsupported MossTTSLocal shape");
   if (hipSetDevice(device) != hipSuccess) return fail(MTTS_E_HIP, "hipSetDevice failed");
   mtts_engine* e = new mtts_engine();
   e->c = c;
@@ -155,12 +161,17 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
     wb += 2ull * ((uint64_t)e->qkv_rows * H + (uint64_t)H * Hq * D + 2ull * I * H + (uint64_t)H * I) + 2ull * 2 * H + 2ull * 2 * D;
   }
   if ((rc = e->alloc(&e->emb_text, (size_t)c.vocab * H)) || (rc = e->alloc(&e->emb_audio, (size_t)c.n_vq * e->audio_rows * H)) ||
-      (rc = e->alloc(&e->final_norm, H)) || (rc = e->alloc(&e->heads, packed_bytes(e->heads_rows, H) / 2)))
+      (rc = e->alloc(&e->final_norm, H)))
     return bail(rc);
-  hipMemset(e->heads, 0, packed_bytes(e->heads_rows, H));
-  wb += 2ull * (uint64_t)e->heads_rows * H + 2ull * H;
+  wb += 2ull * H;
+  if (c.model_kind == MTTS_MODEL_DELAY) {  // MossTTSLocal keeps one packed head per channel (local.cpp)
+    if ((rc = e->alloc(&e->heads, packed_bytes(e->heads_rows, H) / 2))) return bail(rc);
+    hipMemset(e->heads, 0, packed_bytes(e->heads_rows, H));
+    wb += 2ull * (uint64_t)e->heads_rows * H;
+  }
   e->step_weight_bytes = wb;
   if ((rc = alloc_capacity(e))) return bail(rc);
+  if (c.model_kind == MTTS_MODEL_LOCAL && ((rc = local_create(e)) || (rc = local_alloc_capacity(e)))) return bail(rc);
   if (hipDeviceSynchronize() != hipSuccess) return bail(fail(MTTS_E_HIP, "init sync failed"));
   *out = e;
   return 0;
@@ -172,6 +183,7 @@ extern "C" int mtts_engine_reserve(mtts_engine* e, int max_batch, int max_ctx, i
   HIPCHK(hipStreamSynchronize(e->stream));
   for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second.exec);
   e->graphs.clear();
+  local_clear_graphs(e);
   for (void* p : e->cap_allocs) hipFree(p);
   e->cap_allocs.clear();
   e->c.max_batch = max_batch;
@@ -179,6 +191,7 @@ extern "C" int mtts_engine_reserve(mtts_engine* e, int max_batch, int max_ctx, i
   e->c.max_prefill_tokens = max_prefill_tokens > 0 ? max_prefill_tokens : 8192;
   e->gen_B = 0;
   int rc = alloc_capacity(e);
+  if (!rc && e->lp) rc = local_alloc_capacity(e);
   if (rc) return rc;
   HIPCHK(hipDeviceSynchronize());
   return 0;
@@ -215,57 +228,34 @@ bool parse_layer(const char* name, int* layer, std::string* rest) {
   return true;
 }
 
-extern "C" int mtts_engine_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev) {
-  if (!e || !name || !src) return fail(MTTS_E_INVALID, "null argument");
-  hipSetDevice(e->device);
-  const mtts_config& c = e->c;
-  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
-  hipStream_t s = e->stream;
-  // resolve target
-  enum Kind { RAW, PACK };
-  Kind kind = RAW;
-  bf16_t* dst = nullptr;
-  size_t expect = 0;
-  int rows = 0, K = 0, row_off = 0, inter = 0, which = 0;
-  int layer = -1;
-  std::string rest;
-  if (!std::strcmp(name, "language_model.embed_tokens.weight")) {
-    dst = e->emb_text; expect = (size_t)c.vocab * H;
-  } else if (!std::strcmp(name, "language_model.norm.weight")) {
-    dst = e->final_norm; expect = H;
-  } else if (!std::strncmp(name, "emb_ext.", 8)) {
-    const int j = std::atoi(name + 8);
-    if (j < 0 || j >= c.n_vq) return fail(MTTS_E_INVALID, std::string("bad name ") + name);
-    dst = e->emb_audio + (size_t)j * e->audio_rows * H; expect = (size_t)e->audio_rows * H;
-  } else if (!std::strncmp(name, "lm_heads.", 9)) {
-    const int j = std::atoi(name + 9);
-    if (j < 0 || j > c.n_vq) return fail(MTTS_E_INVALID, std::string("bad name ") + name);
-    kind = PACK; dst = e->heads; K = H;
-    rows = j == 0 ? c.vocab : e->audio_rows;
-    row_off = j == 0 ? 0 : c.vocab + (j - 1) * e->audio_rows;
-    expect = (size_t)rows * H;
-  } else if (parse_layer(name, &layer, &rest)) {
-    if (layer < 0 || layer >= c.layers) return fail(MTTS_E_INVALID, std::string("bad layer in ") + name);
-    LayerW& w = e->L[layer];
-    if (rest == "self_attn.q_proj.weight") { kind = PACK; dst = w.qkv; rows = Hq * D; K = H; row_off = 0; }
-    else if (rest == "self_attn.k_proj.weight") { kind = PACK; dst = w.qkv; rows = Hkv * D; K = H; row_off = Hq * D; }
-    else if (rest == "self_attn.v_proj.weight") { kind = PACK; dst = w.qkv; rows = Hkv * D; K = H; row_off = (Hq + Hkv) * D; }
-    else if (rest == "self_attn.o_proj.weight") { kind = PACK; dst = w.o; rows = H; K = Hq * D; }
-    else if (rest == "mlp.gate_proj.weight") { kind = PACK; dst = w.gu; rows = I; K = H; inter = 1; which = 0; }
-    else if (rest == "mlp.up_proj.weight") { kind = PACK; dst = w.gu; rows = I; K = H; inter = 1; which = 1; }
-    else if (rest == "mlp.down_proj.weight") { kind = PACK; dst = w.down; rows = H; K = I; }
-    else if (rest == "self_attn.q_norm.weight") { dst = w.q_norm; expect = D; }
-    else if (rest == "self_attn.k_norm.weight") { dst = w.k_norm; expect = D; }
-    else if (rest == "input_layernorm.weight") { dst = w.in_norm; expect = H; }
-    else if (rest == "post_attention_layernorm.weight") { dst = w.post_norm; expect = H; }
-    else return fail(MTTS_E_INVALID, std::string("unknown weight ") + name);
-    if (kind == PACK) expect = (size_t)rows * K;
-  } else {
-    return fail(MTTS_E_INVALID, std::string("unknown weight ") + name);
+bool layer_target(const LayerW& w, const std::string& rest, int H, int I, int Hq, int Hkv, int D, WTarget* t) {
+  WTarget r;
+  r.pack = true;
+  if (rest == "self_attn.q_proj.weight") { r.dst = w.qkv; r.rows = Hq * D; r.K = H; r.row_off = 0; }
+  else if (rest == "self_attn.k_proj.weight") { r.dst = w.qkv; r.rows = Hkv * D; r.K = H; r.row_off = Hq * D; }
+  else if (rest == "self_attn.v_proj.weight") { r.dst = w.qkv; r.rows = Hkv * D; r.K = H; r.row_off = (Hq + Hkv) * D; }
+  else if (rest == "self_attn.o_proj.weight") { r.dst = w.o; r.rows = H; r.K = Hq * D; }
+  else if (rest == "mlp.gate_proj.weight") { r.dst = w.gu; r.rows = I; r.K = H; r.inter = 1; r.which = 0; }
+  else if (rest == "mlp.up_proj.weight") { r.dst = w.gu; r.rows = I; r.K = H; r.inter = 1; r.which = 1; }
+  else if (rest == "mlp.down_proj.weight") { r.dst = w.down; r.rows = H; r.K = I; }
+  else {
+    r.pack = false;
+    if (rest == "self_attn.q_norm.weight") { r.dst = w.q_norm; r.expect = D; }
+    else if (rest == "self_attn.k_norm.weight") { r.dst = w.k_norm; r.expect = D; }
+    else if (rest == "input_layernorm.weight") { r.dst = w.in_norm; r.expect = H; }
+    else if (rest == "post_attention_layernorm.weight") { r.dst = w.post_norm; r.expect = H; }
+    else return false;
   }
-  if (bytes != expect * 2) return fail(MTTS_E_INVALID, std::string("size mismatch for ") + name);
-  if (kind == RAW) {
-    HIPCHK(hipMemcpyAsync(dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+  if (r.pack) r.expect = (size_t)r.rows * r.K;
+  *t = r;
+  return true;
+}
+
+int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void* src, size_t bytes, int on_dev) {
+  hipStream_t s = e->stream;
+  if (bytes != t.expect * 2) return fail(MTTS_E_INVALID, std::string("size mismatch for ") + name);
+  if (!t.pack) {
+    HIPCHK(hipMemcpyAsync(t.dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   } else {
     const bf16_t* from = reinterpret_cast<const bf16_t*>(src);
     if (!on_dev) {
@@ -274,16 +264,54 @@ extern "C" int mtts_engine_load_weight(mtts_engine* e, const char* name, const v
       HIPCHK(hipMemcpyAsync(e->staging, src, bytes, hipMemcpyHostToDevice, s));
       from = e->staging;
     }
-    HIPCHK(pack_weight(from, dst, rows, K, row_off, inter, which, s));
+    HIPCHK(pack_weight(from, t.dst, t.rows, t.K, t.row_off, t.inter, t.which, s));
   }
   HIPCHK(hipStreamSynchronize(s));
   return 0;
+}
+
+extern "C" int mtts_engine_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev) {
+  if (!e || !name || !src) return fail(MTTS_E_INVALID, "null argument");
+  hipSetDevice(e->device);
+  if (e->lp) {  // MossTTSLocal names (model.embedding_list.*, local_transformer.*, ...)
+    int rc = 0;
+    if (local_load_weight(e, name, src, bytes, on_dev, &rc)) return rc;
+  }
+  const mtts_config& c = e->c;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
+  WTarget t;
+  int layer = -1;
+  std::string rest;
+  if (!std::strcmp(name, "language_model.embed_tokens.weight")) {
+    t.dst = e->emb_text; t.expect = (size_t)c.vocab * H;
+  } else if (!std::strcmp(name, "language_model.norm.weight")) {
+    t.dst = e->final_norm; t.expect = H;
+  } else if (!std::strncmp(name, "emb_ext.", 8)) {
+    const int j = std::atoi(name + 8);
+    if (j < 0 || j >= c.n_vq) return fail(MTTS_E_INVALID, std::string("bad name ") + name);
+    t.dst = e->emb_audio + (size_t)j * e->audio_rows * H; t.expect = (size_t)e->audio_rows * H;
+  } else if (!std::strncmp(name, "lm_heads.", 9) && !e->lp) {
+    const int j = std::atoi(name + 9);
+    if (j < 0 || j > c.n_vq) return fail(MTTS_E_INVALID, std::string("bad name ") + name);
+    t.pack = true; t.dst = e->heads; t.K = H;
+    t.rows = j == 0 ? c.vocab : e->audio_rows;
+    t.row_off = j == 0 ? 0 : c.vocab + (j - 1) * e->audio_rows;
+    t.expect = (size_t)t.rows * H;
+  } else if (parse_layer(name, &layer, &rest)) {
+    if (layer < 0 || layer >= c.layers) return fail(MTTS_E_INVALID, std::string("bad layer in ") + name);
+    if (!layer_target(e->L[layer], rest, H, I, Hq, Hkv, D, &t))
+      return fail(MTTS_E_INVALID, std::string("unknown weight ") + name);
+  } else {
+    return fail(MTTS_E_INVALID, std::string("unknown weight ") + name);
+  }
+  return store_weight(e, t, name, src, bytes, on_dev);
 }
 
 // same tensor order / init as oracle.moss_delay.weight_specs + scale_for (no text boost)
 extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
   if (!e) return fail(MTTS_E_INVALID, "null engine");
   hipSetDevice(e->device);
+  if (e->lp) return local_init_random(e, seed);
   const mtts_config& c = e->c;
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
   struct Spec { std::string name; size_t rows, cols; int kind; };  // 0 lin 1 norm 2 emb 3 head
@@ -523,6 +551,7 @@ void leave(mtts_engine* e, void* user) {
 extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
                             uint16_t* logits, void* stream) {
   if (!e || !ids || !mask || !logits) return fail(MTTS_E_INVALID, "null argument");
+  if (e->lp) return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal engine: use mtts_local_forward");
   const mtts_config& c = e->c;
   if (B <= 0 || B > c.max_batch || S <= 0 || past < 0 || past + S > c.max_ctx) return fail(MTTS_E_INVALID, "bad B/S/past");
   hipStream_t s = enter(e, stream);
@@ -546,6 +575,7 @@ static int decode_step_launch(mtts_engine* e, hipStream_t s) {
 extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T, int max_new,
                                    const mtts_sampling* sp, const int32_t* forced, void* stream) {
   if (!e || !ids || !sp) return fail(MTTS_E_INVALID, "null argument");
+  if (e->lp) return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal engine: use mtts_local_generate_begin");
   const mtts_config& c = e->c;
   if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
     return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
@@ -585,6 +615,7 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
 
 extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   if (!e) return fail(MTTS_E_INVALID, "null engine");
+  if (e->lp) return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal engine: use mtts_local_generate_decode");
   if (e->gen_B <= 0) return fail(MTTS_E_INVALID, "generate_begin not called");
   hipStream_t s = enter(e, stream);
   // the graph bakes the kernel arguments (buffers, B, the forced-schedule pointer);
@@ -754,7 +785,8 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
     case 1: W = w.o; N = H; K = Hq * D; x = e->attnb; ldx = K; y = e->h; res = e->h; ldy = H; ldres = H; epi = EPI_RESADD; wrows = H; break;
     case 2: W = w.gu; N = I; y = e->act; ldy = I; epi = EPI_SWIGLU; wrows = 2ull * I; break;
     case 3: W = w.down; N = H; K = I; x = e->act; ldx = I; y = e->h; res = e->h; ldy = H; ldres = H; epi = EPI_RESADD; wrows = H; break;
-    case 4: W = e->heads; N = e->heads_rows; y = e->logits; ldy = e->heads_ld; epi = EPI_LOGITS; ps = c.vocab;
+    case 4: if (!e->heads) return fail(MTTS_E_UNSUPPORTED, "no joint heads in a MossTTSLocal engine");
+      W = e->heads; N = e->heads_rows; y = e->logits; ldy = e->heads_ld; epi = EPI_LOGITS; ps = c.vocab;
       pp = e->audio_rows; po = e->audio_rows - 1; wrows = N; break;
     default: return fail(MTTS_E_INVALID, "bad which");
   }

@@ -117,7 +117,17 @@ struct mtts_engine {
   }
 };
 
+// where a reference tensor lands: a raw copy (norms, embeddings) or an MFMA-tile repack
+struct WTarget {
+  bf16_t* dst = nullptr;
+  bool pack = false;
+  int rows = 0, K = 0, row_off = 0, inter = 0, which = 0;
+  size_t expect = 0;  // elements
+};
+
 // ---- shared engine internals (engine.cpp) ----
+bool layer_target(const LayerW& w, const std::string& rest, int H, int I, int Hq, int Hkv, int D, WTarget* t);
+int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void* src, size_t bytes, int on_dev);
 int ensure_staging(mtts_engine* e, size_t bytes);
 bool parse_layer(const char* name, int* layer, std::string* rest);
 int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s);
@@ -138,5 +148,7 @@ void leave(mtts_engine* e, void* user);
 int local_create(mtts_engine* e);
 int local_alloc_capacity(mtts_engine* e);
 void local_destroy(mtts_engine* e);
+void local_clear_graphs(mtts_engine* e);
+int local_init_random(mtts_engine* e, uint64_t seed);
 // 1: the name belongs to the local stage and was loaded (or failed: *rc set); 0: not a local name
 int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev, int* rc);

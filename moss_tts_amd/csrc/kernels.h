@@ -179,6 +179,13 @@ size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);
+// local.hip (MossTTSLocal depth stage)
+hipError_t moss_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s);
+hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld_out, int B, hipStream_t s);
+hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, int C, int64_t* gen_ids, int Ltot,
+                      uint8_t* mask, int Cmax, int* finished, hipStream_t s);
+hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, int B, int C,
+                          int n_ch, int eos, int pad, hipStream_t s);
 // init.hip
 hipError_t fill_uniform_bf16(bf16_t* dst, size_t n, unsigned long long seed, unsigned long long tensor_id, float scale,
                              float offset, hipStream_t s);

@@ -1,0 +1,472 @@
+// MossTTSLocal on the engine: the Qwen3 backbone of engine.cpp plus the per-frame depth stage
+// of `CustomMixin._sample` (moss_tts_local/modeling_moss_tts.py:377-456):
+//
+//   g   = final-normed backbone state of the last position                     (:384-390)
+//   x_0 = speech_embedding_to_local_mlp(g)                                      (:395)
+//   for channel i < n_ch = min(1+n_vq, 1+n_vq_for_inference):
+//     local transformer over x_0..x_i (4 Qwen3 layers, no RoPE, causal)        (:397-401)
+//     logits_i = lm_heads[i](MossTTSRMSNorm_i(local_to_speech_embedding_mlps[i](h_i)))  (:402-410)
+//     pad column -inf for i >= 1; token = argmax                               (:411-419)
+//     x_{i+1} = speech_embedding_to_local_mlp(embedding_list[i](token))        (:421-423)
+//   finished rows emit eos / pad; append; stop on eos in channel 0             (:425-446)
+//
+// The reference re-runs the local transformer over the whole prefix per channel; attention
+// is causal and position-free, so the depth stack keeps a KV cache over channel positions
+// instead (same function, one new position per channel).  Everything here is launched on
+// the engine stream; one decode frame is captured as a hipGraph per (batch, n_ch).
+#include "engine_internal.h"
+
+constexpr int LOCAL_CMAX = 64;  // channel positions of the depth stack's KV cache (1 + n_vq <= 64)
+
+struct LocalParts {
+  int LH = 0, LL = 0, LI = 0, F = 0, C = 0, qkv_rows = 0;
+  std::vector<LayerW> L;
+  bf16_t* norm = nullptr;                       // local_transformer.norm
+  bf16_t *mi_gu = nullptr, *mi_down = nullptr;  // speech_embedding_to_local_mlp (gate|up interleaved), down
+  std::vector<bf16_t*> mo_gu, mo_down;          // local_to_speech_embedding_mlps[i]
+  std::vector<bf16_t*> ln, head;                // layer_norm_before_lm_heads[i], lm_heads[i] (packed)
+  uint64_t backbone_bytes = 0, channel_bytes = 0, text_head_bytes = 0, audio_head_bytes = 0;
+  // capacity
+  bf16_t *kc = nullptr, *vc = nullptr;
+  size_t layer_kv = 0;
+  uint8_t* mask = nullptr;
+  int* lpos = nullptr;  // [LOCAL_CMAX]: position i of channel i
+  bf16_t *h = nullptr, *xn = nullptr, *qkvb = nullptr, *attnb = nullptr, *act = nullptr;
+  float* ss = nullptr;
+  float* part = nullptr;
+  int* att_cnt = nullptr;
+  bf16_t *hid = nullptr, *eb = nullptr, *actF = nullptr, *zero = nullptr, *z = nullptr, *zn = nullptr, *logits = nullptr;
+  int ld_logits = 0;
+  int64_t* next = nullptr;  // [Bmax][C] tokens of the frame being built (the next forward's input)
+  int* finished = nullptr;  // [Bmax]
+  int n_ch = 0;
+  bool no_graph = false;
+  std::unordered_map<long long, hipGraphExec_t> graphs;
+};
+
+static Stack local_stack(mtts_engine* e) {
+  const LocalParts& p = *e->lp;
+  const mtts_config& c = e->c;
+  Stack st;
+  st.L = p.L.data(); st.layers = p.LL; st.H = p.LH; st.Hq = c.n_heads; st.Hkv = c.n_kv; st.D = c.head_dim;
+  st.I = p.LI; st.qkv_rows = p.qkv_rows;
+  st.kc = p.kc; st.vc = p.vc; st.layer_kv = p.layer_kv; st.Cmax = LOCAL_CMAX;
+  st.cos_t = nullptr; st.sin_t = nullptr;  // MossTTSLocalTransformer: no positional embedding
+  st.mask = p.mask;
+  st.h = p.h; st.xn = p.xn; st.qkvb = p.qkvb; st.qb = nullptr; st.attnb = p.attnb; st.act = p.act;
+  st.ss = p.ss; st.part = p.part; st.att_cnt = p.att_cnt;
+  return st;
+}
+
+int local_create(mtts_engine* e) {
+  const mtts_config& c = e->c;
+  e->lp = new LocalParts();
+  LocalParts& p = *e->lp;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv;
+  p.LH = c.local_hidden; p.LL = c.local_layers; p.LI = c.local_inter; p.F = c.local_mlp_ffn; p.C = c.n_vq + 1;
+  p.qkv_rows = (Hq + 2 * Hkv) * D;
+  if (const char* v = getenv("MTTS_LOCAL_NO_GRAPH")) p.no_graph = v[0] == '1';
+  const int LH = p.LH, LI = p.LI, F = p.F, C = p.C;
+  int rc = 0;
+  p.L.resize(p.LL);
+  uint64_t lb = 0;
+  for (int l = 0; l < p.LL; ++l) {
+    LayerW& w = p.L[l];
+    if ((rc = e->alloc(&w.qkv, packed_bytes(p.qkv_rows, LH) / 2)) || (rc = e->alloc(&w.o, packed_bytes(LH, Hq * D) / 2)) ||
+        (rc = e->alloc(&w.gu, packed_bytes(2 * LI, LH) / 2)) || (rc = e->alloc(&w.down, packed_bytes(LH, LI) / 2)) ||
+        (rc = e->alloc(&w.in_norm, LH)) || (rc = e->alloc(&w.post_norm, LH)) || (rc = e->alloc(&w.q_norm, D)) ||
+        (rc = e->alloc(&w.k_norm, D)))
+      return rc;
+    hipMemset(w.qkv, 0, packed_bytes(p.qkv_rows, LH));
+    hipMemset(w.o, 0, packed_bytes(LH, Hq * D));
+    lb += 2ull * ((uint64_t)p.qkv_rows * LH + (uint64_t)LH * Hq * D + 2ull * LI * LH + (uint64_t)LH * LI) + 4ull * LH + 4ull * D;
+  }
+  if ((rc = e->alloc(&p.norm, LH)) || (rc = e->alloc(&p.mi_gu, packed_bytes(2 * F, H) / 2)) ||
+      (rc = e->alloc(&p.mi_down, packed_bytes(LH, F) / 2)))
+    return rc;
+  p.mo_gu.assign(C, nullptr); p.mo_down.assign(C, nullptr); p.ln.assign(C, nullptr); p.head.assign(C, nullptr);
+  for (int i = 0; i < C; ++i) {
+    const int V = i == 0 ? c.vocab : e->audio_rows;
+    if ((rc = e->alloc(&p.mo_gu[i], packed_bytes(2 * F, LH) / 2)) || (rc = e->alloc(&p.mo_down[i], packed_bytes(H, F) / 2)) ||
+        (rc = e->alloc(&p.ln[i], H)) || (rc = e->alloc(&p.head[i], packed_bytes(V, H) / 2)))
+      return rc;
+    hipMemset(p.head[i], 0, packed_bytes(V, H));  // pad rows of the last tile
+    hipMemset(p.mo_down[i], 0, packed_bytes(H, F));
+  }
+  hipMemset(p.mi_down, 0, packed_bytes(LH, F));
+  // weight bytes one frame streams: backbone once, then per channel the depth stack, its norm,
+  // both adapters, the channel norm and the channel head
+  p.backbone_bytes = e->step_weight_bytes;
+  p.channel_bytes = lb + 2ull * LH + 2ull * (2ull * F * H + (uint64_t)LH * F) + 2ull * (2ull * F * LH + (uint64_t)H * F) + 2ull * H;
+  p.text_head_bytes = 2ull * c.vocab * H;
+  p.audio_head_bytes = 2ull * e->audio_rows * H;
+  e->step_weight_bytes = p.backbone_bytes + C * p.channel_bytes + p.text_head_bytes + (C - 1) * p.audio_head_bytes;
+  return 0;
+}
+
+int local_alloc_capacity(mtts_engine* e) {
+  const mtts_config& c = e->c;
+  LocalParts& p = *e->lp;
+  const int B = c.max_batch, H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv;
+  const int LH = p.LH, F = p.F, C = p.C;
+  int rc = 0;
+  e->cap_mode = true;
+  p.layer_kv = (size_t)B * Hkv * LOCAL_CMAX * D;
+  const size_t ns = attn_decode_splits(LOCAL_CMAX);
+  p.ld_logits = (c.vocab + 7) / 8 * 8;
+  if ((rc = e->alloc(&p.kc, p.layer_kv * p.LL)) || (rc = e->alloc(&p.vc, p.layer_kv * p.LL)) ||
+      (rc = e->alloc(&p.mask, (size_t)B * LOCAL_CMAX)) || (rc = e->alloc(&p.lpos, LOCAL_CMAX)) ||
+      (rc = e->alloc(&p.h, (size_t)B * LH)) || (rc = e->alloc(&p.xn, (size_t)B * LH)) ||
+      (rc = e->alloc(&p.qkvb, (size_t)B * p.qkv_rows)) || (rc = e->alloc(&p.attnb, (size_t)B * Hq * D)) ||
+      (rc = e->alloc(&p.act, (size_t)B * p.LI)) || (rc = e->alloc(&p.ss, (size_t)B * (LH / 16))) ||
+      (rc = e->alloc(&p.part, (size_t)B * ns * Hq * (D + 2))) || (rc = e->alloc(&p.att_cnt, (size_t)B * Hkv)) ||
+      (rc = e->alloc(&p.hid, (size_t)B * H)) || (rc = e->alloc(&p.eb, (size_t)B * H)) ||
+      (rc = e->alloc(&p.actF, (size_t)B * F)) || (rc = e->alloc(&p.zero, (size_t)B * LH)) ||
+      (rc = e->alloc(&p.z, (size_t)B * H)) || (rc = e->alloc(&p.zn, (size_t)B * H)) ||
+      (rc = e->alloc(&p.logits, (size_t)B * p.ld_logits)) || (rc = e->alloc(&p.next, (size_t)B * C)) ||
+      (rc = e->alloc(&p.finished, B)))
+    return rc;
+  e->cap_mode = false;
+  std::vector<int> pos(LOCAL_CMAX);
+  for (int i = 0; i < LOCAL_CMAX; ++i) pos[i] = i;
+  HIPCHK(hipMemcpy(p.lpos, pos.data(), LOCAL_CMAX * sizeof(int), hipMemcpyHostToDevice));
+  HIPCHK(hipMemset(p.mask, 1, (size_t)B * LOCAL_CMAX));  // the depth stack attends to every channel so far
+  HIPCHK(hipMemset(p.att_cnt, 0, (size_t)B * Hkv * sizeof(int)));
+  HIPCHK(hipMemset(p.zero, 0, (size_t)B * LH * 2));
+  HIPCHK(hipMemset(p.next, 0, (size_t)B * C * 8));
+  return 0;
+}
+
+void local_clear_graphs(mtts_engine* e) {
+  if (!e->lp) return;
+  for (auto& kv : e->lp->graphs) hipGraphExecDestroy(kv.second);
+  e->lp->graphs.clear();
+}
+
+void local_destroy(mtts_engine* e) {
+  if (!e->lp) return;
+  local_clear_graphs(e);
+  delete e->lp;
+  e->lp = nullptr;
+}
+
+// ---------------------------------------------------------------------------
+// weights by the reference's state_dict names (moss_tts_local/modeling_moss_tts.py:495-512,
+// :560-600): backbone names get the engine's own, the depth stage lands here
+static bool channel_index(const char* name, const char* prefix, int C, int* i, std::string* rest) {
+  const size_t n = std::strlen(prefix);
+  if (std::strncmp(name, prefix, n) != 0) return false;
+  char* end = nullptr;
+  const long v = std::strtol(name + n, &end, 10);
+  if (end == name + n || *end != '.' || v < 0 || v >= C) return false;
+  *i = (int)v;
+  *rest = std::string(end + 1);
+  return true;
+}
+
+int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev, int* rc) {
+  const mtts_config& c = e->c;
+  LocalParts& p = *e->lp;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv;
+  const int LH = p.LH, F = p.F, C = p.C;
+  int i = -1;
+  std::string rest;
+  WTarget t;
+  auto bad = [&](const char* why) {
+    *rc = fail(MTTS_E_INVALID, std::string(why) + ": " + name);
+    return 1;
+  };
+  // backbone: renamed onto the engine's names
+  if (channel_index(name, "model.embedding_list.", C, &i, &rest)) {
+    if (rest != "weight") return bad("unknown weight");
+    const std::string to = i == 0 ? std::string("language_model.embed_tokens.weight") : "emb_ext." + std::to_string(i - 1) + ".weight";
+    *rc = mtts_engine_load_weight(e, to.c_str(), src, bytes, on_dev);
+    return 1;
+  }
+  if (!std::strcmp(name, "model.language_model.embed_tokens.weight")) {  // unused: inputs_embeds path (:515-530)
+    *rc = 0;
+    return 1;
+  }
+  if (!std::strncmp(name, "model.language_model.", 21)) {
+    *rc = mtts_engine_load_weight(e, name + 6, src, bytes, on_dev);
+    return 1;
+  }
+  // depth stage
+  if (!std::strncmp(name, "local_transformer.layers.", 25)) {
+    if (!channel_index(name, "local_transformer.layers.", p.LL, &i, &rest)) return bad("bad layer");
+    if (!layer_target(p.L[i], rest, LH, p.LI, Hq, Hkv, D, &t)) return bad("unknown weight");
+  } else if (!std::strcmp(name, "local_transformer.norm.weight")) {
+    t.dst = p.norm; t.expect = LH;
+  } else if (!std::strncmp(name, "speech_embedding_to_local_mlp.", 30)) {
+    rest = name + 30;
+    t.pack = true;
+    if (rest == "gate_proj.weight") { t.dst = p.mi_gu; t.rows = F; t.K = H; t.inter = 1; t.which = 0; }
+    else if (rest == "up_proj.weight") { t.dst = p.mi_gu; t.rows = F; t.K = H; t.inter = 1; t.which = 1; }
+    else if (rest == "down_proj.weight") { t.dst = p.mi_down; t.rows = LH; t.K = F; }
+    else return bad("unknown weight");
+    t.expect = (size_t)t.rows * t.K;
+  } else if (channel_index(name, "local_to_speech_embedding_mlps.", C, &i, &rest)) {
+    t.pack = true;
+    if (rest == "gate_proj.weight") { t.dst = p.mo_gu[i]; t.rows = F; t.K = LH; t.inter = 1; t.which = 0; }
+    else if (rest == "up_proj.weight") { t.dst = p.mo_gu[i]; t.rows = F; t.K = LH; t.inter = 1; t.which = 1; }
+    else if (rest == "down_proj.weight") { t.dst = p.mo_down[i]; t.rows = H; t.K = F; }
+    else return bad("unknown weight");
+    t.expect = (size_t)t.rows * t.K;
+  } else if (channel_index(name, "layer_norm_before_lm_heads.", C, &i, &rest)) {
+    if (rest != "weight") return bad("unknown weight");
+    t.dst = p.ln[i]; t.expect = H;
+  } else if (channel_index(name, "lm_heads.", C, &i, &rest)) {
+    if (rest != "weight") return bad("unknown weight");
+    t.pack = true; t.dst = p.head[i]; t.rows = i == 0 ? c.vocab : e->audio_rows; t.K = H;
+    t.expect = (size_t)t.rows * H;
+  } else {
+    return 0;
+  }
+  *rc = store_weight(e, t, name, src, bytes, on_dev);
+  return 1;
+}
+
+// same tensor order / init as oracle.moss_local.weight_specs + _scale
+int local_init_random(mtts_engine* e, uint64_t seed) {
+  const mtts_config& c = e->c;
+  const LocalParts& p = *e->lp;
+  const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, C = p.C, LH = p.LH, F = p.F;
+  struct Spec { std::string name; size_t rows, cols; int kind; };  // 0 lin/head 1 norm 2 emb
+  std::vector<Spec> sp;
+  sp.push_back({"model.embedding_list.0.weight", (size_t)c.vocab, (size_t)H, 2});
+  for (int i = 1; i < C; ++i) sp.push_back({"model.embedding_list." + std::to_string(i) + ".weight", (size_t)e->audio_rows, (size_t)H, 2});
+  auto layer = [&](const std::string& pf, int Hs, int I) {
+    sp.push_back({pf + "self_attn.q_proj.weight", (size_t)Hq * D, (size_t)Hs, 0});
+    sp.push_back({pf + "self_attn.k_proj.weight", (size_t)Hkv * D, (size_t)Hs, 0});
+    sp.push_back({pf + "self_attn.v_proj.weight", (size_t)Hkv * D, (size_t)Hs, 0});
+    sp.push_back({pf + "self_attn.o_proj.weight", (size_t)Hs, (size_t)Hq * D, 0});
+    sp.push_back({pf + "self_attn.q_norm.weight", 1, (size_t)D, 1});
+    sp.push_back({pf + "self_attn.k_norm.weight", 1, (size_t)D, 1});
+    sp.push_back({pf + "mlp.gate_proj.weight", (size_t)I, (size_t)Hs, 0});
+    sp.push_back({pf + "mlp.up_proj.weight", (size_t)I, (size_t)Hs, 0});
+    sp.push_back({pf + "mlp.down_proj.weight", (size_t)Hs, (size_t)I, 0});
+    sp.push_back({pf + "input_layernorm.weight", 1, (size_t)Hs, 1});
+    sp.push_back({pf + "post_attention_layernorm.weight", 1, (size_t)Hs, 1});
+  };
+  for (int l = 0; l < c.layers; ++l) layer("model.language_model.layers." + std::to_string(l) + ".", H, c.inter);
+  sp.push_back({"model.language_model.norm.weight", 1, (size_t)H, 1});
+  for (int l = 0; l < p.LL; ++l) layer("local_transformer.layers." + std::to_string(l) + ".", LH, p.LI);
+  sp.push_back({"local_transformer.norm.weight", 1, (size_t)LH, 1});
+  sp.push_back({"speech_embedding_to_local_mlp.gate_proj.weight", (size_t)F, (size_t)H, 0});
+  sp.push_back({"speech_embedding_to_local_mlp.up_proj.weight", (size_t)F, (size_t)H, 0});
+  sp.push_back({"speech_embedding_to_local_mlp.down_proj.weight", (size_t)LH, (size_t)F, 0});
+  for (int i = 0; i < C; ++i) {
+    const std::string pf = "local_to_speech_embedding_mlps." + std::to_string(i) + ".";
+    sp.push_back({pf + "gate_proj.weight", (size_t)F, (size_t)LH, 0});
+    sp.push_back({pf + "up_proj.weight", (size_t)F, (size_t)LH, 0});
+    sp.push_back({pf + "down_proj.weight", (size_t)H, (size_t)F, 0});
+  }
+  for (int i = 0; i < C; ++i) sp.push_back({"layer_norm_before_lm_heads." + std::to_string(i) + ".weight", 1, (size_t)H, 1});
+  sp.push_back({"lm_heads.0.weight", (size_t)c.vocab, (size_t)H, 0});
+  for (int i = 1; i < C; ++i) sp.push_back({"lm_heads." + std::to_string(i) + ".weight", (size_t)e->audio_rows, (size_t)H, 0});
+  size_t mx = 0;
+  for (auto& s : sp) mx = std::max(mx, s.rows * s.cols);
+  int rc = ensure_staging(e, mx * 2);
+  if (rc) return rc;
+  for (size_t tid = 0; tid < sp.size(); ++tid) {
+    const Spec& s = sp[tid];
+    float scale = 1.f, offset = 0.f;
+    if (s.kind == 0) scale = (float)std::sqrt(3.0 / (double)s.cols);
+    else if (s.kind == 1) { scale = 0.25f; offset = 1.0f; }
+    HIPCHK(fill_uniform_bf16(e->staging, s.rows * s.cols, seed, tid, scale, offset, e->stream));
+    rc = mtts_engine_load_weight(e, s.name.c_str(), e->staging, s.rows * s.cols * 2, 1);
+    if (rc) return rc;
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// speech_embedding_to_local_mlp(x) -> the depth stack's residual stream (+ its per-16-column
+// sums of squares for the first layer's input norm); x [B, H]
+static int mlp_in(mtts_engine* e, const Stack& st, const bf16_t* x, int B, hipStream_t s) {
+  LocalParts& p = *e->lp;
+  const int H = e->c.hidden, LH = p.LH, F = p.F;
+  GemvArgs g = gemv_args(p.mi_gu, x, H, p.actF, F, B, F, H);
+  HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
+  g = gemv_args(p.mi_down, p.actF, F, st.h, LH, B, LH, F);
+  g.res = p.zero; g.ldres = LH; g.ss_out = st.ss; g.ld_ss_out = LH / 16;  // bf16(0 + y) == y
+  HIPCHK(gemv_ex(g, EPI_RESADD, s));
+  return 0;
+}
+
+// The depth loop of one frame from the backbone state p.hid [B, H].  Greedy tokens go to
+// p.next[b][i]; forced != nullptr feeds forced[b * ld_forced + i] to channel i+1 instead
+// (teacher forcing); dump != nullptr receives channel i's logits at dump + i*B*ld_dump.
+static int local_depth(mtts_engine* e, int B, int n_ch, const int64_t* forced, int ld_forced, bf16_t* dump, int ld_dump,
+                       hipStream_t s) {
+  LocalParts& p = *e->lp;
+  const mtts_config& c = e->c;
+  const int H = c.hidden, LH = p.LH, F = p.F, C = p.C;
+  const Stack st = local_stack(e);
+  if (int rc = mlp_in(e, st, p.hid, B, s)) return rc;
+  for (int i = 0; i < n_ch; ++i) {
+    if (int rc = run_layers(e, st, 0, B, 1, p.lpos + i, CH_DECODE, 1, s)) return rc;
+    GemvArgs g = gemv_args(p.mo_gu[i], st.xn, LH, p.actF, F, B, F, LH);
+    if (int rc = normed_input(e, st, g, p.norm, B, s)) return rc;  // local_transformer.norm (Qwen3RMSNorm)
+    HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
+    g = gemv_args(p.mo_down[i], p.actF, F, p.z, H, B, H, F);
+    HIPCHK(gemv_ex(g, EPI_STORE, s));
+    HIPCHK(moss_rmsnorm(p.z, p.ln[i], p.zn, B, H, c.rms_eps, s));
+    const int V = i == 0 ? c.vocab : e->audio_rows;
+    bf16_t* lg = dump ? dump + (size_t)i * B * ld_dump : p.logits;
+    const int ldl = dump ? ld_dump : p.ld_logits;
+    g = gemv_args(p.head[i], p.zn, H, lg, ldl, B, V, H);
+    if (i == 0) { g.pad_start = V; }
+    else { g.pad_start = 0; g.pad_period = e->audio_rows; g.pad_off = c.audio_pad_code; }
+    HIPCHK(gemv_ex(g, EPI_LOGITS, s));
+    HIPCHK(argmax_rows(lg, ldl, V, p.next + i, C, B, s));
+    if (i + 1 < n_ch) {
+      const int64_t* tok = forced ? forced + i : p.next + i;
+      const bf16_t* table = i == 0 ? e->emb_text : e->emb_audio + (size_t)(i - 1) * e->audio_rows * H;
+      HIPCHK(embed(tok, 1, table, nullptr, e->audio_rows, H, p.eb, B, s, nullptr, 0, forced ? ld_forced : C));
+      if (int rc = mlp_in(e, st, p.eb, B, s)) return rc;
+    }
+  }
+  return 0;
+}
+
+static int local_frame_end(mtts_engine* e, hipStream_t s) {
+  LocalParts& p = *e->lp;
+  HIPCHK(local_finalize(e->st, p.next, p.finished, e->gen_ids, e->mask, e->gen_B, p.C, p.n_ch, e->c.eos_token_id,
+                        e->c.audio_pad_code, s));
+  return 0;
+}
+
+static int local_step_launch(mtts_engine* e, hipStream_t s) {
+  LocalParts& p = *e->lp;
+  const int B = e->gen_B;
+  const int n_split = (e->c.max_ctx + CH_DECODE - 1) / CH_DECODE;
+  int rc = forward_rows(e, p.next, 0, B, 1, &e->st->fwd_pos, CH_DECODE, n_split, nullptr, s, nullptr, false, p.hid,
+                        p.n_ch);
+  if (!rc) rc = local_depth(e, B, p.n_ch, nullptr, 0, nullptr, 0, s);
+  if (!rc) rc = local_frame_end(e, s);
+  return rc;
+}
+
+static int n_channels(const mtts_engine* e, int n_vq_inf) {
+  const int C = e->c.n_vq + 1;
+  return n_vq_inf < 0 ? C : std::min(C, 1 + n_vq_inf);
+}
+
+// ---------------------------------------------------------------------------
+// C ABI (include/mtts.h)
+extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T,
+                                         int max_new, int n_vq_for_inference, const mtts_sampling* sp, void* stream) {
+  if (!e || !ids) return fail(MTTS_E_INVALID, "null argument");
+  if (!e->lp) return fail(MTTS_E_UNSUPPORTED, "not a MossTTSLocal engine");
+  const mtts_config& c = e->c;
+  if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
+    return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
+  if (sp && (sp->text_temperature > 0.f || sp->audio_temperature > 0.f))
+    return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal sampling is not implemented yet (greedy only)");
+  LocalParts& p = *e->lp;
+  hipStream_t s = enter(e, stream);
+  GenDev& g = e->hst;
+  std::memset(&g, 0, sizeof(g));
+  g.T0 = T; g.step = 0; g.fwd_pos = 0; g.done_step = -1;
+  g.B = B; g.n_vq = c.n_vq; g.C = p.C; g.Ltot = c.max_ctx; g.Cmax = c.max_ctx;
+  g.vocab = c.vocab; g.audio_rows = e->audio_rows;
+  e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = nullptr;
+  p.n_ch = n_channels(e, n_vq_for_inference);
+  HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
+  HIPCHK(local_init(ids, mask, B, T, p.C, e->gen_ids, c.max_ctx, e->mask, c.max_ctx, p.finished, s));
+  int rc = forward_chunked(e, ids, B, T, 0, nullptr, s, p.hid, p.n_ch);
+  if (!rc) rc = local_depth(e, B, p.n_ch, nullptr, 0, nullptr, 0, s);
+  if (!rc) rc = local_frame_end(e, s);
+  if (rc) return rc;
+  e->steps_issued = 1;
+  leave(e, stream);
+  return 0;
+}
+
+extern "C" int mtts_local_generate_decode(mtts_engine* e, int n_steps, void* stream) {
+  if (!e) return fail(MTTS_E_INVALID, "null engine");
+  if (!e->lp) return fail(MTTS_E_UNSUPPORTED, "not a MossTTSLocal engine");
+  if (e->gen_B <= 0) return fail(MTTS_E_INVALID, "generate_begin not called");
+  LocalParts& p = *e->lp;
+  hipStream_t s = enter(e, stream);
+  if (p.no_graph) {  // MTTS_LOCAL_NO_GRAPH=1: direct launches (A/B)
+    for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
+      if (int rc = local_step_launch(e, s)) return rc;
+      ++e->steps_issued;
+    }
+    leave(e, stream);
+    return 0;
+  }
+  const long long key = (long long)e->gen_B * 256 + p.n_ch;
+  auto it = p.graphs.find(key);
+  hipGraphExec_t exec = nullptr;
+  if (it != p.graphs.end()) {
+    exec = it->second;
+  } else {
+    hipGraph_t graph;
+    HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    int rc = local_step_launch(e, s);
+    hipError_t ce = hipStreamEndCapture(s, &graph);
+    if (rc) return rc;
+    if (ce != hipSuccess) return fail(MTTS_E_HIP, std::string("capture: ") + hipGetErrorString(ce));
+    HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    hipGraphDestroy(graph);
+    p.graphs[key] = exec;
+  }
+  for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
+    HIPCHK(hipGraphLaunch(exec, s));
+    ++e->steps_issued;
+  }
+  leave(e, stream);
+  return 0;
+}
+
+extern "C" int mtts_local_generate(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T, int max_new,
+                                   int n_vq_for_inference, const mtts_sampling* sp, int chunk, int* n_rows, void* stream) {
+  int rc = mtts_local_generate_begin(e, ids, mask, B, T, max_new, n_vq_for_inference, sp, stream);
+  if (rc) return rc;
+  if (chunk <= 0) chunk = 16;
+  int steps = 1, done = -1;
+  while (true) {
+    rc = mtts_generate_poll(e, &steps, &done, stream);
+    if (rc) return rc;
+    if (done >= 0 || steps >= max_new) break;
+    rc = mtts_local_generate_decode(e, std::min(chunk, max_new - steps), stream);
+    if (rc) return rc;
+  }
+  if (n_rows) *n_rows = done >= 0 ? done + 1 : steps;
+  return 0;
+}
+
+extern "C" int mtts_local_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
+                                  int n_vq_for_inference, const int64_t* forced, uint16_t* logits, int ld_logits,
+                                  void* stream) {
+  if (!e || !ids || !mask || !logits) return fail(MTTS_E_INVALID, "null argument");
+  if (!e->lp) return fail(MTTS_E_UNSUPPORTED, "not a MossTTSLocal engine");
+  const mtts_config& c = e->c;
+  if (B <= 0 || B > c.max_batch || S <= 0 || past < 0 || past + S > c.max_ctx) return fail(MTTS_E_INVALID, "bad B/S/past");
+  if (ld_logits < c.vocab) return fail(MTTS_E_INVALID, "ld_logits < vocab");
+  LocalParts& p = *e->lp;
+  const int n_ch = n_channels(e, n_vq_for_inference);
+  hipStream_t s = enter(e, stream);
+  HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
+  int rc = forward_chunked(e, ids, B, S, past, nullptr, s, p.hid, n_ch);
+  if (!rc) rc = local_depth(e, B, n_ch, forced, p.C, reinterpret_cast<bf16_t*>(logits), ld_logits, s);
+  leave(e, stream);
+  return rc;
+}
+
+extern "C" int mtts_local_frame_bytes(const mtts_engine* e, int n_vq_for_inference, uint64_t* bytes) {
+  if (!e || !bytes) return fail(MTTS_E_INVALID, "null argument");
+  if (!e->lp) return fail(MTTS_E_UNSUPPORTED, "not a MossTTSLocal engine");
+  const LocalParts& p = *e->lp;
+  const int n_ch = n_channels(e, n_vq_for_inference);
+  *bytes = p.backbone_bytes + n_ch * p.channel_bytes + p.text_head_bytes + (uint64_t)(n_ch - 1) * p.audio_head_bytes;
+  return 0;
+}
+
+extern "C" int mtts_k_moss_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int H, float eps, void* stream) {
+  HIPCHK(moss_rmsnorm(x, w, y, M, H, eps, (hipStream_t)stream));
+  return 0;
+}

@@ -39,6 +39,13 @@ class EngineConfig:
     max_batch: int = 32
     max_ctx: int = 2048
     max_prefill_tokens: int = 8192
+    # MossTTSLocal (model_kind 1): depth transformer + adapters (moss_tts_local/configuration_moss_tts.py)
+    model_kind: int = 0
+    local_hidden: int = 0
+    local_layers: int = 0
+    local_inter: int = 0
+    local_mlp_ffn: int = 0
+    eos_token_id: int = 151653
 
     def to_c(self):
         c = N.MttsConfig()
@@ -164,6 +171,44 @@ class Engine:
         out = torch.empty(B, T + n.value, C, dtype=torch.int64, device=self.device)
         N.check(N.load().mtts_generate_fetch(self._h, _ptr(out), n.value, _stream_ptr(self.device)), "fetch")
         return out
+
+
+    # ---- MossTTSLocal ------------------------------------------------------------
+    def local_forward(self, ids: torch.Tensor, mask: torch.Tensor, past: int, forced: torch.Tensor,
+                      n_vq_for_inference: int = -1):
+        """Teacher-forced frame (backbone over `ids` at `past`, then the depth loop fed `forced`
+        [B, 1+n_vq]); returns bf16 logits per channel [n_ch][B, V_i] (pad column -inf, i >= 1)."""
+        B, S, C = ids.shape
+        c = self.cfg
+        n_ch = C if n_vq_for_inference < 0 else min(C, 1 + n_vq_for_inference)
+        ld = (c.vocab + 7) // 8 * 8
+        ids = ids.to(self.device, torch.int64).contiguous()
+        mask = mask.to(self.device, torch.uint8).contiguous()
+        forced = forced.to(self.device, torch.int64).contiguous()
+        assert tuple(forced.shape) == (B, C)
+        out = torch.empty(n_ch, B, ld, dtype=torch.bfloat16, device=self.device)
+        N.check(N.load().mtts_local_forward(self._h, _ptr(ids), _ptr(mask), B, S, past, n_vq_for_inference, _ptr(forced),
+                                            _ptr(out), ld, _stream_ptr(self.device)), "local_forward")
+        A = c.audio_vocab + 1
+        return [out[0, :, :c.vocab]] + [out[i, :, :A] for i in range(1, n_ch)]
+
+    def local_generate_ids(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor], max_new_tokens: int,
+                           n_vq_for_inference: int = -1, chunk: int = 16):
+        """Greedy MossTTSLocal loop on the device; returns generation_ids [B, T + n, 1+n_vq]."""
+        B, T, C = input_ids.shape
+        ids = input_ids.to(self.device, torch.int64).contiguous()
+        mask = None if attention_mask is None else attention_mask.to(self.device, torch.uint8).contiguous()
+        n = ctypes.c_int()
+        N.check(N.load().mtts_local_generate(self._h, _ptr(ids), _ptr(mask), B, T, max_new_tokens, n_vq_for_inference,
+                                             None, chunk, ctypes.byref(n), _stream_ptr(self.device)), "local_generate")
+        out = torch.empty(B, T + n.value, C, dtype=torch.int64, device=self.device)
+        N.check(N.load().mtts_generate_fetch(self._h, _ptr(out), n.value, _stream_ptr(self.device)), "fetch")
+        return out
+
+    def local_frame_bytes(self, n_vq_for_inference: int = -1) -> int:
+        v = ctypes.c_uint64()
+        N.check(N.load().mtts_local_frame_bytes(self._h, n_vq_for_inference, ctypes.byref(v)), "local_frame_bytes")
+        return int(v.value)
 
 
 class GenerateSession:

@@ -1,0 +1,190 @@
+"""MossTTSLocal on the GPU engine against the oracle (oracle/moss_local.py) and the golden
+vectors made by the reference's own modules (tests/golden/make_golden_local.py).
+
+Tolerances: logits within 12 bf16 ulps of the row's max |logit| (the oracle-vs-reference
+band of tests/test_oracle_local.py), argmax equal where the top-2 margin is clear; greedy
+ids identical, except that a divergence must sit on a near-tie (top-2 margin <= 24 ulps)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import moss_local as L
+from tests.parity_util import margin_top2, ulp_bf16
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+
+
+@pytest.fixture(scope="module")
+def gl():
+    g = np.load(os.path.join(HERE, "golden", "golden_local.npz"))
+    cases = json.load(open(os.path.join(HERE, "golden", "cases_local.json")))
+    return g, cases
+
+
+def make_local_engine(cfg, W=None, max_batch=4, max_ctx=128, seed=None):
+    from moss_tts_amd.engine import Engine, EngineConfig
+    e = Engine(EngineConfig(hidden=cfg.hidden, layers=cfg.layers, n_heads=cfg.n_heads, n_kv=cfg.n_kv,
+                            head_dim=cfg.head_dim, inter=cfg.inter, vocab=cfg.vocab, n_vq=cfg.n_vq,
+                            rope_theta=cfg.rope_theta, rms_eps=cfg.eps, max_batch=max_batch, max_ctx=max_ctx,
+                            max_prefill_tokens=512, model_kind=1, local_hidden=cfg.local_hidden,
+                            local_layers=cfg.local_layers, local_inter=cfg.local_inter, local_mlp_ffn=cfg.mlp_ffn,
+                            eos_token_id=cfg.eos_token_id, audio_pad_code=cfg.audio_pad_code,
+                            audio_start_token_id=cfg.audio_start_token_id), 0)
+    if W is not None:
+        e.load_state_dict({k: torch.from_numpy(v) for k, v in W.items()})
+    else:
+        e.init_random(seed)
+    return e
+
+
+def lcase(gl, name):
+    g, cases = gl
+    c = cases[name]
+    cfg = L.tiny_lcfg(n_vq=c["n_vq"])
+    W = L.make_weights(cfg, c["seed"], dtype="bf16", eos_boost=c["eos_boost"])
+    return g, c, cfg, W
+
+
+def band_check(got, want, k):
+    fin = np.isfinite(want)
+    assert (np.isfinite(got) == fin).all(), k
+    scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
+    u = ulp_bf16(np.broadcast_to(scale, want.shape))
+    err = np.abs(got - np.where(fin, want, 0))[fin]
+    assert (err <= 12 * u[fin]).all(), (k, float(err.max()), float(u.max()))
+    srt = np.sort(np.where(fin, want, -np.inf), axis=-1)
+    clear = (srt[:, -1] - srt[:, -2]) > 24 * u[:, 0]
+    assert (np.argmax(got, -1) == np.argmax(want, -1))[clear].all(), k
+
+
+def frame_logits(eng, ids_all, T, frames, n_vq_inf):
+    """teacher-forced logits of `frames` frames: frame 0 from the prompt, frame f from frame f-1"""
+    B = ids_all.shape[0]
+    out = []
+    for f in range(frames):
+        if f == 0:
+            x, past = ids_all[:, :T], 0
+        else:
+            x, past = ids_all[:, T + f - 1:T + f], T + f - 1
+        mask = np.ones((B, past + x.shape[1]), np.uint8)
+        lg = eng.local_forward(torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(mask), past,
+                               torch.from_numpy(np.ascontiguousarray(ids_all[:, T + f])), n_vq_inf)
+        out += [t.float().cpu().numpy() for t in lg]
+    return out
+
+
+@pytest.mark.parametrize("name", ["l_nvq4_bf16", "l_nvq8_clone_bf16", "l_nvq8_depth4_bf16"])
+def test_local_teacher_forced_logits_vs_reference(gpu, gl, name):
+    """Every channel's logits of the first two frames against the reference's own modules."""
+    g, c, cfg, W = lcase(gl, name)
+    ids, ref = g[name + "/input_ids"], g[name + "/out"]
+    eng = make_local_engine(cfg, W)
+    got = frame_logits(eng, ref, ids.shape[1], 2, c["n_vq_inf"])
+    eng.close()
+    assert len(got) == c["n_logits"]
+    for k in range(c["n_logits"]):
+        band_check(got[k], g[f"{name}/logit{k}"], k)
+
+
+def check_trajectory(cfg, W, ids, got, want, n_vq_inf):
+    """ids equal, or the first divergence is a near-tie of the oracle's teacher-forced logits"""
+    T = ids.shape[1]
+    n = min(got.shape[1], want.shape[1])
+    diff = np.argwhere((got[:, :n] != want[:, :n]))
+    if diff.size == 0:
+        assert got.shape == want.shape
+        return
+    f = int(diff[:, 1].min()) - T
+    assert f >= 0, "prompt rows differ"
+    n_ch = min(ids.shape[2], 1 + n_vq_inf)
+    trace = []
+    L.generate(W, cfg, ids, max_new_tokens=f + 1, n_vq_for_inference=n_vq_inf, dtype="bf16", trace=trace,
+               forced=want[:, T:T + f + 1])
+    rows = diff[diff[:, 1] == T + f]
+    for b in np.unique(rows[:, 0]):
+        i = int(rows[rows[:, 0] == b, 2].min())  # later channels of the frame are conditioned on this one
+        assert i < n_ch, "channels beyond n_vq_for_inference must be 0 / pad"
+        lg = trace[f * n_ch + i][b]
+        u = float(ulp_bf16(np.abs(lg[np.isfinite(lg)]).max()))
+        assert margin_top2(lg) <= 24 * u, f"frame {f} row {b} channel {i}: divergence without a near tie"
+
+
+@pytest.mark.parametrize("name", ["l_nvq4_bf16", "l_nvq8_clone_bf16", "l_nvq8_depth4_bf16"])
+def test_local_generate_vs_reference(gpu, gl, name):
+    g, c, cfg, W = lcase(gl, name)
+    ids, ref = g[name + "/input_ids"], g[name + "/out"]
+    eng = make_local_engine(cfg, W)
+    out = eng.local_generate_ids(torch.from_numpy(ids), None, c["steps"], c["n_vq_inf"]).cpu().numpy()
+    eng.close()
+    assert out.shape[2] == ids.shape[2] and np.array_equal(out[:, :ids.shape[1]], ids)
+    check_trajectory(cfg, W, ids, out, ref, c["n_vq_inf"])
+
+
+def test_local_generate_stop_matches_oracle(gpu):
+    """eos on channel 0 stops a row; finished rows emit eos / pad; the loop ends when every
+    row has stopped (_sample :425-446).  bf16 oracle trajectory with a boosted eos row."""
+    cfg = L.tiny_lcfg(n_vq=4)
+    W = L.make_weights(cfg, 31, dtype="bf16", eos_boost=10.0)  # rows stop at frames 2, 2, 1
+    rng = np.random.default_rng(31)
+    C = cfg.n_vq + 1
+    ids = np.full((3, 14, C), cfg.audio_pad_code, np.int64)
+    ids[..., 0] = rng.integers(200, 20000, (3, 14))
+    ids[:, -1, 0] = cfg.audio_start_token_id
+    want_rows = L.generate(W, cfg, ids, max_new_tokens=40, dtype="bf16")
+    T = ids.shape[1]
+    want = np.stack([np.concatenate([ids[b, :T - r[0] - 1], r[1]], 0) for b, r in enumerate(want_rows)])
+    eng = make_local_engine(cfg, W)
+    out = eng.local_generate_ids(torch.from_numpy(ids), None, 40).cpu().numpy()
+    eng.close()
+    assert want.shape[1] < T + 40, "fixture must stop before max_new_tokens"
+    check_trajectory(cfg, W, ids, out, want, cfg.n_vq)
+    if np.array_equal(out, want):
+        fin = out[:, T:, 0] == cfg.eos_token_id
+        assert fin[:, -1].all()
+
+
+def test_local_init_random_matches_oracle_weights(gpu, gl):
+    """mtts_engine_init_random == oracle.moss_local.make_weights (same names, order, scales)."""
+    name = "l_nvq4_bf16"
+    g, c, cfg, W = lcase(gl, name)
+    ids, ref = g[name + "/input_ids"], g[name + "/out"]
+    a = make_local_engine(cfg, W)
+    b = make_local_engine(cfg, None, seed=c["seed"])
+    la = frame_logits(a, ref, ids.shape[1], 1, c["n_vq_inf"])
+    lb = frame_logits(b, ref, ids.shape[1], 1, c["n_vq_inf"])
+    a.close()
+    b.close()
+    for x, y in zip(la, lb):
+        assert np.array_equal(x, y)
+
+
+def test_moss_rmsnorm_kernel(gpu):
+    """bf16 MossTTSRMSNorm kernel vs the oracle's op-by-op bf16 restatement"""
+    import ctypes
+    from moss_tts_amd import _native as N
+    from oracle.moss_delay import _Ctx
+    rng = np.random.default_rng(5)
+    for M, H in [(1, 64), (3, 2048), (5, 520)]:
+        x = (rng.standard_normal((M, H)) * rng.uniform(0.1, 30)).astype(np.float32)
+        w = rng.uniform(0.5, 1.5, H).astype(np.float32)
+        xt = torch.from_numpy(x).to(torch.bfloat16)
+        wt = torch.from_numpy(w).to(torch.bfloat16)
+        want = L.moss_rmsnorm_bf16(_Ctx("bf16"), xt.float().numpy(), wt.float().numpy(), 1e-6)
+        xd, wd = xt.cuda(), wt.cuda()
+        y = torch.empty_like(xd)
+        N.check(N.load().mtts_k_moss_rmsnorm(ctypes.c_void_p(xd.data_ptr()), ctypes.c_void_p(wd.data_ptr()),
+                                             ctypes.c_void_p(y.data_ptr()), M, H, 1e-6, None), "moss_rmsnorm")
+        torch.cuda.synchronize()
+        got = y.float().cpu().numpy()
+        u = ulp_bf16(want)
+        assert (np.abs(got - want) <= u).all(), (M, H)
