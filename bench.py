@@ -133,6 +133,215 @@ def cpu_baseline(args, T, n_steps, frames):
                        f"{t_heads * 1e3:.0f}ms), composed to one utterance of {n_steps} steps = {utt:.1f}s")}
 
 
+def local_prompt(rng, n_vq=32, text_tokens=48, ref_frames=38, template_tokens=56):
+    """MossTTSLocal clone prompt (moss_tts_local/processing_moss_tts.py:597-641): user turn with
+    an aligned (undelayed) reference-audio block, then the assistant header + audio_start"""
+    pad = 1024
+    rows = []
+
+    def text(t):
+        rows.append([int(t)] + [pad] * n_vq)
+
+    text(151644)
+    for t in rng.integers(200, 20000, template_tokens):
+        text(t)
+    text(151652)
+    for r in rng.integers(0, 1024, (ref_frames, n_vq)):
+        rows.append([151654] + [int(v) for v in r])
+    text(151653)
+    for t in rng.integers(200, 20000, text_tokens):
+        text(t)
+    for t in (151645, 198, 151644, 77091, 198, 151652):
+        text(t)
+    return np.array(rows, np.int64)
+
+
+def cpu_baseline_local(T, frames):
+    """oracle.moss_local (numpy fp32) at the MossTTSLocal-1.7B shape on this host's cores, on a
+    bounded sample: 1 backbone prefill layer (T tokens), 2 backbone decode layer-steps, 2
+    depth-transformer layer-steps (at channel position 16), one adapter pair and the text and
+    one audio head; composed into one utterance of `frames` frames (28 backbone layers +
+    33 channels x (4 depth layers + adapters + head) per frame)."""
+    from oracle import moss_delay as O
+    from oracle import moss_local as L
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([p.get("num_threads", 1) for p in threadpool_info()] or [os.cpu_count() or 1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    cfg = L.LCfg()
+    ctx = O._Ctx("fp32")
+    rng = np.random.default_rng(0)
+    D = cfg.head_dim
+
+    def rnd(shape, s=None):
+        return rng.standard_normal(shape, dtype=np.float32) * np.float32(s if s else shape[-1] ** -0.5)
+
+    def layer_w(pf, H, I):
+        return {pf + "self_attn.q_proj.weight": rnd((cfg.n_heads * D, H)), pf + "self_attn.k_proj.weight": rnd((cfg.n_kv * D, H)),
+                pf + "self_attn.v_proj.weight": rnd((cfg.n_kv * D, H)), pf + "self_attn.o_proj.weight": rnd((H, cfg.n_heads * D)),
+                pf + "self_attn.q_norm.weight": np.ones(D, np.float32), pf + "self_attn.k_norm.weight": np.ones(D, np.float32),
+                pf + "mlp.gate_proj.weight": rnd((I, H)), pf + "mlp.up_proj.weight": rnd((I, H)),
+                pf + "mlp.down_proj.weight": rnd((H, I)), pf + "input_layernorm.weight": np.ones(H, np.float32),
+                pf + "post_attention_layernorm.weight": np.ones(H, np.float32)}
+
+    H, LH = cfg.hidden, cfg.local_hidden
+    bp, lp = "b.", "l."
+    W = {**layer_w(bp, H, cfg.inter), **layer_w(lp, LH, cfg.local_inter)}
+    cos, sin = O.rope_cos_sin(ctx, cfg, np.arange(T + 4))
+    cache = L.Cache(1)
+    t0 = time.perf_counter()
+    L.decoder_layer(ctx, W, cfg, bp, rnd((1, T, H), 1.0), cos[:T], sin[:T], cache, 0, np.ones((1, T), bool), np.arange(T))
+    t_pf = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    for s in range(2):
+        L.decoder_layer(ctx, W, cfg, bp, rnd((1, 1, H), 1.0), cos[T + s:T + s + 1], sin[T + s:T + s + 1], cache, 0,
+                        np.ones((1, T + s + 1), bool), np.array([T + s]))
+    t_bl = (time.perf_counter() - t0) / 2
+    lc = L.Cache(1)
+    for s in range(16):
+        L.decoder_layer(ctx, W, cfg, lp, rnd((1, 1, LH), 1.0), None, None, lc, 0, np.ones((1, s + 1), bool), np.array([s]))
+    t0 = time.perf_counter()
+    for s in range(2):
+        L.decoder_layer(ctx, W, cfg, lp, rnd((1, 1, LH), 1.0), None, None, lc, 0, np.ones((1, 17 + s), bool),
+                        np.array([16 + s]))
+    t_ll = (time.perf_counter() - t0) / 2
+    F = cfg.mlp_ffn
+    A = {"i.gate_proj.weight": rnd((F, H)), "i.up_proj.weight": rnd((F, H)), "i.down_proj.weight": rnd((LH, F)),
+         "o.gate_proj.weight": rnd((F, LH)), "o.up_proj.weight": rnd((F, LH)), "o.down_proj.weight": rnd((H, F))}
+    t0 = time.perf_counter()
+    L.swiglu_mlp(ctx, A, "i.", rnd((1, H), 1.0))
+    L.swiglu_mlp(ctx, A, "o.", rnd((1, LH), 1.0))
+    t_ad = time.perf_counter() - t0
+    del W, A
+    x = rnd((1, H), 1.0)
+    th = rnd((cfg.vocab, H))
+    t0 = time.perf_counter()
+    _ = x @ th.T
+    t_th = time.perf_counter() - t0
+    del th
+    ah = rnd((cfg.audio_vocab + 1, H))
+    t0 = time.perf_counter()
+    _ = x @ ah.T
+    t_ah = time.perf_counter() - t0
+    C = cfg.n_vq + 1
+    frame = cfg.layers * t_bl + C * (cfg.local_layers * t_ll + t_ad) + t_th + cfg.n_vq * t_ah
+    utt = cfg.layers * t_pf + frames * frame
+    return {"value": round(frames / FRAME_RATE / utt, 5), "unit": "audio-s/s", "cores": int(cores), "kind": "port",
+            "sample": (f"oracle.moss_local fp32 at the 1.7B shape, batch 1: 1 prefill layer (T={T}, {t_pf:.2f}s), "
+                       f"backbone layer-step {t_bl * 1e3:.1f}ms, depth layer-step {t_ll * 1e3:.1f}ms, adapters "
+                       f"{t_ad * 1e3:.1f}ms, text head {t_th * 1e3:.0f}ms, audio head {t_ah * 1e3:.1f}ms; composed to "
+                       f"one utterance of {frames} frames = {utt:.1f}s")}
+
+
+def main_local(args, world, rank, local):
+    """BASELINE configs[3]: MossTTSLocal-1.7B shape, bf16, batch 8 per GPU, greedy depth loop
+    over 1 + 32 channels per frame, 173 frames (13.84 s of audio) per utterance."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from moss_tts_amd.engine import Engine, EngineConfig
+    from moss_tts_amd import _native as Nn
+    B = args.batch if args.batch > 1 else 8
+    frames = args.decode_steps if args.decode_steps != 208 else 173
+    rng = np.random.default_rng(1 + rank)
+    prompts = [local_prompt(rng) for _ in range(B)]
+    ids = np.stack(prompts)  # equal lengths
+    T = ids.shape[1]
+    ecfg = EngineConfig(hidden=2048, layers=args.layers if args.layers != 36 else 28, n_heads=16, n_kv=8, head_dim=128,
+                        inter=6144, n_vq=32, max_batch=B, max_ctx=T + frames + 16, max_prefill_tokens=max(256 * B, 256),
+                        model_kind=1, local_hidden=1536, local_layers=4, local_inter=8960, local_mlp_ffn=2048)
+    eng = Engine(ecfg, local)
+    eng.init_random(seed=0)
+    ids_d = torch.from_numpy(ids).cuda()
+
+    def one():
+        return eng.local_generate_ids(ids_d, None, frames, -1, chunk=32)
+
+    for _ in range(args.warmup):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    g = out.cpu().numpy()
+    # frames until (and excluding) the eos frame of each row
+    made = []
+    for b in range(B):
+        ch0 = g[b, T:, 0]
+        e = np.nonzero(ch0 == 151653)[0]
+        made.append(int(e[0]) if e.size else int(ch0.shape[0]))
+    audio_s = sum(made) / FRAME_RATE * args.steps
+    t = torch.tensor([dt, audio_s], dtype=torch.float64, device="cuda")
+    if world > 1:
+        tmax = t.clone()
+        dist.all_reduce(tmax[0:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:2], op=dist.ReduceOp.SUM)
+        t[0] = tmax[0]
+    dt_max, audio_total = float(t[0]), float(t[1])
+    # prefill + frame 0 alone, and first chunk (1 s of audio = 13 frames)
+    sp = None
+    tb, lat = [], []
+    for k in range(8):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        Nn.check(Nn.load().mtts_local_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()), None, B, T, frames, -1,
+                                                     sp, None), "begin")
+        if k >= 3:
+            Nn.check(Nn.load().mtts_local_generate_decode(eng._h, 12, None), "decode")
+        Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
+        (tb if k < 3 else lat).append((time.perf_counter() - a) * 1e3)
+    res = None
+    if rank == 0:
+        fb = eng.local_frame_bytes(-1)
+        per_utt_ms = dt_max / args.steps * 1e3
+        t_begin = float(np.median(tb))
+        frame_ms = (per_utt_ms - t_begin) / (frames - 1)
+        kv_pos = 28 * 2 * 8 * 128 * 2
+        frame_bytes = fb + kv_pos * B * (T + frames / 2)
+        ms = ctypes.c_float()
+        nb = ctypes.c_uint64()
+        Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 2, 0, B, 50, ctypes.byref(ms), ctypes.byref(nb)), "time_gemv")
+        ach = nb.value / (ms.value * 1e-3) / 1e9
+        res = {
+            "metric": METRIC, "value": round(audio_total / dt_max, 4), "unit": "audio-s/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_utt_ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (random-init bf16 weights at the MossTTSLocal-1.7B shape; synthetic clone prompts)",
+            "config": {"workload": f"MossTTSLocal bf16 batch={B} on 1xMI355X (depth transformer, 1+32 channels/frame)",
+                       "n_vq": 32, "batch_per_gpu": B, "prompt_tokens": int(T), "frames": frames,
+                       "parallelism": f"dp{world}", "sampling": "greedy"},
+            "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
+            "audio_frames_per_utt": made[0],
+            "prefill_ms": round(t_begin, 3),
+            "p50_first_chunk_ms": round(float(np.median(lat)), 2),
+            "first_chunk_def": "prefill + 13 frames (first 1 s of audio codes complete), codec excluded",
+            "ms_per_frame": round(frame_ms, 4),
+            "frame_alg_bytes": int(frame_bytes),
+            "frame_hbm_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "kernel": "gemv_kernel gate|up (fused RMSNorm prologue, SwiGLU epilogue), backbone, layers rotated", "alg_bytes_per_launch": int(nb.value),
+                         "avg_launch_us": round(ms.value * 1e3, 2)},
+        }
+        if not args.no_cpu_baseline and world == 1:
+            res["cpu_baseline"] = cpu_baseline_local(int(T), frames)
+    eng.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -144,9 +353,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--extra-batches", default="4,32", help="extra per-GPU batch sizes reported in batch_sweep")
-    ap.add_argument("--config", choices=["clone", "ttsd"], default="clone",
+    ap.add_argument("--config", choices=["clone", "ttsd", "local"], default="clone",
                     help="clone: configs[1] (default); ttsd: configs[4], MOSS-TTSD long form (n_vq 16, a "
-                         "2,000-token script, 10 min = 7,500 frames of audio, position-chunked prefill)")
+                         "2,000-token script, 10 min = 7,500 frames of audio, position-chunked prefill); "
+                         "local: configs[3], MossTTSLocal-1.7B batch 8, 173 frames")
     args = ap.parse_args()
 
     import torch
@@ -158,6 +368,8 @@ def main():
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if args.config == "local":
+        return main_local(args, world, rank, local)
 
     from moss_tts_amd.engine import Engine, EngineConfig, sampling_params
     from moss_tts_amd import _native as Nn
@@ -268,7 +480,7 @@ def main():
             ach = nb.value / (ms.value * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": "gemv_kernel<1,2,EPI_SWIGLU> (gate|up + SwiGLU, layer 0)",
+                    "kernel": "gemv_kernel gate|up (fused RMSNorm prologue, SwiGLU epilogue), layers rotated",
                     "alg_bytes_per_launch": int(nb.value), "avg_launch_us": round(ms.value * 1e3, 2)}
         # whole decode step against the weight-stream roofline
         per_utt_ms = dt_max / args.steps * 1e3
