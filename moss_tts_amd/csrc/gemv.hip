@@ -80,13 +80,17 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
   int kt = kt0;
   u32x4 wa[RT][U];
   u32x4 xb[NB][U];
+  // A batch is always U loads; a wave's last batch may cover n < U k-tiles, its surplus loads
+  // re-read the wave's last tile (in-bounds, L2 hits) and their MFMAs see a zero A operand, so
+  // the remainder costs one round trip instead of n dependent single-tile ones.
   auto issue_w = [&](int k) {
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < RT; ++r) wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)(k + u) * 64);
+      for (int r = 0; r < RT; ++r)
+        wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)min(k + u, kt1 - 1) * 64);
   };
-  if (kt + U <= kt1) issue_w(kt);
+  if (kt < kt1) issue_w(kt);
 
   // Prologues (PRO) stage the block's B activation rows in LDS once; the MFMA B fragments
   // are then LDS reads.  PRO_NONE reads the fragments straight from x (L2).
@@ -149,6 +153,7 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
     }
     __syncthreads();
   }
+  // (k < kt1 and the row clamp keep every LDS address inside the staged rows)
   auto load_x = [&](int k, int nb) -> u32x4 {
     if (!xok[nb]) return (u32x4){0u, 0u, 0u, 0u};
     if constexpr (PRO != PRO_NONE) return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
@@ -156,37 +161,25 @@ __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
   };
 
   auto compute = [&](u32x4 (&w)[RT][U], int k) {
+    const int n = kt1 - k;  // k-tiles of this batch that are real (>= U: all)
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int nb = 0; nb < NB; ++nb) xb[nb][u] = load_x(k + u, nb);
+      for (int nb = 0; nb < NB; ++nb) xb[nb][u] = load_x(min(k + u, kt1 - 1), nb);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
-      for (int r = 0; r < RT; ++r)
+      for (int r = 0; r < RT; ++r) {
+        const u32x4 wv = u < n ? w[r][u] : (u32x4){0u, 0u, 0u, 0u};
 #pragma unroll
         for (int nb = 0; nb < NB; ++nb)
           acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, w[r][u]), __builtin_bit_cast(bf16x8, xb[nb][u]), acc[r][nb], 0, 0, 0);
+              __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, xb[nb][u]), acc[r][nb], 0, 0, 0);
+      }
   };
-  {
-    for (; kt + U <= kt1; kt += U) {
-      if (kt != kt0) issue_w(kt);
-      compute(wa, kt);
-    }
-  }
-  for (; kt < kt1; ++kt) {
-    u32x4 xv[NB];
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) xv[nb] = load_x(kt, nb);
-#pragma unroll
-    for (int r = 0; r < RT; ++r) {
-      const u32x4 wv = __builtin_nontemporal_load(wbase[r] + (size_t)kt * 64);
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb)
-        acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, xv[nb]), acc[r][nb], 0, 0, 0);
-    }
+  for (; kt < kt1; kt += U) {
+    if (kt != kt0) issue_w(kt);
+    compute(wa, kt);
   }
 
   // ---- fixed-order reduction of the NW waves' partial tiles through LDS ----
