@@ -133,6 +133,22 @@ def cpu_baseline(args, T, n_steps, frames):
                        f"{t_heads * 1e3:.0f}ms), composed to one utterance of {n_steps} steps = {utt:.1f}s")}
 
 
+def pmc_traffic(config):
+    """HBM bytes per launch of the roofline kernel from the newest committed rocprofv3 PMC
+    summary (profiles/r*_pmc_<config>.json, made by scripts/pmc_round.sh: separate FETCH_SIZE /
+    WRITE_SIZE passes over the same kernel instance, 2 x FETCH_SIZE + WRITE_SIZE per the gfx950
+    correction); None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{config}.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return int(d["traffic_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+    except Exception:
+        return None, None
+
+
 def local_prompt(rng, n_vq=32, text_tokens=48, ref_frames=38, template_tokens=56):
     """MossTTSLocal clone prompt (moss_tts_local/processing_moss_tts.py:597-641): user turn with
     an aligned (undelayed) reference-audio block, then the assistant header + audio_start"""
@@ -311,6 +327,7 @@ def main_local(args, world, rank, local):
         nb = ctypes.c_uint64()
         Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 2, 0, B, 50, ctypes.byref(ms), ctypes.byref(nb)), "time_gemv")
         ach = nb.value / (ms.value * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic("local")
         res = {
             "metric": METRIC, "value": round(audio_total / dt_max, 4), "unit": "audio-s/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_utt_ms, 3),
@@ -328,7 +345,7 @@ def main_local(args, world, rank, local):
             "frame_alg_bytes": int(frame_bytes),
             "frame_hbm_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
                          "kernel": "gemv_kernel gate|up (fused RMSNorm prologue, SwiGLU epilogue), backbone, layers rotated", "alg_bytes_per_launch": int(nb.value),
                          "avg_launch_us": round(ms.value * 1e3, 2)},
         }
@@ -478,8 +495,9 @@ def main():
             Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 2, 0, args.batch, 50, ctypes.byref(ms), ctypes.byref(nb)),
                      "time_gemv")
             ach = nb.value / (ms.value * 1e-3) / 1e9
+            traffic, traffic_src = pmc_traffic("clone") if args.config == "clone" and args.batch == 1 else (None, None)
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
                     "kernel": "gemv_kernel gate|up (fused RMSNorm prologue, SwiGLU epilogue), layers rotated",
                     "alg_bytes_per_launch": int(nb.value), "avg_launch_us": round(ms.value * 1e3, 2)}
         # whole decode step against the weight-stream roofline

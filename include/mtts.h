@@ -142,6 +142,13 @@ int mtts_local_forward(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* 
                        int n_vq_for_inference, const int64_t* forced_dev, uint16_t* logits_dev, int ld, void* stream);
 /* weight bytes one frame streams (backbone + n_ch x depth stage + heads) */
 int mtts_local_frame_bytes(const mtts_engine* eng, int n_vq_for_inference, uint64_t* bytes);
+/* MossTTSLocal channel pick on B rows of bf16 logits [B, ld] (V columns) for channel ch:
+ * temperature <= 0: argmax; else HF RepetitionPenalty (ch >= 1, over seen [B][C][audio_rows])
+ * -> Temperature -> TopK -> TopP -> multinomial (Philox(seed; step, row, ch)).  out[b*C + ch].
+ * Restates the realprocessor chain of moss_tts_local/modeling_moss_tts.py:356-419. */
+int mtts_k_local_pick(const uint16_t* logits, int ld, int V, int ch, const uint8_t* seen_dev, int64_t* out_dev, int C,
+                      int B, int audio_rows, float temperature, int top_k, float top_p, float penalty, uint64_t seed,
+                      int step, void* stream);
 /* bf16 MossTTSRMSNorm (no fp32 upcast, modeling_moss_tts.py:34-44), x/y [M, H] */
 int mtts_k_moss_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int H, float eps, void* stream);
 

@@ -66,6 +66,7 @@ _SIGS = {
     "mtts_local_forward": (I, [P, P, P, I, I, I, I, P, P, I, P]),
     "mtts_local_frame_bytes": (I, [P, I, ctypes.POINTER(U64)]),
     "mtts_k_moss_rmsnorm": (I, [P, P, P, I, I, F, P]),
+    "mtts_k_local_pick": (I, [P, I, I, I, P, P, I, I, I, F, I, F, F, U64, I, P]),
     "mtts_generate_fetch": (I, [P, P, I, P]),
     "mtts_k_pack": (I, [P, P, I, I, I, I, I, P]),
     "mtts_k_packed_bytes": (SZ, [I, I]),

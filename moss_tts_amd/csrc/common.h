@@ -66,6 +66,27 @@ __device__ __forceinline__ ArgMax wave_argmax(ArgMax a) {
   return a;
 }
 
+// ---- Philox4x32-10 (counter-based RNG for the multinomial draws) ----------
+__device__ __forceinline__ uint32_t mulhilo(uint32_t a, uint32_t b, uint32_t* hi) {
+  const uint64_t p = (uint64_t)a * b;
+  *hi = (uint32_t)(p >> 32);
+  return (uint32_t)p;
+}
+__device__ __forceinline__ float philox_uniform(unsigned long long seed, uint32_t c0, uint32_t c1, uint32_t c2) {
+  uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = 0x5eed;
+  uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    uint32_t h0, h1;
+    const uint32_t l0 = mulhilo(0xD2511F53u, x0, &h0);
+    const uint32_t l1 = mulhilo(0xCD9E8D57u, x2, &h1);
+    const uint32_t y0 = h1 ^ x1 ^ k0, y1 = l1, y2 = h0 ^ x3 ^ k1, y3 = l0;
+    x0 = y0; x1 = y1; x2 = y2; x3 = y3;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+  return (float)(x0 >> 8) * (1.0f / 16777216.0f);
+}
+
 // special token ids and shapes the device-side state machine needs
 struct MttsIds {
   int pad, im_start, im_end, audio_start, audio_end, user_slot, gen_slot, delay_slot;

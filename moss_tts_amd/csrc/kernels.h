@@ -183,9 +183,12 @@ hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);
 hipError_t moss_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s);
 hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld_out, int B, hipStream_t s);
 hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, int C, int64_t* gen_ids, int Ltot,
-                      uint8_t* mask, int Cmax, int* finished, hipStream_t s);
-hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, int B, int C,
-                          int n_ch, int eos, int pad, hipStream_t s);
+                      uint8_t* mask, int Cmax, int* finished, uint8_t* seen, int audio_rows, hipStream_t s);
+hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, uint8_t* seen,
+                          int B, int C, int n_ch, int eos, int pad, hipStream_t s);
+// channel token: argmax (greedy) or HF penalty/temperature/top-k/top-p + draw (sampled)
+hipError_t local_pick(const GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
+                      int C, int B, hipStream_t s);
 // init.hip
 hipError_t fill_uniform_bf16(bf16_t* dst, size_t n, unsigned long long seed, unsigned long long tensor_id, float scale,
                              float offset, hipStream_t s);

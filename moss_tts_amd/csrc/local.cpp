@@ -39,6 +39,7 @@ struct LocalParts {
   int ld_logits = 0;
   int64_t* next = nullptr;  // [Bmax][C] tokens of the frame being built (the next forward's input)
   int* finished = nullptr;  // [Bmax]
+  uint8_t* seen = nullptr;  // [Bmax][C][audio_rows] channel histories (repetition penalty)
   int n_ch = 0;
   bool no_graph = false;
   std::unordered_map<long long, hipGraphExec_t> graphs;
@@ -124,7 +125,7 @@ int local_alloc_capacity(mtts_engine* e) {
       (rc = e->alloc(&p.actF, (size_t)B * F)) || (rc = e->alloc(&p.zero, (size_t)B * LH)) ||
       (rc = e->alloc(&p.z, (size_t)B * H)) || (rc = e->alloc(&p.zn, (size_t)B * H)) ||
       (rc = e->alloc(&p.logits, (size_t)B * p.ld_logits)) || (rc = e->alloc(&p.next, (size_t)B * C)) ||
-      (rc = e->alloc(&p.finished, B)))
+      (rc = e->alloc(&p.finished, B)) || (rc = e->alloc(&p.seen, (size_t)B * C * e->audio_rows)))
     return rc;
   e->cap_mode = false;
   std::vector<int> pos(LOCAL_CMAX);
@@ -134,6 +135,7 @@ int local_alloc_capacity(mtts_engine* e) {
   HIPCHK(hipMemset(p.att_cnt, 0, (size_t)B * Hkv * sizeof(int)));
   HIPCHK(hipMemset(p.zero, 0, (size_t)B * LH * 2));
   HIPCHK(hipMemset(p.next, 0, (size_t)B * C * 8));
+  HIPCHK(hipMemset(p.seen, 0, (size_t)B * C * e->audio_rows));
   return 0;
 }
 
@@ -319,7 +321,8 @@ static int local_depth(mtts_engine* e, int B, int n_ch, const int64_t* forced, i
     if (i == 0) { g.pad_start = V; }
     else { g.pad_start = 0; g.pad_period = e->audio_rows; g.pad_off = c.audio_pad_code; }
     HIPCHK(gemv_ex(g, EPI_LOGITS, s));
-    HIPCHK(argmax_rows(lg, ldl, V, p.next + i, C, B, s));
+    if (dump) HIPCHK(argmax_rows(lg, ldl, V, p.next + i, C, B, s));  // teacher forcing: no generate state
+    else HIPCHK(local_pick(e->st, lg, ldl, V, i, p.seen, p.next, C, B, s));
     if (i + 1 < n_ch) {
       const int64_t* tok = forced ? forced + i : p.next + i;
       const bf16_t* table = i == 0 ? e->emb_text : e->emb_audio + (size_t)(i - 1) * e->audio_rows * H;
@@ -332,8 +335,8 @@ static int local_depth(mtts_engine* e, int B, int n_ch, const int64_t* forced, i
 
 static int local_frame_end(mtts_engine* e, hipStream_t s) {
   LocalParts& p = *e->lp;
-  HIPCHK(local_finalize(e->st, p.next, p.finished, e->gen_ids, e->mask, e->gen_B, p.C, p.n_ch, e->c.eos_token_id,
-                        e->c.audio_pad_code, s));
+  HIPCHK(local_finalize(e->st, p.next, p.finished, e->gen_ids, e->mask, p.seen, e->gen_B, p.C, p.n_ch,
+                        e->c.eos_token_id, e->c.audio_pad_code, s));
   return 0;
 }
 
@@ -362,8 +365,9 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   const mtts_config& c = e->c;
   if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
     return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
-  if (sp && (sp->text_temperature > 0.f || sp->audio_temperature > 0.f))
-    return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal sampling is not implemented yet (greedy only)");
+  if (sp && sp->text_temperature > 0.f && (sp->text_top_k <= 0 || sp->text_top_k > 1024))
+    return fail(MTTS_E_UNSUPPORTED, "sampled text channel needs top_k in [1, 1024]");
+  if (sp && sp->audio_temperature > 0.f && sp->audio_top_k > 1024) return fail(MTTS_E_UNSUPPORTED, "audio top_k > 1024");
   LocalParts& p = *e->lp;
   hipStream_t s = enter(e, stream);
   GenDev& g = e->hst;
@@ -371,10 +375,22 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   g.T0 = T; g.step = 0; g.fwd_pos = 0; g.done_step = -1;
   g.B = B; g.n_vq = c.n_vq; g.C = p.C; g.Ltot = c.max_ctx; g.Cmax = c.max_ctx;
   g.vocab = c.vocab; g.audio_rows = e->audio_rows;
+  // generation_config.layers (:356-368): channel 0 <- text_*, channels >= 1 <- audio_*;
+  // do_samples[i] = temperature > 0; repetition penalty on audio channels only (i != 0)
+  if (sp) {
+    g.text_sample = sp->text_temperature > 0.f;
+    g.audio_sample = sp->audio_temperature > 0.f;
+    g.text_temp = g.text_sample ? sp->text_temperature : 1.f;
+    g.audio_temp = g.audio_sample ? sp->audio_temperature : 1.f;
+    g.text_top_p = sp->text_top_p; g.audio_top_p = sp->audio_top_p;
+    g.text_top_k = sp->text_top_k; g.audio_top_k = sp->audio_top_k;
+    g.rep_penalty = sp->audio_repetition_penalty;
+    g.seed = sp->seed;
+  }
   e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = nullptr;
   p.n_ch = n_channels(e, n_vq_for_inference);
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
-  HIPCHK(local_init(ids, mask, B, T, p.C, e->gen_ids, c.max_ctx, e->mask, c.max_ctx, p.finished, s));
+  HIPCHK(local_init(ids, mask, B, T, p.C, e->gen_ids, c.max_ctx, e->mask, c.max_ctx, p.finished, p.seen, e->audio_rows, s));
   int rc = forward_chunked(e, ids, B, T, 0, nullptr, s, p.hid, p.n_ch);
   if (!rc) rc = local_depth(e, B, p.n_ch, nullptr, 0, nullptr, 0, s);
   if (!rc) rc = local_frame_end(e, s);
@@ -468,5 +484,33 @@ extern "C" int mtts_local_frame_bytes(const mtts_engine* e, int n_vq_for_inferen
 
 extern "C" int mtts_k_moss_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_t* y, int M, int H, float eps, void* stream) {
   HIPCHK(moss_rmsnorm(x, w, y, M, H, eps, (hipStream_t)stream));
+  return 0;
+}
+
+// kernel-level channel pick (parity tests): B rows of logits [B, ld]; row b's channel history
+// in seen [B][C][audio_rows] (channel ch); the draw of row b uses Philox(seed; step, b, ch)
+extern "C" int mtts_k_local_pick(const uint16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* out, int C,
+                                 int B, int audio_rows, float temperature, int top_k, float top_p, float penalty,
+                                 uint64_t seed, int step, void* stream) {
+  if (!logits || !out || B <= 0 || V <= 0 || ch < 0 || ch >= C || (ch > 0 && V > audio_rows))
+    return fail(MTTS_E_INVALID, "bad local_pick args");
+  if (temperature > 0.f && ((ch == 0 && (top_k <= 0 || top_k > 1024)) || top_k > 1024))
+    return fail(MTTS_E_UNSUPPORTED, "top_k out of range");
+  hipStream_t s = (hipStream_t)stream;
+  GenDev g;
+  std::memset(&g, 0, sizeof(g));
+  g.step = step; g.audio_rows = audio_rows; g.seed = seed;
+  g.text_sample = g.audio_sample = temperature > 0.f;
+  g.text_temp = g.audio_temp = temperature > 0.f ? temperature : 1.f;
+  g.text_top_k = g.audio_top_k = top_k;
+  g.text_top_p = g.audio_top_p = top_p;
+  g.rep_penalty = penalty;
+  GenDev* d = nullptr;
+  HIPCHK(hipMallocAsync((void**)&d, sizeof(GenDev), s));
+  HIPCHK(hipMemcpyAsync(d, &g, sizeof(g), hipMemcpyHostToDevice, s));
+  hipError_t err = local_pick(d, reinterpret_cast<const bf16_t*>(logits), ld, V, ch, seen, out, C, B, s);
+  HIPCHK(hipFreeAsync(d, s));
+  HIPCHK(err);
+  HIPCHK(hipStreamSynchronize(s));
   return 0;
 }

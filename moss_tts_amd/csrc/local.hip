@@ -80,21 +80,199 @@ hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Channel token choice (:414-419).  Greedy channels: torch.argmax of the raw logits (no
+// processors are attached when do_samples[i] is False).  Sampled channels run the HF
+// processors in the reference's order (:360-368) on the bf16 logits, then
+// multinomial(softmax):
+//   RepetitionPenaltyLogitsProcessor (audio channels): over the row's channel history,
+//     s < 0 ? s * p : s / p                                      (bf16 ops)
+//   TemperatureLogitsWarper: s / T                               (bf16)
+//   TopKLogitsWarper: keep s >= the k-th largest (ties kept)
+//   TopPLogitsWarper: ascending sort, bf16 softmax, cumsum; drop cum <= bf16(1 - top_p),
+//     the largest always kept
+// The k-th largest is found by a two-pass radix select on the 16-bit order-preserving keys
+// of the (bf16-exact) processed scores, so the whole vocab is never sorted.  The draw uses
+// Philox(seed; frame, row, channel): distribution-level parity (torch's RNG stream is not
+// reproduced).
+constexpr int PICK_CAND = 2048;
+
+__device__ __forceinline__ uint32_t okey(float v) {  // order-preserving key of a bf16-exact float
+  const uint32_t u = __float_as_uint(v) >> 16;
+  return (u & 0x8000u) ? (~u & 0xFFFFu) : (u | 0x8000u);
+}
+
+__global__ __launch_bounds__(1024) void local_pick_kernel(const GenDev* __restrict__ st, const bf16_t* __restrict__ logits,
+                                                          int ld, int V, int ch, const uint8_t* __restrict__ seen,
+                                                          int64_t* __restrict__ next, int C) {
+  __shared__ ArgMax sh[16];
+  __shared__ int hist[256];
+  __shared__ int s_hi, s_need, s_thr, s_n;
+  __shared__ unsigned long long cand[PICK_CAND];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const bf16_t* row = logits + (size_t)b * ld;
+  const bool audio = ch > 0;
+  const int sample = audio ? st->audio_sample : st->text_sample;
+  if (!sample) {
+    ArgMax a{-INFINITY, 0x7fffffff};
+    for (int i = t; i < V; i += 1024) a = am_better(a, ArgMax{bf2f(row[i]), i});
+    a = wave_argmax(a);
+    if ((t & 63) == 0) sh[t >> 6] = a;
+    __syncthreads();
+    if (t == 0) {
+      ArgMax r = sh[0];
+      for (int i = 1; i < 16; ++i) r = am_better(r, sh[i]);
+      next[(size_t)b * C + ch] = r.i == 0x7fffffff ? 0 : r.i;
+    }
+    return;
+  }
+  const float temp = audio ? st->audio_temp : st->text_temp;
+  const float pen = audio ? st->rep_penalty : 1.0f;
+  const int top_k = audio ? st->audio_top_k : st->text_top_k;
+  const float top_p = audio ? st->audio_top_p : st->text_top_p;
+  const uint8_t* sn = (audio && pen != 1.0f) ? seen + ((size_t)b * C + ch) * st->audio_rows : nullptr;
+  auto val = [&](int i) -> float {
+    float v = bf2f(row[i]);
+    if (sn && sn[i]) v = v < 0.f ? rbf(v * pen) : rbf(v / pen);
+    return rbf(v / temp);
+  };
+  const int K = top_k > 0 ? min(top_k, V) : V;
+  // pass 1: histogram of the high key byte over finite scores
+  for (int i = t; i < 256; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int i = t; i < V; i += 1024) {
+    const float v = val(i);
+    if (v > -INFINITY) atomicAdd(&hist[okey(v) >> 8], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int cum = 0, hi;
+    for (hi = 255; hi >= 0; --hi) {
+      if (cum + hist[hi] >= K) break;
+      cum += hist[hi];
+    }
+    s_hi = hi;  // -1: fewer than K finite scores (all are kept)
+    s_need = K - cum;
+  }
+  __syncthreads();
+  const int hi = s_hi;
+  if (hi >= 0) {
+    // pass 2: low byte inside the selected high bin
+    for (int i = t; i < 256; i += 1024) hist[i] = 0;
+    __syncthreads();
+    for (int i = t; i < V; i += 1024) {
+      const float v = val(i);
+      if (v > -INFINITY) {
+        const uint32_t k = okey(v);
+        if ((int)(k >> 8) == hi) atomicAdd(&hist[k & 255], 1);
+      }
+    }
+    __syncthreads();
+    if (t == 0) {
+      int cum = 0, lo;
+      for (lo = 255; lo > 0; --lo) {
+        if (cum + hist[lo] >= s_need) break;
+        cum += hist[lo];
+      }
+      s_thr = (hi << 8) | lo;
+    }
+  } else if (t == 0) {
+    s_thr = 0;
+  }
+  if (t == 0) s_n = 0;
+  __syncthreads();
+  // pass 3: candidates = finite scores with key >= threshold, sort key (score desc, index asc)
+  const uint32_t thr = (uint32_t)s_thr;
+  for (int i = t; i < V; i += 1024) {
+    const float v = val(i);
+    if (v > -INFINITY && okey(v) >= thr) {
+      const int slot = atomicAdd(&s_n, 1);
+      if (slot < PICK_CAND) cand[slot] = ((unsigned long long)(0xFFFFu - okey(v)) << 32) | (unsigned)i;
+    }
+  }
+  __syncthreads();
+  const int n = min(s_n, PICK_CAND);
+  int np = 1;
+  while (np < n) np <<= 1;
+  for (int i = n + t; i < np; i += 1024) cand[i] = ~0ull;
+  __syncthreads();
+  // bitonic sort of np entries (ascending key)
+  for (int k = 2; k <= np; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < np; i += 1024) {
+        const int p = i ^ j;
+        if (p > i) {
+          const unsigned long long x = cand[i], y = cand[p];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { cand[i] = y; cand[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  if (t == 0) {
+    // scores from keys (bf16-exact), largest first
+    auto score = [&](int i) -> float {
+      const uint32_t k = 0xFFFFu - (uint32_t)(cand[i] >> 32);
+      const uint32_t u = (k & 0x8000u) ? (k & 0x7FFFu) : (~k & 0xFFFFu);
+      return __uint_as_float(u << 16);
+    };
+    const float mx = score(0);
+    float S = 0.f;
+    for (int i = 0; i < n; ++i) S += expf(score(i) - mx);
+    // HF top-p on the ascending order: cum over candidates from the smallest up
+    int keep = n;
+    if (top_p < 1.0f) {
+      const float thr_p = rbf((float)(1.0 - (double)top_p));
+      float cum = 0.f;
+      keep = 1;
+      for (int i = n - 1; i >= 1; --i) {
+        cum += rbf(expf(score(i) - mx) / S);
+        if (rbf(cum) > thr_p) { keep = i + 1; break; }
+      }
+    }
+    float S2 = 0.f;
+    for (int i = 0; i < keep; ++i) S2 += expf(score(i) - mx);
+    const float u = philox_uniform(st->seed, (uint32_t)st->step, (uint32_t)b, (uint32_t)ch);
+    const float target = u * S2;
+    float c = 0.f;
+    int pick = (int)(cand[keep - 1] & 0xffffffffu);
+    for (int i = 0; i < keep; ++i) {
+      c += expf(score(i) - mx);
+      if (c > target) { pick = (int)(cand[i] & 0xffffffffu); break; }
+    }
+    next[(size_t)b * C + ch] = n > 0 ? pick : 0;
+  }
+}
+
+hipError_t local_pick(const GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
+                      int C, int B, hipStream_t s) {
+  if (B <= 0 || V <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(local_pick_kernel, dim3(B), dim3(1024), 0, s, st, logits, ld, V, ch, seen, next, C);
+  return hipGetLastError();
+}
+
 // prompt rows into the generation buffer and the backbone key mask; rows start unfinished
 __global__ void local_init_kernel(const int64_t* __restrict__ ids, const uint8_t* __restrict__ mask_in, int T, int C,
                                   int64_t* __restrict__ gen_ids, int Ltot, uint8_t* __restrict__ mask, int Cmax,
-                                  int* __restrict__ finished) {
+                                  int* __restrict__ finished, uint8_t* __restrict__ seen, int audio_rows) {
   const int b = blockIdx.x;
-  for (int i = threadIdx.x; i < T * C; i += blockDim.x)
-    gen_ids[(size_t)b * Ltot * C + i] = ids[(size_t)b * T * C + i];
+  for (int i = threadIdx.x; i < C * audio_rows; i += blockDim.x) seen[(size_t)b * C * audio_rows + i] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < T * C; i += blockDim.x) {
+    const int64_t v = ids[(size_t)b * T * C + i];
+    gen_ids[(size_t)b * Ltot * C + i] = v;
+    const int c = i % C;  // the penalty's history: input_ids[..., c] incl. the prompt
+    if (c > 0 && v >= 0 && v < audio_rows) seen[((size_t)b * C + c) * audio_rows + v] = 1;
+  }
   for (int t = threadIdx.x; t < Cmax; t += blockDim.x)
     mask[(size_t)b * Cmax + t] = t < T ? (mask_in ? mask_in[(size_t)b * T + t] : (uint8_t)1) : (uint8_t)0;
   if (threadIdx.x == 0) finished[b] = 0;
 }
 
 hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, int C, int64_t* gen_ids, int Ltot,
-                      uint8_t* mask, int Cmax, int* finished, hipStream_t s) {
-  hipLaunchKernelGGL(local_init_kernel, dim3(B), dim3(256), 0, s, ids, mask_in, T, C, gen_ids, Ltot, mask, Cmax, finished);
+                      uint8_t* mask, int Cmax, int* finished, uint8_t* seen, int audio_rows, hipStream_t s) {
+  hipLaunchKernelGGL(local_init_kernel, dim3(B), dim3(256), 0, s, ids, mask_in, T, C, gen_ids, Ltot, mask, Cmax, finished,
+                     seen, audio_rows);
   return hipGetLastError();
 }
 
@@ -103,7 +281,8 @@ hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, 
 // in channel 0.  One block, a thread per row.
 __global__ __launch_bounds__(256) void local_finalize_kernel(GenDev* st, int64_t* __restrict__ next, int* __restrict__ finished,
                                                              int64_t* __restrict__ gen_ids, uint8_t* __restrict__ mask,
-                                                             int B, int C, int n_ch, int eos, int pad) {
+                                                             uint8_t* __restrict__ seen, int B, int C, int n_ch,
+                                                             int eos, int pad) {
   __shared__ int alive;
   const int b = threadIdx.x;
   if (b == 0) alive = 0;
@@ -118,6 +297,7 @@ __global__ __launch_bounds__(256) void local_finalize_kernel(GenDev* st, int64_t
       if (fin) v = i == 0 ? eos : pad;
       row[i] = v;
       g[i] = v;
+      if (i > 0 && v >= 0 && v < st->audio_rows) seen[((size_t)b * C + i) * st->audio_rows + v] = 1;
     }
     mask[(size_t)b * st->Cmax + col] = 1;
     const int f = fin | (row[0] == eos);
@@ -132,11 +312,11 @@ __global__ __launch_bounds__(256) void local_finalize_kernel(GenDev* st, int64_t
   }
 }
 
-hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, int B, int C,
-                          int n_ch, int eos, int pad, hipStream_t s) {
+hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, uint8_t* seen,
+                          int B, int C, int n_ch, int eos, int pad, hipStream_t s) {
   if (B <= 0 || B > 256) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(local_finalize_kernel, dim3(1), dim3(256), 0, s, st, next, finished, gen_ids, mask, B, C, n_ch, eos,
-                     pad);
+  hipLaunchKernelGGL(local_finalize_kernel, dim3(1), dim3(256), 0, s, st, next, finished, gen_ids, mask, seen, B, C, n_ch,
+                     eos, pad);
   return hipGetLastError();
 }
 

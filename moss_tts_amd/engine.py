@@ -193,14 +193,17 @@ class Engine:
         return [out[0, :, :c.vocab]] + [out[i, :, :A] for i in range(1, n_ch)]
 
     def local_generate_ids(self, input_ids: torch.Tensor, attention_mask: Optional[torch.Tensor], max_new_tokens: int,
-                           n_vq_for_inference: int = -1, chunk: int = 16):
-        """Greedy MossTTSLocal loop on the device; returns generation_ids [B, T + n, 1+n_vq]."""
+                           n_vq_for_inference: int = -1, chunk: int = 16, sampling: Optional[N.MttsSampling] = None):
+        """MossTTSLocal loop on the device (greedy unless `sampling` has a positive temperature:
+        text_* drive channel 0, audio_* the codebook channels); returns generation_ids
+        [B, T + n, 1+n_vq]."""
         B, T, C = input_ids.shape
         ids = input_ids.to(self.device, torch.int64).contiguous()
         mask = None if attention_mask is None else attention_mask.to(self.device, torch.uint8).contiguous()
         n = ctypes.c_int()
+        sp = None if sampling is None else ctypes.byref(sampling)
         N.check(N.load().mtts_local_generate(self._h, _ptr(ids), _ptr(mask), B, T, max_new_tokens, n_vq_for_inference,
-                                             None, chunk, ctypes.byref(n), _stream_ptr(self.device)), "local_generate")
+                                             sp, chunk, ctypes.byref(n), _stream_ptr(self.device)), "local_generate")
         out = torch.empty(B, T + n.value, C, dtype=torch.int64, device=self.device)
         N.check(N.load().mtts_generate_fetch(self._h, _ptr(out), n.value, _stream_ptr(self.device)), "fetch")
         return out

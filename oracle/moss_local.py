@@ -278,3 +278,44 @@ def generate(W, cfg: LCfg, input_ids, attention_mask=None, max_new_tokens=100, n
             break
     starts = find_last_equal_C(ids[..., 0], cfg.audio_start_token_id)
     return [(T - int(starts[b]) - 1, cur[b, int(starts[b]):]) for b in range(B)]
+
+
+# ----------------------------------------------------------------------------
+def hf_pick_distribution(logits, history, ch, temperature, top_k, top_p, penalty):
+    """Sampling distribution of one channel's token (`_sample` :356-419 with do_samples[ch]):
+    the HF processor chain on the bf16 logits row, then softmax.  Restates
+    transformers/generation/logits_process.py (RepetitionPenaltyLogitsProcessor :306,
+    TemperatureLogitsWarper :238, TopKLogitsWarper :542, TopPLogitsWarper :473) in bf16:
+      penalty (ch != 0): s[h] = bf16(s*p) if s < 0 else bf16(s/p) for h in the history
+      temperature: bf16(s / T)
+      top-k: drop s < k-th largest (ties kept)
+      top-p: ascending sort, bf16 softmax, bf16 cumsum; drop cum <= bf16(1 - top_p); the
+             largest is always kept
+    Returns probabilities over the row (float64, zeros outside the kept set)."""
+    r = _bf.rnd
+    s = r(np.asarray(logits, np.float32))
+    if ch != 0 and penalty is not None and penalty != 1.0:
+        h = np.unique(np.asarray(history, np.int64))
+        v = s[h]
+        s[h] = np.where(v < 0, r(v * np.float32(penalty)), r(v / np.float32(penalty)))
+    s = r(s / np.float32(temperature))
+    if top_k is not None and top_k > 0:
+        k = min(top_k, s.size)
+        kth = np.sort(s)[::-1][k - 1]
+        s = np.where(s < kth, -np.inf, s).astype(np.float32)
+    if top_p is not None:
+        order = np.argsort(s, kind="stable")
+        srt = s[order]
+        mx = srt[-1]
+        e = np.exp((srt - mx).astype(np.float64))
+        p = r((e / e.sum()).astype(np.float32))
+        cum = r(np.cumsum(p.astype(np.float32), dtype=np.float32))
+        rm = cum <= r(np.float32(1.0 - top_p))
+        rm[-1] = False
+        s = s.copy()
+        s[order[rm]] = -np.inf
+    fin = np.isfinite(s)
+    out = np.zeros(s.size, np.float64)
+    e = np.exp((s[fin] - s[fin].max()).astype(np.float64))
+    out[fin] = e / e.sum()
+    return out

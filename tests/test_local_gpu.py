@@ -188,3 +188,26 @@ def test_moss_rmsnorm_kernel(gpu):
         got = y.float().cpu().numpy()
         u = ulp_bf16(want)
         assert (np.abs(got - want) <= u).all(), (M, H)
+
+
+def test_local_generate_sampling_readme_config(gpu, gl):
+    """README generation_config (text 1.5/50/1.0; audio penalty 1.1, 1.0/50/0.95): valid ids,
+    the audio pad code never drawn, same seed -> same trajectory, new seed -> a new one."""
+    from moss_tts_amd.engine import sampling_params
+    name = "l_nvq8_clone_bf16"
+    g, c, cfg, W = lcase(gl, name)
+    ids = g[name + "/input_ids"]
+    eng = make_local_engine(cfg, W)
+    sp = lambda seed: sampling_params(text_temperature=1.5, text_top_k=50, text_top_p=1.0, audio_temperature=1.0,
+                                      audio_top_k=50, audio_top_p=0.95, audio_repetition_penalty=1.1, seed=seed)
+    a = eng.local_generate_ids(torch.from_numpy(ids), None, 12, sampling=sp(1)).cpu().numpy()
+    b = eng.local_generate_ids(torch.from_numpy(ids), None, 12, sampling=sp(1)).cpu().numpy()
+    d = eng.local_generate_ids(torch.from_numpy(ids), None, 12, sampling=sp(2)).cpu().numpy()
+    eng.close()
+    T = ids.shape[1]
+    assert np.array_equal(a, b)
+    assert not np.array_equal(a, d)
+    gen = a[:, T:]
+    live = np.cumsum(gen[:, :, 0] == cfg.eos_token_id, axis=1) == 0  # frames before a row's eos
+    assert ((gen[..., 0] >= 0) & (gen[..., 0] < cfg.vocab)).all()
+    assert ((gen[..., 1:] >= 0) & (gen[..., 1:] < cfg.audio_pad_code))[live].all()

@@ -1,0 +1,111 @@
+"""MossTTSLocal sampling: the oracle's restatement of the HF processor chain
+(oracle.moss_local.hf_pick_distribution) pinned to transformers' own processors on CPU,
+and the device pick (mtts_k_local_pick) checked against it on the GPU: every draw inside the
+kept set, and the empirical distribution of 8192 Philox draws consistent with the oracle's
+(chi-square at fixed seeds).  Torch's RNG stream is not reproduced: parity is distributional."""
+import numpy as np
+import pytest
+
+from oracle import moss_local as L
+
+torch = pytest.importorskip("torch")
+
+CASES = [
+    # ch, V, temperature, top_k, top_p, penalty  (README defaults: text 1.5/50/1.0, audio 1.0/50/0.95/1.1)
+    (0, 151936, 1.5, 50, 1.0, None),
+    (3, 1025, 1.0, 50, 0.95, 1.1),
+    (1, 1025, 0.7, 25, 0.8, 1.3),
+    (2, 1025, 1.2, 1024, 0.9, 1.1),
+]
+
+
+def make_row(V, ch, seed):
+    rng = np.random.default_rng(seed)
+    x = (rng.standard_normal(V) * 2.5).astype(np.float32)
+    x[rng.integers(0, V, 6)] += 6.0  # a few strong candidates
+    if ch > 0:
+        x[V - 1] = -np.inf  # audio pad column
+    x = torch.from_numpy(x).to(torch.bfloat16).float().numpy()
+    hist = rng.integers(0, V - 1, 40) if ch > 0 else np.zeros(0, np.int64)
+    return x, hist
+
+
+def hf_reference(x, hist, ch, temperature, top_k, top_p, penalty):
+    from transformers.generation.logits_process import (LogitsProcessorList, RepetitionPenaltyLogitsProcessor,
+                                                        TemperatureLogitsWarper, TopKLogitsWarper, TopPLogitsWarper)
+    procs = LogitsProcessorList()
+    if penalty is not None and ch != 0:
+        procs.append(RepetitionPenaltyLogitsProcessor(penalty=penalty))
+    procs.append(TemperatureLogitsWarper(temperature=temperature))
+    procs.append(TopKLogitsWarper(top_k=top_k))
+    procs.append(TopPLogitsWarper(top_p=top_p))
+    ids = torch.from_numpy(np.asarray(hist if len(hist) else [0], np.int64))[None]
+    s = procs(ids, torch.from_numpy(x)[None].to(torch.bfloat16))
+    return torch.softmax(s.float(), -1)[0].double().numpy()
+
+
+@pytest.mark.parametrize("case", CASES)
+def test_oracle_pick_matches_hf_processors(case):
+    ch, V, temperature, top_k, top_p, penalty = case
+    x, hist = make_row(V, ch, 7 + ch)
+    want = hf_reference(x, hist, ch, temperature, top_k, top_p, penalty)
+    got = L.hf_pick_distribution(x, hist, ch, temperature, top_k, top_p, penalty)
+    assert np.array_equal(want > 0, got > 0)
+    assert np.allclose(got, want, atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES)
+def test_device_pick_distribution(case):
+    import ctypes
+    from scipy.stats import chisquare
+    from moss_tts_amd import _native as N
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ch, V, temperature, top_k, top_p, penalty = case
+    x, hist = make_row(V, ch, 7 + ch)
+    probs = L.hf_pick_distribution(x, hist, ch, temperature, top_k, top_p, penalty)
+    R, C, A = 8192, 4, 1025
+    logits = torch.from_numpy(x).to(torch.bfloat16)[None].expand(R, V).contiguous().cuda()
+    seen = torch.zeros(R, C, A, dtype=torch.uint8)
+    if ch > 0:
+        seen[:, ch, torch.from_numpy(np.unique(hist))] = 1
+    seen = seen.cuda()
+    out = torch.full((R, C), -1, dtype=torch.int64, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    N.check(N.load().mtts_k_local_pick(P(logits), V, V, ch, P(seen), P(out), C, R, A, temperature, top_k, top_p,
+                                       penalty if penalty else 1.0, 1234, 5, None), "local_pick")
+    draws = out[:, ch].cpu().numpy()
+    kept = np.nonzero(probs > 0)[0]
+    assert np.isin(draws, kept).all(), "draw outside the kept set"
+    cnt = np.bincount(draws, minlength=V)[kept].astype(np.float64)
+    exp = probs[kept] * R
+    big = exp >= 5  # chi-square on the well-populated cells, the rest pooled
+    f_obs = np.append(cnt[big], cnt[~big].sum())
+    f_exp = np.append(exp[big], exp[~big].sum())
+    if f_exp[-1] == 0:
+        f_obs, f_exp = f_obs[:-1], f_exp[:-1]
+    f_exp *= f_obs.sum() / f_exp.sum()
+    assert chisquare(f_obs, f_exp).pvalue > 1e-3
+
+
+@pytest.mark.gpu
+def test_device_pick_greedy_and_top1():
+    """temperature <= 0: torch.argmax (first index); top_k = 1: the tied maxima only"""
+    import ctypes
+    from moss_tts_amd import _native as N
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    x, hist = make_row(1025, 2, 3)
+    x[100] = x[200] = np.float32(x.max() + 1)  # a tie: first index wins
+    R, C, A = 4, 4, 1025
+    logits = torch.from_numpy(x).to(torch.bfloat16)[None].expand(R, 1025).contiguous().cuda()
+    seen = torch.zeros(R, C, A, dtype=torch.uint8, device="cuda")
+    out = torch.full((R, C), -1, dtype=torch.int64, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    N.check(N.load().mtts_k_local_pick(P(logits), 1025, 1025, 2, P(seen), P(out), C, R, A, 0.0, 50, 1.0, 1.0, 1, 0,
+                                       None), "pick")
+    assert (out[:, 2].cpu() == 100).all()
+    N.check(N.load().mtts_k_local_pick(P(logits), 1025, 1025, 2, P(seen), P(out), C, R, A, 1.0, 1, 1.0, 1.0, 1, 0,
+                                       None), "pick")
+    assert np.isin(out[:, 2].cpu().numpy(), [100, 200]).all()  # TopKLogitsWarper keeps ties
