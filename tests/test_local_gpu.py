@@ -211,3 +211,50 @@ def test_local_generate_sampling_readme_config(gpu, gl):
     live = np.cumsum(gen[:, :, 0] == cfg.eos_token_id, axis=1) == 0  # frames before a row's eos
     assert ((gen[..., 0] >= 0) & (gen[..., 0] < cfg.vocab)).all()
     assert ((gen[..., 1:] >= 0) & (gen[..., 1:] < cfg.audio_pad_code))[live].all()
+
+
+def build_local_model(cfg, W):
+    from transformers import Qwen3Config
+    from moss_tts_amd.local import MossTTSDelayConfig, MossTTSDelayModel
+    lc = Qwen3Config(vocab_size=cfg.vocab, hidden_size=cfg.hidden, intermediate_size=cfg.inter,
+                     num_hidden_layers=cfg.layers, num_attention_heads=cfg.n_heads, num_key_value_heads=cfg.n_kv,
+                     head_dim=cfg.head_dim, rope_theta=cfg.rope_theta, rms_norm_eps=cfg.eps)
+    model = MossTTSDelayModel(MossTTSDelayConfig(language_config=lc, n_vq=cfg.n_vq, local_hidden_size=cfg.local_hidden,
+                                                 local_num_layers=cfg.local_layers, local_ffn_hidden_size=cfg.local_inter,
+                                                 additional_mlp_ffn_hidden_size=cfg.mlp_ffn))
+    sd = model.state_dict()
+    for k, v in W.items():
+        assert k in sd, k
+        sd[k].copy_(torch.from_numpy(v))
+    return model.to("cuda", torch.bfloat16).eval()
+
+
+def test_local_model_generate_dropin(gpu, gl):
+    """reference-shaped model + generation_config (greedy, n_vq_for_inference) -> the
+    reference's output contract, ids equal to the engine run"""
+    from transformers import GenerationConfig
+    name = "l_nvq8_depth4_bf16"
+    g, c, cfg, W = lcase(gl, name)
+    ids = torch.from_numpy(g[name + "/input_ids"]).cuda()
+    model = build_local_model(cfg, W)
+    gc = GenerationConfig(max_new_tokens=c["steps"], eos_token_id=cfg.eos_token_id)
+    gc.n_vq_for_inference = c["n_vq_inf"]
+    gc.do_samples = [False] * (cfg.n_vq + 1)
+    gc.layers = [{}] * (cfg.n_vq + 1)
+    out = model.generate(input_ids=ids, attention_mask=torch.ones(ids.shape[:2], dtype=torch.bool, device="cuda"),
+                         generation_config=gc)
+    eng = make_local_engine(cfg, W)
+    want = eng.local_generate_ids(ids, None, c["steps"], c["n_vq_inf"]).cpu()
+    eng.close()
+    T = ids.shape[1]
+    starts = L.find_last_equal_C(g[name + "/input_ids"][..., 0], cfg.audio_start_token_id)
+    assert len(out) == c["B"]
+    for b, (start_len, rows) in enumerate(out):
+        assert int(start_len) == T - int(starts[b]) - 1
+        assert torch.equal(rows.cpu(), want[b, int(starts[b]):])
+    # README sampling layout runs through the same entry point
+    gc.do_samples = [True] * (cfg.n_vq + 1)
+    gc.layers = [{"repetition_penalty": 1.0, "temperature": 1.5, "top_p": 1.0, "top_k": 50}] + \
+        [{"repetition_penalty": 1.1, "temperature": 1.0, "top_p": 0.95, "top_k": 50}] * cfg.n_vq
+    out = model.generate(input_ids=ids, generation_config=gc)
+    assert out[0][1].shape[1] == cfg.n_vq + 1
