@@ -123,12 +123,13 @@ def left_pad(seqs: List[torch.Tensor], pad_token_id: int, audio_pad_code: int) -
     return {"input_ids": ids, "attention_mask": mask}
 
 
-def split_audio_segments(audio_codes: torch.Tensor, pad_code: int) -> List[torch.Tensor]:
+def split_audio_segments(audio_codes: torch.Tensor, pad_code: int, delay: bool = True) -> List[torch.Tensor]:
     """`processing_moss_tts.py:668-685`: de-delay, drop all-pad rows, cut into maximal runs
     of consecutive frames.  (The reference hands break *indices* to torch.split, which
     expects sizes, and raises for more than one segment -- see DESIGN.md; this returns
-    the intended runs.)"""
-    a = apply_de_delay_pattern(audio_codes)
+    the intended runs.)  delay=False: MossTTSLocal's undelayed codes
+    (`moss_tts_local/processing_moss_tts.py:668-690`)."""
+    a = apply_de_delay_pattern(audio_codes) if delay else audio_codes
     non_pad = ~(a == pad_code).all(dim=1)
     if not bool(non_pad.any()):
         return []
@@ -139,8 +140,9 @@ def split_audio_segments(audio_codes: torch.Tensor, pad_code: int) -> List[torch
 
 
 def replace_audio_placeholders(content: str, lengths: List[int], n_vq: int, gen_slot_token: str,
-                               delay_slot_token: str, audio_start_token: str, audio_end_token: str) -> str:
-    """`processing_moss_tts.py:433-471`."""
+                               delay_slot_token: str, audio_start_token: str, audio_end_token: str,
+                               delay: bool = True) -> str:
+    """`processing_moss_tts.py:433-471` (delay=False: no delay slots, MossTTSLocal :465)."""
     if n_vq < 1:
         raise ValueError(f"n_vq must be >= 1, got {n_vq}")
     n_ph = content.count(AUDIO_PLACEHOLDER)
@@ -154,7 +156,7 @@ def replace_audio_placeholders(content: str, lengths: List[int], n_vq: int, gen_
             raise ValueError(f"length must be >= 0, got {n}")
         if n == 0:
             return audio_start_token + audio_end_token
-        return audio_start_token + gen_slot_token * n + delay_slot_token * (n_vq - 1) + audio_end_token
+        return audio_start_token + gen_slot_token * n + delay_slot_token * ((n_vq - 1) if delay else 0) + audio_end_token
 
     return re.sub(re.escape(AUDIO_PLACEHOLDER), block, content)
 
@@ -192,7 +194,9 @@ def loudness_normalize(wav: torch.Tensor, target_dbfs: float = -20, gain_range=(
 
 # ----------------------------------------------------------------------------
 class MossTTSDelayProcessor:
-    """Mirror of `MossTTSDelayProcessor` (`processing_moss_tts.py:148-930`)."""
+    """Mirror of `MossTTSDelayProcessor` (`processing_moss_tts.py:148-930`).  delay_pattern
+    False is the MossTTSLocal processor (moss_tts_local/processing_moss_tts.py)."""
+    delay_pattern = True
 
     def __init__(self, tokenizer, audio_tokenizer: Any = None, model_config: Optional[MossTTSDelayConfig] = None,
                  **kwargs):
@@ -275,13 +279,15 @@ class MossTTSDelayProcessor:
         if len(audio_codes_list) > 1 and AUDIO_PLACEHOLDER in content:
             content, audio_codes_list = merge_consecutive_audio_placeholders(content, audio_codes_list)
         content = replace_audio_placeholders(content, [len(a) for a in audio_codes_list], n_vq, gen_tok, delay_tok,
-                                             self.audio_start_token, self.audio_end_token)
+                                             self.audio_start_token, self.audio_end_token, self.delay_pattern)
         dev = audio_codes_list[0].device if audio_codes_list else None
         text = torch.tensor(self.tokenizer.encode(content), device=dev)
         starts = torch.where(text == mc.audio_start_token_id)[0]
         ends = torch.where(text == mc.audio_end_token_id)[0]
         if len(starts) != len(audio_codes_list) or len(ends) != len(audio_codes_list):
             raise ValueError("Audio placeholders do not match the provided audio codes list.")
+        if not self.delay_pattern and len(audio_codes_list) > 1:
+            raise AssertionError("MossTTSLocal takes at most one audio block per message")
         if not audio_codes_list:
             audio = torch.full((len(text), n_vq), mc.audio_pad_code, device=text.device, dtype=text.dtype)
         else:
@@ -289,8 +295,10 @@ class MossTTSDelayProcessor:
             for s, e, codes in zip(starts.tolist(), ends.tolist(), audio_codes_list):
                 pieces.append(torch.full((s - prefix + 1, n_vq), mc.audio_pad_code, device=codes.device,
                                          dtype=codes.dtype))
-                pieces.append(apply_delay_pattern(codes, mc.audio_pad_code))
+                pieces.append(apply_delay_pattern(codes, mc.audio_pad_code) if self.delay_pattern else codes)
                 prefix = e
+            if truncation and not self.delay_pattern:
+                raise RuntimeError("Truncation generation is not supported at present")
             if truncation:
                 pieces[-1] = pieces[-1][: -(n_vq - 1), :]
             else:
@@ -358,7 +366,13 @@ class MossTTSDelayProcessor:
                             enc[p_] = c_
                     codes = list(enc)
                 unified.append(self._get_unified_codes(msg["role"], content, codes, truncation))
-            seqs.append(torch.cat(unified))
+            u = torch.cat(unified)
+            if mode == "generation" and not self.delay_pattern:
+                # MossTTSLocal prompts end on an audio_start row (moss_tts_local/processing_moss_tts.py:351-356)
+                row = torch.full((1, u.shape[1]), self.model_config.audio_pad_code, dtype=u.dtype, device=u.device)
+                row[0, 0] = self.model_config.audio_start_token_id
+                u = torch.cat([u, row])
+            seqs.append(u)
         return BatchFeature(data=self._pad(seqs))
 
     # ---- decode ---------------------------------------------------------------
@@ -374,7 +388,7 @@ class MossTTSDelayProcessor:
     def _parse_audio_codes(self, start_length, audio_codes):
         """`processing_moss_tts.py:668-709`: segments -> one batched codec decode -> trim the
         first segment by the start_length ratio."""
-        segs = split_audio_segments(audio_codes, self.model_config.audio_pad_code)
+        segs = split_audio_segments(audio_codes, self.model_config.audio_pad_code, self.delay_pattern)
         if not segs:
             return []
         wavs = self.decode_audio_codes(segs)
