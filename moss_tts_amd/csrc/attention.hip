@@ -346,338 +346,13 @@ hipError_t attention(const AttnArgs& a0, hipStream_t st) {
 
 }  // namespace mtts
 
-// ===========================================================================
-// Fused decode attention (one new token per row), MFMA form.
-// Grid (split, KV head, row b); a 1024-thread block (16 waves) owns 512 consecutive keys,
-// 32 per wave, so a context of <= 512 tokens is ONE block per (row, KV head) and needs no
-// cross-block combine.
-//   prologue  q_norm (TF/.../modeling_qwen3.py:252-254) + RoPE (:148-170) of the G query
-//             heads; the block whose range holds the new token also norms/ropes its key and
-//             appends k and v to the cache at `pos` (TF/cache_utils.py:127-145).  The prologue
-//             loads go out first, then the first pass's K / V^T / mask loads, then the math.
-//   S[key][head] = K_tile[16 keys x 32 dims] . Q^T[32 dims x 16 heads]  (v_mfma_f32_16x16x32_bf16)
-//   softmax per head over the wave's 32 keys (fp32; probabilities rounded to bf16 before
-//   P.V as the reference's bf16 SDPA does), O[head][dim] += P[16 x 32] . V[32 x 16 dims] with
-//   V^T fragments straight from the TRANSPOSED cache (one 16-byte load per lane); the 16
-//   wave partials merge in LDS in a fixed order.
-// Longer contexts: several blocks per head publish (m, l, o) partials (agent-scope release +
-// arrival ticket); the last arriver merges them in split order (deterministic).
-// Cache layouts: K [Bmax][Hkv][Cmax][D], V [Bmax][Hkv][D][Cmax].
+// Fused decode attention: body in attn_body.h (shared with the fused attention + o_proj launch)
+#include "attn_body.h"
 namespace mtts {
-
-constexpr int DEC_KW = 32;      // keys per wave
-constexpr int DEC_MAXS = 256;  // splits per head
 
 template <int G, int D, int NWV>
 __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(DecAttnArgs a) {
-  constexpr int KW = DEC_KW, KB = KW * NWV;
-  constexpr int QS = (D + 31) / 32;  // 32-dim MFMA steps of q.k
-  constexpr int DT = (D + 15) / 16;  // 16-dim output tiles of p.v
-  const int sp = blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int g4 = lane >> 4, c16 = lane & 15;
-  const int pos = *a.pos;
-  const int nact = pos / KB + 1;
-  if (sp >= nact || a.probe == 1) return;
-  const bool owner = sp == nact - 1;
-  const int Cmax = a.Cmax;
-  __shared__ __attribute__((aligned(16))) bf16_t q_s[16][QS * 32];  // bf16 q (zero outside G x D)
-  __shared__ float k_s[D];
-  __shared__ float v_s[D];
-  __shared__ __attribute__((aligned(16))) bf16_t p_s[NWV][16][KW];
-  __shared__ float ml_s[NWV][G][2];
-  __shared__ float acc_s[NWV][G][D];
-  __shared__ float mlp_s[DEC_MAXS][G][2];
-  __shared__ int last_s;
-
-  for (int i = threadIdx.x; i < 16 * QS * 32; i += NWV * 64)
-    if (i / (QS * 32) >= G || i % (QS * 32) >= D) (&q_s[0][0])[i] = 0;
-  const int heads = a.Hq + 2 * a.Hkv;
-  const bf16_t* row = a.qkv + (size_t)b * heads * D;
-  bf16_t* kcache = a.kc + (((size_t)b * a.Hkv + kvh) * Cmax) * D;  // [Cmax][D]
-  bf16_t* vcache = a.vc + (((size_t)b * a.Hkv + kvh) * D) * Cmax;  // [D][Cmax]
-  const uint8_t* mrow = a.mask + (size_t)b * Cmax;
-
-  // ---- prologue loads: job j < G: q head j; G: k; G+1: v (k, v only in the owner);
-  // wave w takes jobs w, w + NWV, ... ----
-  constexpr int JOBS = (G + 2 + NWV - 1) / NWV;
-  const int njobs = G + (owner ? 2 : 0);
-  uint32_t pr[JOBS], pw[JOBS], pc[JOBS], ps[JOBS];
-#pragma unroll
-  for (int jj = 0; jj < JOBS; ++jj) {
-    const int j = wave + jj * NWV;
-    pr[jj] = pw[jj] = pc[jj] = ps[jj] = 0;
-    if (j < njobs && 2 * lane < D) {
-      const int hd = j < G ? kvh * G + j : (j == G ? a.Hq + kvh : a.Hq + a.Hkv + kvh);
-      pr[jj] = *reinterpret_cast<const uint32_t*>(row + (size_t)hd * D + 2 * lane);
-      if (j <= G) {
-        pw[jj] = *reinterpret_cast<const uint32_t*>((j < G ? a.qn_w : a.kn_w) + 2 * lane);
-        if (a.cos_t) {
-          pc[jj] = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
-          ps[jj] = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
-        }
-      }
-    }
-  }
-  // ---- a wave's 32 keys k0..k0+31: K tiles (A operands), V^T fragments (B operands), mask.
-  // Keys >= pos read as zero; the new key / value are patched in from LDS below. ----
-  u32x4 kt[2][QS];
-  u32x4 vt[DT];
-  uint32_t mk[2];
-  auto load_keys = [&](int k0) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      const int key = k0 + t * 16 + c16;
-#pragma unroll
-      for (int st = 0; st < QS; ++st) {
-        const int d0 = st * 32 + 8 * g4;
-        kt[t][st] = (key < pos && d0 < D) ? *reinterpret_cast<const u32x4*>(kcache + (size_t)key * D + d0)
-                                          : (u32x4){0u, 0u, 0u, 0u};
-      }
-      // 16-key tiles that start at or before pos lie inside the row (Cmax % 64 == 0)
-      mk[t] = (k0 + t * 16 <= pos) ? *reinterpret_cast<const uint32_t*>(mrow + k0 + t * 16 + g4 * 4) : 0u;
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int dim = dt * 16 + c16;
-      const int kb = k0 + 8 * g4;  // lane's keys kb .. kb+7
-      vt[dt] = (dim < D && kb < pos) ? *reinterpret_cast<const u32x4*>(vcache + (size_t)dim * Cmax + kb)
-                                     : (u32x4){0u, 0u, 0u, 0u};
-    }
-  };
-  const int kbeg = sp * KB + wave * KW;
-  if (kbeg <= pos) load_keys(kbeg);
-
-  // ---- prologue math ----
-#pragma unroll
-  for (int jj = 0; jj < JOBS; ++jj) {
-    const int j = wave + jj * NWV;
-    if (j >= njobs) continue;  // wave-uniform
-    const bool act = 2 * lane < D;
-    const float x0 = __uint_as_float(pr[jj] << 16), x1 = __uint_as_float(pr[jj] & 0xffff0000u);
-    if (j == G + 1) {
-      if (act) {
-        v_s[2 * lane] = x0;
-        v_s[2 * lane + 1] = x1;
-        vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
-        vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
-      }
-      continue;
-    }
-    const float ss = wave_sum(x0 * x0 + x1 * x1);
-    const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
-    const float w0 = __uint_as_float(pw[jj] << 16), w1 = __uint_as_float(pw[jj] & 0xffff0000u);
-    const float c0 = __uint_as_float(pc[jj] << 16), c1 = __uint_as_float(pc[jj] & 0xffff0000u);
-    const float s0 = __uint_as_float(ps[jj] << 16), s1 = __uint_as_float(ps[jj] & 0xffff0000u);
-    const float n0 = rbf(w0 * rbf(x0 * r)), n1 = rbf(w1 * rbf(x1 * r));
-    constexpr int q4 = D / 4;
-    const bool lo = 2 * lane < D / 2;
-    const int partner = lo ? lane + q4 : lane - q4;
-    const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
-    const float sg = lo ? -1.f : 1.f;
-    // no cos table: attention without positional embedding (MossTTSLocal's depth
-    // transformer, moss_tts_local/modeling_moss_tts.py:126-176)
-    const float o0 = a.cos_t ? rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)) : n0;
-    const float o1 = a.cos_t ? rbf(rbf(n1 * c1) + rbf(sg * p1 * s1)) : n1;
-    if (act) {
-      if (j < G) {
-        q_s[j][2 * lane] = f2bf(o0);
-        q_s[j][2 * lane + 1] = f2bf(o1);
-      } else {
-        k_s[2 * lane] = o0;
-        k_s[2 * lane + 1] = o1;
-        *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
-      }
-    }
-  }
-  __syncthreads();
-  if (a.probe == 2) {
-    if (threadIdx.x == 0 && kbeg <= pos) a.out[b] = (bf16_t)(kt[0][0][0] ^ vt[DT - 1][0] ^ mk[0]);
-    return;
-  }
-
-  float m_run = -INFINITY, l_run = 0.f;  // stats of head (lane & 15)
-  f32x4 o_run[DT];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o_run[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if (kbeg <= pos) {  // waves past the new token hold no keys (their loads never ran)
-    const int k0 = kbeg;
-    // ---- S = K . Q^T (the new key patched in from LDS) ----
-    f32x4 sacc[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      if (k0 + t * 16 + c16 == pos) {
-#pragma unroll
-        for (int st = 0; st < QS; ++st) {
-          const int d0 = st * 32 + 8 * g4;
-          u32x4 v = {0u, 0u, 0u, 0u};
-          if (d0 < D)
-            for (int i = 0; i < 4; ++i) v[i] = pack2(k_s[d0 + 2 * i], k_s[d0 + 2 * i + 1]);
-          kt[t][st] = v;
-        }
-      }
-      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      // Q^T B-operand fragments from LDS: lane -> head (lane & 15), dims st*32 + 8*(lane>>4) .. +7
-#pragma unroll
-      for (int st = 0; st < QS; ++st)
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][st]),
-                                                         *reinterpret_cast<const bf16x8*>(&q_s[c16][st * 32 + 8 * g4]),
-                                                         sacc[t], 0, 0, 0);
-    }
-    // V^T: keys >= pos zeroed, the new token's value patched in from LDS
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int dim = dt * 16 + c16;
-      const int kb = k0 + 8 * g4;
-      if (dim < D && kb + 8 > pos && kb <= pos) {
-        u32x4 v = vt[dt];
-        const uint32_t nv = (uint32_t)f2bf(v_s[dim]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kk = kb + 2 * i;
-          const uint32_t lo = kk < pos ? (v[i] & 0xffffu) : (kk == pos ? nv : 0u);
-          const uint32_t hi = kk + 1 < pos ? (v[i] >> 16) : (kk + 1 == pos ? nv : 0u);
-          v[i] = lo | (hi << 16);
-        }
-        vt[dt] = v;
-      }
-    }
-    // ---- softmax over the 32 keys for head c16 (rows: keys t*16 + g4*4 + r) ----
-    float sv[2][4];
-    float mc = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + t * 16 + g4 * 4 + r;
-        const bool valid = key <= pos && ((mk[t] >> (8 * r)) & 0xffu);
-        sv[t][r] = valid ? sacc[t][r] * a.scale : -INFINITY;
-        mc = fmaxf(mc, sv[t][r]);
-      }
-    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
-    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
-    float lc = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float pr4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
-        lc += p;
-        pr4[r] = p;
-      }
-      uint2 pk;
-      pk.x = pack2(pr4[0], pr4[1]);
-      pk.y = pack2(pr4[2], pr4[3]);
-      *reinterpret_cast<uint2*>(&p_s[wave][c16][t * 16 + g4 * 4]) = pk;  // bf16-rounded probabilities
-    }
-    lc += __shfl_xor(lc, 16, 64);
-    lc += __shfl_xor(lc, 32, 64);
-    const float mn = fmaxf(m_run, mc);
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
-    l_run = l_run * alpha + lc * beta;
-    m_run = mn;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // ---- O += P . V ----
-    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[wave][c16][8 * g4]);
-    float al[4], be[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      al[r] = __shfl(alpha, g4 * 4 + r, 64);
-      be[r] = __shfl(beta, g4 * 4 + r, 64);
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
-                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  }
-  if (lane < G) {
-    ml_s[wave][lane][0] = m_run;
-    ml_s[wave][lane][1] = l_run;
-  }
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = g4 * 4 + r, dim = dt * 16 + c16;
-      if (h < G && dim < D) acc_s[wave][h][dim] = o_run[dt][r];
-    }
-  __syncthreads();
-
-  // ---- merge the 16 wave partials (fixed order) into the block's result / partial ----
-  const int t = threadIdx.x;
-  const bool single = nact == 1 && !a.publish_only;
-  float* part = a.part + (((size_t)b * a.Hkv + kvh) * a.ns + sp) * (G * (D + 2));
-  for (int e = t; e < G * D; e += NWV * 64) {
-    const int h = e / D, d = e % D;
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) M = fmaxf(M, ml_s[w][h][0]);
-    float L = 0.f, o = 0.f;
-#pragma unroll
-    for (int w = 0; w < NWV; ++w) {
-      const float mw = ml_s[w][h][0];
-      const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
-      L += f * ml_s[w][h][1];
-      o += f * acc_s[w][h][d];
-    }
-    if (single) {
-      a.out[(size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e] = f2bf(L > 0.f ? o / L : 0.f);
-    } else {
-      part[e] = o;
-      if (d == 0) {
-        part[G * D + 2 * h] = M;
-        part[G * D + 2 * h + 1] = L;
-      }
-    }
-  }
-  if (single || a.publish_only || a.probe == 3) return;
-
-  // ---- publish + arrival ticket (agent-scope release / acquire) ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* cnt = a.cnt + (size_t)b * a.Hkv + kvh;
-  if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    last_s = ticket == nact - 1;
-    if (last_s) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!last_s) return;
-  // ---- the last arriver merges the nact partials in split order: the (m, l) pairs go to
-  // LDS with all loads in flight at once, then each thread sums its element over splits ----
-  const float* p0 = a.part + ((size_t)b * a.Hkv + kvh) * a.ns * (G * (D + 2));
-  constexpr int PS = G * (D + 2);
-  float* mlp = &mlp_s[0][0][0];
-  for (int i = t; i < nact * G * 2; i += NWV * 64) mlp[i] = p0[(size_t)(i / (2 * G)) * PS + G * D + i % (2 * G)];
-  __syncthreads();
-  for (int e = t; e < G * D; e += NWV * 64) {
-    const int h = e / D;
-    float M = -INFINITY;
-    for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, mlp[(s2 * G + h) * 2]);
-    float L = 0.f, o = 0.f;
-#pragma unroll 8
-    for (int s2 = 0; s2 < nact; ++s2) {
-      const float ms = mlp[(s2 * G + h) * 2];
-      const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
-      L += f * mlp[(s2 * G + h) * 2 + 1];
-      o += f * p0[(size_t)s2 * PS + e];
-    }
-    a.out[(size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e] = f2bf(L > 0.f ? o / L : 0.f);
-  }
-  if (t == 0) *cnt = 0;  // ready for the next launch (graph replay)
+  attn_decode_body<G, D, NWV>(a, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
 }
 
 template <int D, int NWV>
@@ -724,8 +399,11 @@ hipError_t attn_decode(const DecAttnArgs& a0, int B, hipStream_t s) {
   if (!a0.part || !a0.cnt) return hipErrorInvalidValue;
   if (attn_decode_splits(a0.Cmax) > DEC_MAXS) return hipErrorInvalidValue;
   DecAttnArgs a = a0;
-  a.nwv = decode_waves();
-  a.ns = attn_decode_splits(a.Cmax);
+  // publish-only blocks must match the o_proj prologue's view (attn_decode_keys_per_block);
+  // the self-combining form (B > 16) takes 16 waves = 512 keys per block, which halves the
+  // splits to merge (B=32: 5.31 vs 5.62 ms/step; B=1: 8 waves stay faster, 3.29 vs 3.37)
+  a.nwv = (!a.publish_only && !getenv("MTTS_ATTN_NWV") && B > 16) ? 16 : decode_waves();
+  a.ns = (a.Cmax + DEC_KW * a.nwv - 1) / (DEC_KW * a.nwv);
   static const int probe = getenv("MTTS_ATTN_PROBE") ? atoi(getenv("MTTS_ATTN_PROBE")) : 0;
   a.probe = probe;
   switch (a.D) {

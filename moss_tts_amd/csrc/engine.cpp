@@ -89,8 +89,9 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->part, e->part_floats))) return rc;
   if ((rc = e->alloc(&e->logits, (size_t)c.max_batch * e->heads_ld))) return rc;
   if ((rc = e->alloc(&e->d_pos, 4))) return rc;
-  if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv))) return rc;
+  if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv)) || (rc = e->alloc(&e->fsync, 4))) return rc;
   if (hipMemset(e->att_cnt, 0, (size_t)c.max_batch * Hkv * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
+  if (hipMemset(e->fsync, 0, 4 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   // generate state
   const int B = c.max_batch;
   if ((rc = e->alloc(&e->st, 1)) || (rc = e->alloc(&e->is_stopping, B)) || (rc = e->alloc(&e->is_audio, B)) ||
@@ -129,6 +130,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_GEMV_PREFILL")) e->gemv_prefill = v[0] == '1';
   if (const char* v = getenv("MTTS_UNFUSED_ATTN")) e->unfused_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
+  if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -376,7 +378,7 @@ Stack backbone_stack(mtts_engine* e) {
   st.kc = e->kc; st.vc = e->vc; st.layer_kv = e->layer_kv; st.Cmax = c.max_ctx;
   st.cos_t = e->cos_t; st.sin_t = e->sin_t; st.mask = e->mask;
   st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
-  st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt;
+  st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt; st.fsync = e->fsync;
   return st;
 }
 
@@ -389,9 +391,12 @@ Stack backbone_stack(mtts_engine* e) {
 // GEMV (+residual, +sums of squares).
 // token-parallel projections: the decode GEMV for a handful of rows, the prefill GEMM
 // (weights read once per 256 tokens instead of once per 32) beyond that
-constexpr int GEMM_MIN_ROWS = 33;
+static int gemm_min_rows() {  // MTTS_GEMM_MIN_ROWS (A/B): token rows from which projections use the GEMM
+  static const int v = getenv("MTTS_GEMM_MIN_ROWS") ? atoi(getenv("MTTS_GEMM_MIN_ROWS")) : 33;
+  return v;
+}
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
-  if (g.B >= GEMM_MIN_ROWS && !g.ss_in && !e->gemv_prefill) return gemm_ex(g, epi, s);
+  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill) return gemm_ex(g, epi, s);
   return gemv_ex(g, epi, s);
 }
 
@@ -412,6 +417,9 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     if (int rc = normed_input(e, st, g, w.in_norm, M, s)) return rc;
     g.force_nw = e->nw[0];
     HIPCHK(proj(e, g, EPI_STORE, s));
+    // decode, small batch: attention + o_proj in one launch (fused.hip)
+    const bool fused_ao = fuse_attn && e->fused_ao && st.fsync &&
+                          fused_attn_splits(st.Cmax) * Hkv * B <= 1024;
     if (S == 1) {
       DecAttnArgs da{};
       da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
@@ -420,7 +428,13 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
       da.publish_only = fuse_attn ? 1 : 0;
       da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
-      HIPCHK(attn_decode(da, B, s));
+      if (fused_ao) {
+        GemvArgs go = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
+        go.res = st.h; go.ldres = H; go.ss_out = st.ss; go.ld_ss_out = NT;
+        HIPCHK(attn_oproj(da, go, st.fsync, B, s));
+      } else {
+        HIPCHK(attn_decode(da, B, s));
+      }
     } else {
       if (!st.cos_t) return fail(MTTS_E_UNSUPPORTED, "multi-token forward of a stack without positions");
       QKRopeArgs qa;
@@ -436,13 +450,15 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       if (e->old_prefill_attn) HIPCHK(attention(aa, s));
       else HIPCHK(attention_prefill(aa, s));
     }
-    g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
-    g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
-    if (fuse_attn) {
-      g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
-      g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
+    if (!(S == 1 && fused_ao)) {
+      g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
+      g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
+      if (fuse_attn) {
+        g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
+        g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
+      }
+      HIPCHK(proj(e, g, EPI_RESADD, s));
     }
-    HIPCHK(proj(e, g, EPI_RESADD, s));
     g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
     if (int rc = normed_input(e, st, g, w.post_norm, M, s)) return rc;
     g.force_nw = e->nw[2];

@@ -45,6 +45,7 @@ struct Stack {
   float* ss = nullptr;      // per-16-column sums of squares of h
   float* part = nullptr;
   int* att_cnt = nullptr;
+  int* fsync = nullptr;     // 4 ticket words of the fused attention + o_proj launch (zero between launches)
 };
 
 inline size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
@@ -78,6 +79,8 @@ struct mtts_engine {
   bool gemv_prefill = false;      // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)
   bool unfused_attn = false;      // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)
   bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)
+  bool fused_ao = false;          // MTTS_FUSED_AO=1: decode attention + o_proj as one launch (fused.hip; A/B, slower)
+  int* fsync = nullptr;
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};

@@ -24,225 +24,16 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "kernels.h"
+#include "gemv_body.h"
 
 namespace mtts {
 
 size_t norm_lds_bytes(int B, int K) { return (size_t)(B + 1) * K * 2; }
 
-// bf16(nw * bf16(x * r)) for 8 packed elements (Qwen3RMSNorm rounding points)
-__device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
-  u32x4 o;
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const float x0 = __uint_as_float(xv[i] << 16), x1 = __uint_as_float(xv[i] & 0xffff0000u);
-    const float w0 = __uint_as_float(wv[i] << 16), w1 = __uint_as_float(wv[i] & 0xffff0000u);
-    o[i] = pack2(w0 * rbf(x0 * r), w1 * rbf(x1 * r));
-  }
-  return o;
-}
-
 template <int NB, int RT, int EPI, int PRO, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
-  // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
-  // bytes in flight per wave for more resident waves (the default for 17-32 rows)
-  constexpr int U = PIPE ? 4 : 8;
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
   if (a.gate && *a.gate == 0) return;
-  const int bt = blockIdx.x + a.tile0;  // output row tile
-  const int KT = a.KT;
-  const int per = (KT + NW - 1) / NW;
-  const int kt0 = wave * per;
-  const int kt1 = min(KT, kt0 + per);
-
-  f32x4 acc[RT][NB];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) acc[r][nb] = (f32x4){0.f, 0.f, 0.f, 0.f};
-
-  // A operand: packed weight tiles
-  const u32x4* wbase[RT];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-    wbase[r] = reinterpret_cast<const u32x4*>(a.w) + ((size_t)(bt * RT + r) * KT) * 64 + lane;
-  // B operand: x rows (b = lane&15 + 16 nb), 8 consecutive k at 8*(lane>>4)
-  const u32x4* xbase[NB];
-  bool xok[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    const int b = (lane & 15) + 16 * nb;
-    xok[nb] = b < a.B;
-    xbase[nb] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
-  }
-  // all weight loads of the first k-batch go out before the (latency-bound) norm prologue
-  int kt = kt0;
-  u32x4 wa[RT][U];
-  u32x4 xb[NB][U];
-  // A batch is always U loads; a wave's last batch may cover n < U k-tiles, its surplus loads
-  // re-read the wave's last tile (in-bounds, L2 hits) and their MFMAs see a zero A operand, so
-  // the remainder costs one round trip instead of n dependent single-tile ones.
-  auto issue_w = [&](int k) {
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < RT; ++r)
-        wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)min(k + u, kt1 - 1) * 64);
-  };
-  if (kt < kt1) issue_w(kt);
-
-  // Prologues (PRO) stage the block's B activation rows in LDS once; the MFMA B fragments
-  // are then LDS reads.  PRO_NONE reads the fragments straight from x (L2).
-  //   PRO_NORM:  bf16(nw * bf16(x * r_b)), r_b from the producer's per-16-column sums of
-  //              squares (Qwen3RMSNorm, TF/models/qwen3/modeling_qwen3.py:59-64)
-  //   PRO_ATTN:  the decode attention output, merged here from its per-split (m, l, o)
-  //              partials in split order: x = bf16(sum_s f_s o_s / sum_s f_s l_s),
-  //              f_s = exp(m_s - max m) -- the cross-block combine of attn_decode
-  extern __shared__ u32x4 xs_dyn[];
-  const int K8 = KT * 4;  // 16-byte chunks per row
-  if constexpr (PRO == PRO_NORM) {
-    __shared__ float r_s[32];
-    const int n8x = a.B * K8;
-    for (int i = threadIdx.x; i < n8x + K8; i += NW * 64) {
-      const int b = i / K8, c = i - b * K8;
-      xs_dyn[i] = i < n8x ? reinterpret_cast<const u32x4*>(a.x + (size_t)b * a.ldx)[c]
-                          : reinterpret_cast<const u32x4*>(a.nw)[c];
-    }
-    for (int b = wave; b < a.B; b += NW) {
-      const float* sp = a.ss_in + (size_t)b * a.ld_ss;
-      float ss = 0.f;
-      for (int t4 = lane * 4; t4 < a.n_ss; t4 += 256) {
-        const float4 v = *reinterpret_cast<const float4*>(sp + t4);
-        ss += (v.x + v.y) + (v.z + v.w);
-      }
-      ss = wave_sum(ss);
-      if (lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < n8x; i += NW * 64) {
-      const int b = i / K8;
-      xs_dyn[i] = norm8(xs_dyn[i], xs_dyn[n8x + i - b * K8], r_s[b]);
-    }
-    __syncthreads();
-  } else if constexpr (PRO == PRO_ATTN) {
-    const AttnPartView& v = a.attn;
-    const int nact = *v.pos / v.kb + 1;
-    const int G = v.G, D = v.D, PS = G * (D + 2);
-    for (int i = threadIdx.x; i < a.B * K8; i += NW * 64) {
-      const int b = i / K8, k0 = (i - b * K8) * 8;
-      const int h = k0 / D, d0 = k0 - h * D, kvh = h / G, hg = h - kvh * G;
-      const float* pp = v.part + ((size_t)b * v.Hkv + kvh) * v.ns * PS;
-      float M = -INFINITY;
-      for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, pp[(size_t)s2 * PS + G * D + 2 * hg]);
-      float L = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int s2 = 0; s2 < nact; ++s2) {
-        const float* q = pp + (size_t)s2 * PS;
-        const float ms = q[G * D + 2 * hg];
-        const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
-        L += f * q[G * D + 2 * hg + 1];
-        const float4 o0 = *reinterpret_cast<const float4*>(q + hg * D + d0);
-        const float4 o1 = *reinterpret_cast<const float4*>(q + hg * D + d0 + 4);
-        o[0] += f * o0.x; o[1] += f * o0.y; o[2] += f * o0.z; o[3] += f * o0.w;
-        o[4] += f * o1.x; o[5] += f * o1.y; o[6] += f * o1.z; o[7] += f * o1.w;
-      }
-      u32x4 r;
-#pragma unroll
-      for (int q2 = 0; q2 < 4; ++q2) r[q2] = L > 0.f ? pack2(o[2 * q2] / L, o[2 * q2 + 1] / L) : 0u;
-      xs_dyn[i] = r;
-    }
-    __syncthreads();
-  }
-  // (k < kt1 and the row clamp keep every LDS address inside the staged rows)
-  auto load_x = [&](int k, int nb) -> u32x4 {
-    if (!xok[nb]) return (u32x4){0u, 0u, 0u, 0u};
-    if constexpr (PRO != PRO_NONE) return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
-    return xbase[nb][k * 4];
-  };
-
-  auto compute = [&](u32x4 (&w)[RT][U], int k) {
-    const int n = kt1 - k;  // k-tiles of this batch that are real (>= U: all)
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int nb = 0; nb < NB; ++nb) xb[nb][u] = load_x(min(k + u, kt1 - 1), nb);
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        const u32x4 wv = u < n ? w[r][u] : (u32x4){0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int nb = 0; nb < NB; ++nb)
-          acc[r][nb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              __builtin_bit_cast(bf16x8, wv), __builtin_bit_cast(bf16x8, xb[nb][u]), acc[r][nb], 0, 0, 0);
-      }
-  };
-  for (; kt < kt1; kt += U) {
-    if (kt != kt0) issue_w(kt);
-    compute(wa, kt);
-  }
-
-  // ---- fixed-order reduction of the NW waves' partial tiles through LDS ----
-  __shared__ float red[NW][RT][NB][256];
-  __shared__ float sq[NB][16][17];
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) red[wave][r][nb][lane * 4 + i] = acc[r][nb][i];
-  __syncthreads();
-
-  const int t = threadIdx.x;
-  if (t < 256) {
-    // element t: lane = t/4, reg = t%4 -> n = ((lane>>4)*4 + reg), b = lane & 15
-    const int ln = t >> 2;
-    const int nl = ((ln >> 4) << 2) + (t & 3);
-    const int n = bt * 16 + nl;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int bl = ln & 15;
-      const int b = bl + 16 * nb;
-      float v[RT];
-#pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        float s = 0.f;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) s += red[w][r][nb][t];
-        v[r] = s;
-      }
-      bf16_t out = 0;
-      if constexpr (EPI == EPI_STORE) {
-        out = f2bf(v[0]);
-      } else if constexpr (EPI == EPI_LOGITS) {
-        out = f2bf(v[0]);
-        if (n >= a.pad_start && ((n - a.pad_start) % a.pad_period) == a.pad_off) out = 0xFF80;  // -inf
-      } else if constexpr (EPI == EPI_RESADD) {
-        // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
-        if (b < a.B && n < a.N) out = f2bf(bf2f(a.res[(size_t)b * a.ldres + n]) + rbf(v[0]));
-        const float ho = bf2f(out);
-        sq[nb][bl][nl] = ho * ho;
-      } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
-        const float g = rbf(v[0]);
-        const float u = rbf(v[RT - 1]);
-        const float s = rbf(g / (1.0f + expf(-g)));
-        out = f2bf(s * u);
-      }
-      if (b < a.B && n < a.N) a.y[(size_t)b * a.ldy + n] = out;
-    }
-  }
-  if constexpr (EPI == EPI_RESADD) {
-    __syncthreads();
-    if (a.ss_out && t < 16 * NB) {
-      const int nb = t >> 4, bl = t & 15, b = bl + 16 * nb;
-      if (b < a.B) {
-        float s = 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) s += sq[nb][bl][i];
-        a.ss_out[(size_t)b * a.ld_ss_out + bt] = s;
-      }
-    }
-  }
+  gemv_body<NB, RT, EPI, PRO, NW, PIPE>(a, (int)blockIdx.x + a.tile0, [] {});
 }
 
 // ---------------------------------------------------------------------------

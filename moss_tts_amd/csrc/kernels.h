@@ -176,6 +176,10 @@ int attn_decode_splits(int Cmax);
 int attn_decode_keys_per_block();
 // workspace of attn_decode: ticket counters (zero-filled once by the owner) + partials
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
+// fused.hip: decode attention + o_proj as one launch (block roles by arrival ticket);
+// go = the o_proj GemvArgs (EPI_RESADD, ss_out); sync = 4 zeroed ints owned by the caller
+hipError_t attn_oproj(const DecAttnArgs& da, const GemvArgs& go, int* sync, int B, hipStream_t s);
+int fused_attn_splits(int Cmax);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);
