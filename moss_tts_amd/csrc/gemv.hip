@@ -84,8 +84,25 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16>), dim3(n_tiles), dim3(1024), lds, s, a);
 }
 
+// RT = 2 output tiles per block for the plain projections once the x fragments (B rows per
+// weight tile) cost as much L2 / TA traffic as the weights: MTTS_GEMV_RT2 = min rows (0: off).
+// Only matrices of >= 384 row tiles (q|k|v, the heads): halving the 256-tile o_proj / down
+// grids leaves CUs idle (B=16: o 10.1 -> 12.6 us, down 24.4 -> 30.2) while q|k|v gains
+// (19.1 -> 16.1 us) and the heads gain most (305 -> 245 us; B=32 451 -> 321 us).
+static int rt2_min_rows() {
+  static const int v = getenv("MTTS_GEMV_RT2") ? atoi(getenv("MTTS_GEMV_RT2")) : 12;
+  return v;
+}
+
 template <int RT, int EPI>
 static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
+  if constexpr (RT == 1 && EPI != EPI_SWIGLU) {
+    const int m = rt2_min_rows();
+    if (m > 0 && a.B >= m && !a.attn.part && !a.gate && a.tile0 == 0 && n_tiles % 2 == 0 && n_tiles >= 384) {
+      launch_epi<2, EPI>(a, n_tiles / 2, s);
+      return;
+    }
+  }
   const bool two = a.B > 16;
   if constexpr (EPI == EPI_RESADD) {
     if (a.attn.part) {  // o_proj reading the attention partials (B <= 16)

@@ -157,8 +157,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   }
 
   // ---- fixed-order reduction of the NW waves' partial tiles through LDS ----
+  // SwiGLU: the RT = 2 tiles are a gate and an up tile -> one output tile; otherwise each of
+  // the RT row tiles is an output tile (RT = 2 amortises the x fragments over 32 weight rows)
+  constexpr int OT = EPI == EPI_SWIGLU ? 1 : RT;
   __shared__ float red[NW][RT][NB][256];
-  __shared__ float sq[NB][16][17];
+  __shared__ float sq[OT][NB][16][17];
 #pragma unroll
   for (int r = 0; r < RT; ++r)
 #pragma unroll
@@ -172,48 +175,52 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     // element t: lane = t/4, reg = t%4 -> n = ((lane>>4)*4 + reg), b = lane & 15
     const int ln = t >> 2;
     const int nl = ((ln >> 4) << 2) + (t & 3);
-    const int n = bt * 16 + nl;
 #pragma unroll
-    for (int nb = 0; nb < NB; ++nb) {
-      const int bl = ln & 15;
-      const int b = bl + 16 * nb;
-      float v[RT];
+    for (int ot = 0; ot < OT; ++ot) {
+      const int n = (bt * OT + ot) * 16 + nl;
 #pragma unroll
-      for (int r = 0; r < RT; ++r) {
-        float s = 0.f;
+      for (int nb = 0; nb < NB; ++nb) {
+        const int bl = ln & 15;
+        const int b = bl + 16 * nb;
+        float v[RT];
 #pragma unroll
-        for (int w = 0; w < NW; ++w) s += red[w][r][nb][t];
-        v[r] = s;
+        for (int r = 0; r < RT; ++r) {
+          float s = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) s += red[w][r][nb][t];
+          v[r] = s;
+        }
+        const float vo = v[EPI == EPI_SWIGLU ? 0 : ot];
+        bf16_t out = 0;
+        if constexpr (EPI == EPI_STORE) {
+          out = f2bf(vo);
+        } else if constexpr (EPI == EPI_LOGITS) {
+          out = f2bf(vo);
+          if (n >= a.pad_start && ((n - a.pad_start) % a.pad_period) == a.pad_off) out = 0xFF80;  // -inf
+        } else if constexpr (EPI == EPI_RESADD) {
+          // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
+          if (b < a.B && n < a.N) out = f2bf(bf2f(a.res[(size_t)b * a.ldres + n]) + rbf(vo));
+          const float ho = bf2f(out);
+          sq[ot][nb][bl][nl] = ho * ho;
+        } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
+          const float g = rbf(v[0]);
+          const float u = rbf(v[RT - 1]);
+          const float s = rbf(g / (1.0f + expf(-g)));
+          out = f2bf(s * u);
+        }
+        if (b < a.B && n < a.N) a.y[(size_t)b * a.ldy + n] = out;
       }
-      bf16_t out = 0;
-      if constexpr (EPI == EPI_STORE) {
-        out = f2bf(v[0]);
-      } else if constexpr (EPI == EPI_LOGITS) {
-        out = f2bf(v[0]);
-        if (n >= a.pad_start && ((n - a.pad_start) % a.pad_period) == a.pad_off) out = 0xFF80;  // -inf
-      } else if constexpr (EPI == EPI_RESADD) {
-        // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
-        if (b < a.B && n < a.N) out = f2bf(bf2f(a.res[(size_t)b * a.ldres + n]) + rbf(v[0]));
-        const float ho = bf2f(out);
-        sq[nb][bl][nl] = ho * ho;
-      } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
-        const float g = rbf(v[0]);
-        const float u = rbf(v[RT - 1]);
-        const float s = rbf(g / (1.0f + expf(-g)));
-        out = f2bf(s * u);
-      }
-      if (b < a.B && n < a.N) a.y[(size_t)b * a.ldy + n] = out;
     }
   }
   if constexpr (EPI == EPI_RESADD) {
     __syncthreads();
-    if (a.ss_out && t < 16 * NB) {
-      const int nb = t >> 4, bl = t & 15, b = bl + 16 * nb;
+    if (a.ss_out && t < 16 * NB * OT) {
+      const int ot = t / (16 * NB), nb = (t >> 4) % NB, bl = t & 15, b = bl + 16 * nb;
       if (b < a.B) {
         float s = 0.f;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) s += sq[nb][bl][i];
-        a.ss_out[(size_t)b * a.ld_ss_out + bt] = s;
+        for (int i = 0; i < 16; ++i) s += sq[ot][nb][bl][i];
+        a.ss_out[(size_t)b * a.ld_ss_out + bt * OT + ot] = s;
       }
     }
   }

@@ -10,7 +10,7 @@ import torch  # noqa: E402
 from moss_tts_amd import _native as N  # noqa: E402
 from moss_tts_amd.engine import Engine, EngineConfig  # noqa: E402
 
-e = Engine(EngineConfig(layers=2, max_batch=32, max_ctx=512, max_prefill_tokens=512), 0)
+e = Engine(EngineConfig(layers=8, max_batch=32, max_ctx=512, max_prefill_tokens=512), 0)
 e.init_random(0)
 names = ["qkv", "o", "gu", "down", "heads"]
 for B in [int(x) for x in (sys.argv[1:] or ["1", "4", "16", "17", "32"])]:
