@@ -97,6 +97,14 @@ int mtts_engine_time_gemv(mtts_engine* eng, int which, int layer, int B, int ite
 int mtts_forward(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int S, int past,
                  uint16_t* logits_dev, void* stream);
 int mtts_heads_ld(const mtts_engine* eng);
+/* Workgroups of the persistent decode launch (one decode step's decoder stack as one kernel,
+ * batches <= 2 rows), 0 when this engine decodes with one launch per stage (MTTS_MEGA=0, or a
+ * shape it does not cover). */
+int mtts_mega_workgroups(const mtts_engine* eng);
+/* Diagnostics (engine created with MTTS_MEGA_TRACE=1): the last persistent launch's
+ * s_memrealtime stamps (100 MHz), [layers][stage q|k|v, attention, o, gate|up, down]
+ * [workgroup][wait start, input ready, staged, done]; n = elements of host. */
+int mtts_mega_trace(mtts_engine* eng, uint64_t* host, size_t n);
 
 /* ---- generate (MossTTSDelayModel.generate, modeling_moss_tts.py:392-525) ----
  * begin: state init + prefill + the step-0 sampling.  decode: n more steps (hipGraph).

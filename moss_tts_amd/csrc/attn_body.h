@@ -23,7 +23,9 @@ namespace mtts {
 constexpr int DEC_KW = 32;      // keys per wave
 constexpr int DEC_MAXS = 256;  // splits per head
 
-template <int G, int D, int NWV>
+// SC1 (mega.hip): partials and outputs are stored write-through (sc1) for consumers inside the
+// same launch; the arrival tickets are per layer and reset by the launch's last workgroup
+template <int G, int D, int NWV, bool SC1 = false>
 __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int sp, const int kvh, const int b) {
   constexpr int KW = DEC_KW, KB = KW * NWV;
   constexpr int QS = (D + 31) / 32;  // 32-dim MFMA steps of q.k
@@ -283,7 +285,21 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       o += f * acc_s[w][h][d];
     }
     if (single) {
-      a.out[(size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e] = f2bf(L > 0.f ? o / L : 0.f);
+      bf16_t* op = a.out + (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e;
+      if constexpr (SC1) {
+        typedef __attribute__((address_space(1))) uint16_t g16;
+        __hip_atomic_store((g16*)op, f2bf(L > 0.f ? o / L : 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        *op = f2bf(L > 0.f ? o / L : 0.f);
+      }
+    } else if constexpr (SC1) {
+      typedef __attribute__((address_space(1))) uint32_t g32;
+      __hip_atomic_store((g32*)(part + e), __float_as_uint(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (d == 0) {
+        __hip_atomic_store((g32*)(part + G * D + 2 * h), __float_as_uint(M), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((g32*)(part + G * D + 2 * h + 1), __float_as_uint(L), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
     } else {
       part[e] = o;
       if (d == 0) {
@@ -299,8 +315,12 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
   __syncthreads();
   int* cnt = a.cnt + (size_t)b * a.Hkv + kvh;
   if (t == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // SC1: the partials were stored write-through and drained above (Guideline 16 R1), no
+    // release fence needed
+    if constexpr (!SC1) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_s = ticket == nact - 1;
     if (last_s) {
@@ -329,9 +349,16 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       L += f * mlp[(s2 * G + h) * 2 + 1];
       o += f * p0[(size_t)s2 * PS + e];
     }
-    a.out[(size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e] = f2bf(L > 0.f ? o / L : 0.f);
+    bf16_t* op = a.out + (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e;
+    if constexpr (SC1) {
+      typedef __attribute__((address_space(1))) uint16_t g16;
+      __hip_atomic_store((g16*)op, f2bf(L > 0.f ? o / L : 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      *op = f2bf(L > 0.f ? o / L : 0.f);
+    }
   }
-  if (t == 0) *cnt = 0;  // ready for the next launch (graph replay)
+  // ready for the next launch (graph replay); SC1 (mega.hip): per-layer tickets, reset at exit
+  if (!SC1 && t == 0) *cnt = 0;
 }
 
 }  // namespace mtts

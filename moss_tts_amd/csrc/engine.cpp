@@ -92,6 +92,24 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv)) || (rc = e->alloc(&e->fsync, 4))) return rc;
   if (hipMemset(e->att_cnt, 0, (size_t)c.max_batch * Hkv * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if (hipMemset(e->fsync, 0, 4 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
+  // persistent decode launch: per-layer pointers (the caches move with the capacity) + counters
+  {
+    std::vector<MegaLayer> ml(c.layers);
+    for (int l = 0; l < c.layers; ++l) {
+      const LayerW& w = e->L[l];
+      ml[l] = MegaLayer{w.qkv, w.o, w.gu, w.down, w.in_norm, w.post_norm, w.q_norm, w.k_norm,
+                        e->kc + l * e->layer_kv, e->vc + l * e->layer_kv};
+    }
+    const int nsync = mega_sync_words(c.layers, Hkv);
+    if ((rc = e->alloc(&e->mega_L, (size_t)c.layers)) || (rc = e->alloc(&e->mega_sync, (size_t)nsync))) return rc;
+    if (hipMemcpy(e->mega_L, ml.data(), ml.size() * sizeof(MegaLayer), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(e->mega_sync, 0, nsync * sizeof(uint32_t)) != hipSuccess)
+      return fail(MTTS_E_HIP, "mega state");
+    e->mega_P = mega_grid(e->device, mega_lds_bytes(MEGA_MAXB, H, Hq * D, I));
+    if (getenv("MTTS_MEGA_TRACE") && e->mega_P > 0 &&
+        (rc = e->alloc(&e->mega_trace, (size_t)c.layers * 5 * e->mega_P * 4)))
+      return rc;
+  }
   // generate state
   const int B = c.max_batch;
   if ((rc = e->alloc(&e->st, 1)) || (rc = e->alloc(&e->is_stopping, B)) || (rc = e->alloc(&e->is_audio, B)) ||
@@ -131,6 +149,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_UNFUSED_ATTN")) e->unfused_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
+  if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -205,6 +224,18 @@ extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
   return 0;
 }
 extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
+extern "C" int mtts_mega_workgroups(const mtts_engine* e) {
+  return e && e->mega && e->c.head_dim == 128 ? e->mega_P : 0;
+}
+extern "C" int mtts_mega_trace(mtts_engine* e, uint64_t* host, size_t n) {
+  if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
+  if (!e->mega_trace) return fail(MTTS_E_UNSUPPORTED, "engine created without MTTS_MEGA_TRACE=1");
+  const size_t have = (size_t)e->c.layers * 5 * e->mega_P * 4;
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(host, e->mega_trace, std::min(n, have) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return 0;
+}
 
 // ---------------------------------------------------------------------------
 // weight loading by reference state_dict name
@@ -408,6 +439,19 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   const int M = B * S;
   const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
   const float eps = e->c.rms_eps;
+  if (S == 1 && B <= MEGA_MAXB && e->mega && e->mega_P > 0 && st.cos_t && st.L == e->L.data() && D == 128) {
+    // the whole stack as one persistent launch (mega.hip)
+    MegaArgs ma{};
+    ma.L = e->mega_L; ma.layers = st.layers; ma.h = st.h; ma.ss = st.ss; ma.qkvb = st.qkvb; ma.act = st.act;
+    ma.part = st.part; ma.cos_t = st.cos_t; ma.sin_t = st.sin_t; ma.mask = st.mask + (size_t)b0 * st.Cmax;
+    ma.pos = pos_base; ma.B = B; ma.H = H; ma.Hq = Hq; ma.Hkv = Hkv; ma.D = D; ma.I = I; ma.qkv_rows = st.qkv_rows;
+    ma.Cmax = st.Cmax; ma.eps = e->c.rms_eps; ma.scale = 1.0f / std::sqrt((float)D); ma.sync = e->mega_sync;
+    ma.attnb = st.attnb; ma.w_err = mega_err_word(st.layers, Hkv); ma.trace = e->mega_trace;
+    if (b0 == 0) {
+      HIPCHK(mega_decode(ma, e->mega_P, s));
+      return 0;
+    }
+  }
   const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn;
   for (int l = 0; l < st.layers; ++l) {
     const LayerW& w = st.L[l];
@@ -669,6 +713,14 @@ extern "C" int mtts_generate_poll(mtts_engine* e, int* steps, int* done_step, vo
   HIPCHK(hipStreamSynchronize(e->stream));
   GenDev g;
   HIPCHK(hipMemcpy(&g, e->st, sizeof(g), hipMemcpyDeviceToHost));
+  if (e->mega_sync) {  // a persistent decode launch that gave up waiting (mega.hip) poisons the run
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, e->mega_sync + mega_err_word(e->c.layers, e->c.n_kv), 4, hipMemcpyDeviceToHost));
+    if (err) {
+      hipMemset(e->mega_sync, 0, mega_sync_words(e->c.layers, e->c.n_kv) * sizeof(uint32_t));
+      return fail(MTTS_E_HIP, "persistent decode launch: a stage wait timed out (results invalid)");
+    }
+  }
   if (steps) *steps = g.step;
   if (done_step) *done_step = g.done_step;
   (void)stream;

@@ -81,6 +81,12 @@ struct mtts_engine {
   bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)
   bool fused_ao = false;          // MTTS_FUSED_AO=1: decode attention + o_proj as one launch (fused.hip; A/B, slower)
   int* fsync = nullptr;
+  // persistent decode launch (mega.hip): MTTS_MEGA=1 turns it on (A/B; off until it wins)
+  bool mega = false;
+  MegaLayer* mega_L = nullptr;   // device [layers]
+  uint32_t* mega_sync = nullptr; // device, mega_sync_words(layers), zero between launches
+  int mega_P = 0;                // workgroups (CUs); 0: unsupported here
+  uint64_t* mega_trace = nullptr; // MTTS_MEGA_TRACE=1: per-stage timestamps of the last launch
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};

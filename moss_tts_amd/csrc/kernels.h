@@ -180,6 +180,41 @@ size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 // go = the o_proj GemvArgs (EPI_RESADD, ss_out); sync = 4 zeroed ints owned by the caller
 hipError_t attn_oproj(const DecAttnArgs& da, const GemvArgs& go, int* sync, int B, hipStream_t s);
 int fused_attn_splits(int Cmax);
+
+// mega.hip: the decoder-layer stack of one decode step as one persistent launch
+constexpr int MEGA_MAXB = 2;
+constexpr size_t MEGA_LDS_LIMIT = 160 * 1024;
+struct MegaLayer {
+  const bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
+  bf16_t *kc, *vc;  // this layer's caches (row 0)
+};
+
+struct MegaArgs {
+  const MegaLayer* L;
+  int layers;
+  bf16_t* h;        // [B, H] residual stream (in / out)
+  float* ss;        // [B, H/16] its per-16-column sums of squares (in / out)
+  bf16_t* qkvb;     // [B, qkv_rows]
+  bf16_t* act;      // [B, I]
+  float* part;      // attention partials [B][Hkv][ns][G*(D+2)]
+  const bf16_t *cos_t, *sin_t;
+  const uint8_t* mask;  // [B][Cmax] (rows of this launch)
+  const int* pos;
+  int B, H, Hq, Hkv, D, I, qkv_rows, Cmax, ns;
+  float eps, scale;
+  bf16_t* attnb;    // [B, Hq*D] attention output
+  uint32_t* sync;   // mega_sync_words: stage counters [layers][5], attention tickets
+                    // [layers][MEGA_MAXB][Hkv], exit ticket, error word (= w_err)
+  int w_err;        // mega_err_word(layers, Hkv)
+  uint64_t* trace;  // nullptr, or [layers][5][P][4] s_memrealtime stamps (wait, ready, staged, done)
+  int lds_x1, lds_x2;  // LDS byte offsets of the two activation regions (dynamic LDS)
+};
+
+size_t mega_lds_bytes(int B, int H, int HqD, int I);
+int mega_sync_words(int layers, int Hkv);  // zeroed words the launch needs (multiple of 4)
+int mega_err_word(int layers, int Hkv);    // index of the error word in them
+int mega_grid(int device, size_t lds);  // workgroups per launch (one per CU), 0: unsupported
+hipError_t mega_decode(const MegaArgs& a, int P, hipStream_t s);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);

@@ -131,6 +131,10 @@ class Engine:
     def init_random(self, seed: int = 0):
         N.check(N.load().mtts_engine_init_random(self._h, seed), "init_random")
 
+    def mega_workgroups(self) -> int:
+        """Workgroups of the persistent decode launch (0: one launch per stage)."""
+        return int(N.load().mtts_mega_workgroups(self._h))
+
     def weight_bytes(self):
         v = ctypes.c_uint64()
         N.check(N.load().mtts_engine_weight_bytes(self._h, ctypes.byref(v)), "weight_bytes")
