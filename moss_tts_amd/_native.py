@@ -8,7 +8,7 @@ runtime failures).
 import ctypes
 import os
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmtts.so")
+_LIB_PATH = os.environ.get("MTTS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmtts.so")
 
 MTTS_OK = 0
 MTTS_E_INVALID = -1
@@ -34,6 +34,20 @@ class MttsSampling(ctypes.Structure):
     _fields_ = [("text_temperature", ctypes.c_float), ("text_top_p", ctypes.c_float), ("text_top_k", ctypes.c_int),
                 ("audio_temperature", ctypes.c_float), ("audio_top_p", ctypes.c_float), ("audio_top_k", ctypes.c_int),
                 ("audio_repetition_penalty", ctypes.c_float), ("seed", ctypes.c_uint64)]
+
+
+class MttsCodecStage(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in ("hidden", "layers", "n_heads", "n_kv", "head_dim", "inter", "upsample")]
+
+
+MTTS_CODEC_MAX_STAGES = 8
+
+
+class MttsCodecConfig(ctypes.Structure):
+    _fields_ = [("n_q", ctypes.c_int), ("codebook_size", ctypes.c_int), ("n_stages", ctypes.c_int),
+                ("stages", MttsCodecStage * MTTS_CODEC_MAX_STAGES), ("patch", ctypes.c_int),
+                ("rope_theta", ctypes.c_float), ("rms_eps", ctypes.c_float),
+                ("max_batch", ctypes.c_int), ("max_frames", ctypes.c_int), ("max_chunk_frames", ctypes.c_int)]
 
 
 P = ctypes.c_void_p
@@ -85,6 +99,16 @@ _SIGS = {
     "mtts_k_attn_decode": (I, [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, F, P]),
     "mtts_rope_table": (I, [F, I, I, P, P]),
     "mtts_k_fill_uniform": (I, [P, SZ, U64, U64, F, F, P]),
+    # codec decoder (include/mtts_codec.h)
+    "mtts_codec_create": (I, [ctypes.POINTER(MttsCodecConfig), I, ctypes.POINTER(P)]),
+    "mtts_codec_destroy": (I, [P]),
+    "mtts_codec_load_weight": (I, [P, ctypes.c_char_p, P, SZ, I]),
+    "mtts_codec_init_random": (I, [P, U64]),
+    "mtts_codec_samples_per_frame": (I, [P]),
+    "mtts_codec_position": (I, [P]),
+    "mtts_codec_reset": (I, [P]),
+    "mtts_codec_decode": (I, [P, P, I, I, I, I, P, SZ, P]),
+    "mtts_codec_weight_bytes": (I, [P, ctypes.POINTER(U64)]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -1,5 +1,5 @@
 """CPU-side checks of the drop-in boundary: libmtts.so loads (no GPU needed to
-dlopen) and exports exactly the entry points include/mtts.h declares."""
+dlopen) and exports exactly the entry points include/*.h declare."""
 import ctypes
 import os
 import re
@@ -10,10 +10,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def declared_symbols():
-    with open(os.path.join(ROOT, "include", "mtts.h")) as f:
-        txt = f.read()
-    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(mtts_[a-z0-9_]+)\s*\(", txt)))
+    out = set()
+    for h in sorted(os.listdir(os.path.join(ROOT, "include"))):
+        if not h.endswith(".h"):
+            continue
+        with open(os.path.join(ROOT, "include", h)) as f:
+            txt = f.read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        out |= set(re.findall(r"\b(mtts_[a-z0-9_]+)\s*\(", txt))
+    return sorted(out)
 
 
 def test_header_and_binding_agree():
@@ -40,6 +45,8 @@ def test_errors_map_to_reference_exceptions():
     # null config -> MTTS_E_INVALID -> ValueError (the reference raises ValueError on bad inputs)
     with pytest.raises(ValueError):
         _native.check(_native.load().mtts_engine_create(None, 0, None), "create")
+    with pytest.raises(ValueError):
+        _native.check(_native.load().mtts_codec_create(None, 0, None), "codec create")
 
 
 def test_rope_table_host_path():
