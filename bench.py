@@ -359,6 +359,41 @@ def main_local(args, world, rank, local):
         print(json.dumps(res), flush=True)
 
 
+def codec_leg(frames: int, n_vq: int) -> dict:
+    """Codec decoder (csrc/codec.cpp, the assumed MOSS-Audio-Tokenizer decode shape with random
+    weights): one utterance's frames decoded at once, and the first 1 s chunk (13 frames) as a
+    streaming decode would emit it.  Codes are synthetic (the decoder's cost does not depend on
+    their values)."""
+    import torch
+    from moss_tts_amd.codec import AudioTokenizerDecoder, CodecConfig
+    dec = AudioTokenizerDecoder(CodecConfig(max_batch=1, max_frames=max(256, frames + 16), max_chunk_frames=256), 0)
+    dec.init_random(0)
+    codes = torch.randint(0, 1024, (1, frames, n_vq), dtype=torch.int64, device="cuda")
+    first = codes[:, :13]
+
+    def timed(fn, reps):
+        ts = []
+        for _ in range(reps):
+            dec.reset()
+            torch.cuda.synchronize()
+            a = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            ts.append((time.perf_counter() - a) * 1e3)
+        return float(np.median(ts))
+
+    timed(lambda: dec.decode_frames(codes), 2)  # warm-up
+    whole = timed(lambda: dec.decode_frames(codes), 5)
+    chunk = timed(lambda: dec.decode_frames(first), 5)
+    out = {"frames": frames, "ms": round(whole, 3), "audio_s_per_s": round(frames / FRAME_RATE / (whole * 1e-3), 2),
+           "first_chunk_frames": 13, "first_chunk_ms": round(chunk, 3), "weight_bytes": dec.weight_bytes(),
+           "samples_per_frame": dec.samples_per_frame,
+           "shape": "assumed decoder (RVQ 32x1024, 4 causal Transformer stages 12.5->100 Hz, 240-sample patches); "
+                    "parity unpinned vs the real codec (absent from the reference)"}
+    dec.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -369,6 +404,7 @@ def main():
     ap.add_argument("--decode-steps", type=int, default=208)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-codec", action="store_true", help="skip the codec-decoder leg")
     ap.add_argument("--extra-batches", default="4,32", help="extra per-GPU batch sizes reported in batch_sweep")
     ap.add_argument("--config", choices=["clone", "ttsd", "local"], default="clone",
                     help="clone: configs[1] (default); ttsd: configs[4], MOSS-TTSD long form (n_vq 16, a "
@@ -538,6 +574,9 @@ def main():
         res["decode_step_hbm_frac"] = round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
         if sweep:
             res["batch_sweep"] = sweep
+        if not args.no_codec and args.config == "clone":
+            res["codec"] = codec_leg(frames0, n_vq)
+            res["p50_first_chunk_ms_incl_codec"] = round(p50 + res["codec"]["first_chunk_ms"], 2)
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline(args, int(T), n_steps, frames0)
         elif not args.no_cpu_baseline:

@@ -92,6 +92,9 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv)) || (rc = e->alloc(&e->fsync, 4))) return rc;
   if (hipMemset(e->att_cnt, 0, (size_t)c.max_batch * Hkv * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if (hipMemset(e->fsync, 0, 4 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
+  if ((rc = e->alloc(&e->ao_part, attn_o_ws_floats(H, Hkv))) || (rc = e->alloc(&e->ao_cnt, (size_t)attn_o_chunks(H))))
+    return rc;
+  if (hipMemset(e->ao_cnt, 0, attn_o_chunks(H) * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   // persistent decode launch: per-layer pointers (the caches move with the capacity) + counters
   {
     std::vector<MegaLayer> ml(c.layers);
@@ -150,6 +153,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
   if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
+  if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -226,6 +230,10 @@ extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
 extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
 extern "C" int mtts_mega_workgroups(const mtts_engine* e) {
   return e && e->mega && e->c.head_dim == 128 ? e->mega_P : 0;
+}
+extern "C" int mtts_attn_o_active(const mtts_engine* e, int B) {
+  return e && e->ao && e->c.max_ctx <= AO_MAX_CTX &&
+         attn_o_supported(B, e->c.n_heads, e->c.n_kv, e->c.head_dim, e->c.hidden) ? 1 : 0;
 }
 extern "C" int mtts_mega_trace(mtts_engine* e, uint64_t* host, size_t n) {
   if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
@@ -410,6 +418,7 @@ Stack backbone_stack(mtts_engine* e) {
   st.cos_t = e->cos_t; st.sin_t = e->sin_t; st.mask = e->mask;
   st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
   st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt; st.fsync = e->fsync;
+  st.ao_part = e->ao_part; st.ao_cnt = e->ao_cnt;
   return st;
 }
 
@@ -453,6 +462,10 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     }
   }
   const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn;
+  // short contexts: attention + o_proj + residual in one launch (ao.hip); its blocks re-read
+  // their KV head from L2 once per o_proj row chunk, so long contexts keep the split form
+  const bool use_ao = S == 1 && e->ao && st.ao_part && st.cos_t && st.Cmax <= AO_MAX_CTX &&
+                      attn_o_supported(B, Hq, Hkv, D, H);
   for (int l = 0; l < st.layers; ++l) {
     const LayerW& w = st.L[l];
     bf16_t* kc = st.kc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
@@ -464,7 +477,17 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     // decode, small batch: attention + o_proj in one launch (fused.hip)
     const bool fused_ao = fuse_attn && e->fused_ao && st.fsync &&
                           fused_attn_splits(st.Cmax) * Hkv * B <= 1024;
-    if (S == 1) {
+    if (use_ao) {
+      AOArgs aa{};
+      aa.qkv = st.qkvb; aa.qn_w = w.q_norm; aa.kn_w = w.k_norm; aa.cos_t = st.cos_t; aa.sin_t = st.sin_t;
+      aa.kc = kc; aa.vc = vc; aa.mask = st.mask + (size_t)b0 * st.Cmax; aa.pos = pos_base; aa.wo = w.o;
+      aa.h = st.h; aa.ldh = H; aa.ss_out = st.ss; aa.ld_ss = NT; aa.part = st.ao_part; aa.cnt = st.ao_cnt;
+      aa.B = B; aa.H = H; aa.NRT = H / 16; aa.KT = Hq * D / 32; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = st.Cmax;
+      aa.eps = eps; aa.scale = 1.0f / std::sqrt((float)D);
+      static const int ao_probe = getenv("MTTS_AO_PROBE") ? atoi(getenv("MTTS_AO_PROBE")) : 0;
+      aa.probe = ao_probe;
+      HIPCHK(attn_o(aa, s));
+    } else if (S == 1) {
       DecAttnArgs da{};
       da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
       da.kc = kc; da.vc = vc; da.mask = st.mask + (size_t)b0 * st.Cmax; da.pos = pos_base; da.out = st.attnb;
@@ -494,7 +517,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       if (e->old_prefill_attn) HIPCHK(attention(aa, s));
       else HIPCHK(attention_prefill(aa, s));
     }
-    if (!(S == 1 && fused_ao)) {
+    if (!(S == 1 && fused_ao) && !use_ao) {
       g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
       g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
       if (fuse_attn) {

@@ -46,7 +46,11 @@ struct Stack {
   float* part = nullptr;
   int* att_cnt = nullptr;
   int* fsync = nullptr;     // 4 ticket words of the fused attention + o_proj launch (zero between launches)
+  float* ao_part = nullptr; // attention + o_proj launch (ao.hip): split-K partials and row-chunk tickets
+  int* ao_cnt = nullptr;
 };
+
+constexpr int AO_MAX_CTX = 2048;  // largest KV capacity that decodes through ao.hip
 
 inline size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
 
@@ -81,6 +85,11 @@ struct mtts_engine {
   bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)
   bool fused_ao = false;          // MTTS_FUSED_AO=1: decode attention + o_proj as one launch (fused.hip; A/B, slower)
   int* fsync = nullptr;
+  // decode attention + o_proj + residual as one launch (ao.hip); MTTS_AO=1 turns it on (A/B;
+  // off until it beats attn_decode + the o_proj GEMV)
+  bool ao = false;
+  float* ao_part = nullptr;
+  int* ao_cnt = nullptr;
   // persistent decode launch (mega.hip): MTTS_MEGA=1 turns it on (A/B; off until it wins)
   bool mega = false;
   MegaLayer* mega_L = nullptr;   // device [layers]

@@ -181,6 +181,32 @@ size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 hipError_t attn_oproj(const DecAttnArgs& da, const GemvArgs& go, int* sync, int B, hipStream_t s);
 int fused_attn_splits(int Cmax);
 
+// ao.hip: decode attention + o_proj + residual as one launch without block roles: every
+// block recomputes its KV head's attention from L2 and streams its own o_proj weight slab
+constexpr int AO_MAXB = 1;
+struct AOArgs {
+  const bf16_t* qkv;    // [B, (Hq + 2 Hkv) * D]  output of the q|k|v GEMV
+  const bf16_t *qn_w, *kn_w, *cos_t, *sin_t;
+  bf16_t *kc, *vc;      // layer cache, K [B][Hkv][Cmax][D], V^T [B][Hkv][D][Cmax] (rows of this launch)
+  const uint8_t* mask;  // [B][Cmax]
+  const int* pos;       // device: position of the new token
+  const bf16_t* wo;     // packed o_proj tiles [NRT][KT]
+  bf16_t* h;            // [B, ldh] residual stream (in / out)
+  int ldh;
+  float* ss_out;        // [B, ld_ss] per-16-column sums of squares of the new h
+  int ld_ss;
+  float* part;          // attn_o_ws_floats(H, Hkv)
+  int* cnt;             // attn_o_chunks(H) tickets, zero between launches
+  int B, H, NRT, KT, Hq, Hkv, D, Cmax;
+  float eps, scale;
+  int probe;  // timing probe (MTTS_AO_PROBE; results invalid): 1 no attention, 2 no weight DMA, 3 no split-K epilogue,
+              // 4 attention in row chunk 0 only
+};
+int attn_o_chunks(int H);
+size_t attn_o_ws_floats(int H, int Hkv);
+bool attn_o_supported(int B, int Hq, int Hkv, int D, int H);
+hipError_t attn_o(const AOArgs& a, hipStream_t s);
+
 // mega.hip: the decoder-layer stack of one decode step as one persistent launch
 constexpr int MEGA_MAXB = 2;
 constexpr size_t MEGA_LDS_LIMIT = 160 * 1024;

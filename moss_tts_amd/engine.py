@@ -135,6 +135,10 @@ class Engine:
         """Workgroups of the persistent decode launch (0: one launch per stage)."""
         return int(N.load().mtts_mega_workgroups(self._h))
 
+    def attn_o_active(self, batch: int) -> bool:
+        """Whether a decode step of `batch` rows runs attention + o_proj as one launch (ao.hip)."""
+        return bool(N.load().mtts_attn_o_active(self._h, batch))
+
     def weight_bytes(self):
         v = ctypes.c_uint64()
         N.check(N.load().mtts_engine_weight_bytes(self._h, ctypes.byref(v)), "weight_bytes")
