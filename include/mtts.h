@@ -104,6 +104,9 @@ int mtts_mega_workgroups(const mtts_engine* eng);
 /* 1 when a decode step of B rows runs attention + o_proj + residual as one launch per layer
  * (ao.hip: B == 1, head_dim 128, KV capacity <= 2048, engine created with MTTS_AO=1), else 0. */
 int mtts_attn_o_active(const mtts_engine* eng, int B);
+/* 1 when a decode step of B rows runs the q|k|v projection and the attention as one launch per
+ * layer (qa.hip: B <= 8 with the fused input RMSNorm, engine created with MTTS_QA=1), else 0. */
+int mtts_qkv_attn_active(const mtts_engine* eng, int B);
 /* Diagnostics (engine created with MTTS_MEGA_TRACE=1): the last persistent launch's
  * s_memrealtime stamps (100 MHz), [layers][stage q|k|v, attention, o, gate|up, down]
  * [workgroup][wait start, input ready, staged, done]; n = elements of host. */

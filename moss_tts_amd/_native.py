@@ -71,6 +71,7 @@ _SIGS = {
     "mtts_heads_ld": (I, [P]),
     "mtts_mega_workgroups": (I, [P]),
     "mtts_attn_o_active": (I, [P, I]),
+    "mtts_qkv_attn_active": (I, [P, I]),
     "mtts_mega_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),
     "mtts_generate_begin": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, P]),
     "mtts_generate_decode": (I, [P, I, P]),

@@ -38,7 +38,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* p, uint32_t 
 // workgroup barrier over LDS only: __syncthreads() is a workgroup release fence, which on
 // gfx9 waits vmcnt(0) for the block's global stores (the KV append) -- and with them for
 // every weight load in flight, serialising the o_proj stream behind the attention chain
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// (the loader waves skip the lgkmcnt wait: it would hold them -- and the barrier -- until their
+// LDS-DMA weight stream has landed)
+__device__ __forceinline__ void lds_barrier(bool loader) {
+  if (loader)
+    asm volatile("s_barrier" ::: "memory");
+  else
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
 constexpr int AO_NA = 8;              // attention waves per block (each: one o_proj row tile at the end)
 constexpr int AO_NW = AO_NA;          // o_proj row tiles per block
 constexpr int AO_NL = 2;              // loader waves per block
@@ -192,7 +199,7 @@ __global__ __launch_bounds__(AO_T) void attn_o_kernel(AOArgs a) {
       }
     }
     }  // attention waves
-    lds_barrier();
+    lds_barrier(owave);
 
     if (!owave && att_on) {
     // ---- passes of 256 keys: online softmax per head (lane & 15) ----
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(AO_T) void attn_o_kernel(AOArgs a) {
         if (h < G) acc_s[wave][h][dt * 16 + c16] = o_run[dt][r];
       }
     }  // attention waves
-    lds_barrier();
+    lds_barrier(owave);
     // ---- merge the 8 wave partials (fixed order): x = bf16(o / l) ----
     for (int e = threadIdx.x; e < G * D; e += AO_T) {
       const int h = e / D, d = e % D;
@@ -328,7 +335,7 @@ __global__ __launch_bounds__(AO_T) void attn_o_kernel(AOArgs a) {
       x_s[b][e] = f2bf(L > 0.f ? o / L : 0.f);
     }
     if (owave) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the weight slab has landed
-    lds_barrier();
+    lds_barrier(owave);
   }
 
   // ---- o_proj partial of this wave's row tile over head group g ----

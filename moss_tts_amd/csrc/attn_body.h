@@ -23,10 +23,19 @@ namespace mtts {
 constexpr int DEC_KW = 32;      // keys per wave
 constexpr int DEC_MAXS = 256;  // splits per head
 
+struct NoWait {
+  __device__ void operator()() const {}
+};
+
 // SC1 (mega.hip): partials and outputs are stored write-through (sc1) for consumers inside the
-// same launch; the arrival tickets are per layer and reset by the launch's last workgroup
-template <int G, int D, int NWV, bool SC1 = false>
-__device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int sp, const int kvh, const int b) {
+// same launch; the arrival tickets are per layer and reset by the launch's last workgroup.
+// Wait (qa.hip): the block's K / V^T / mask loads, which do not depend on the q|k|v GEMV, go
+// out first; wait() then blocks until the q|k|v rows are published, and only then does the
+// prologue read them.
+template <int G, int D, int NWV, bool SC1 = false, class Wait = NoWait>
+__device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int sp, const int kvh, const int b,
+                                                 const Wait& wait = Wait{}) {
+  constexpr bool PF = !__is_same(Wait, NoWait);
   constexpr int KW = DEC_KW, KB = KW * NWV;
   constexpr int QS = (D + 31) / 32;  // 32-dim MFMA steps of q.k
   constexpr int DT = (D + 15) / 16;  // 16-dim output tiles of p.v
@@ -54,27 +63,6 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
   bf16_t* vcache = a.vc + (((size_t)b * a.Hkv + kvh) * D) * Cmax;  // [D][Cmax]
   const uint8_t* mrow = a.mask + (size_t)b * Cmax;
 
-  // ---- prologue loads: job j < G: q head j; G: k; G+1: v (k, v only in the owner);
-  // wave w takes jobs w, w + NWV, ... ----
-  constexpr int JOBS = (G + 2 + NWV - 1) / NWV;
-  const int njobs = G + (owner ? 2 : 0);
-  uint32_t pr[JOBS], pw[JOBS], pc[JOBS], ps[JOBS];
-#pragma unroll
-  for (int jj = 0; jj < JOBS; ++jj) {
-    const int j = wave + jj * NWV;
-    pr[jj] = pw[jj] = pc[jj] = ps[jj] = 0;
-    if (j < njobs && 2 * lane < D) {
-      const int hd = j < G ? kvh * G + j : (j == G ? a.Hq + kvh : a.Hq + a.Hkv + kvh);
-      pr[jj] = *reinterpret_cast<const uint32_t*>(row + (size_t)hd * D + 2 * lane);
-      if (j <= G) {
-        pw[jj] = *reinterpret_cast<const uint32_t*>((j < G ? a.qn_w : a.kn_w) + 2 * lane);
-        if (a.cos_t) {
-          pc[jj] = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
-          ps[jj] = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
-        }
-      }
-    }
-  }
   // ---- a wave's 32 keys k0..k0+31: K tiles (A operands), V^T fragments (B operands), mask.
   // Keys >= pos read as zero; the new key / value are patched in from LDS below. ----
   u32x4 kt[2][QS];
@@ -102,7 +90,35 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
     }
   };
   const int kbeg = sp * KB + wave * KW;
-  if (kbeg <= pos) load_keys(kbeg);
+  if constexpr (PF) {
+    if (kbeg <= pos) load_keys(kbeg);
+    wait();
+  }
+
+  // ---- prologue loads: job j < G: q head j; G: k; G+1: v (k, v only in the owner);
+  // wave w takes jobs w, w + NWV, ... ----
+  constexpr int JOBS = (G + 2 + NWV - 1) / NWV;
+  const int njobs = G + (owner ? 2 : 0);
+  uint32_t pr[JOBS], pw[JOBS], pc[JOBS], ps[JOBS];
+#pragma unroll
+  for (int jj = 0; jj < JOBS; ++jj) {
+    const int j = wave + jj * NWV;
+    pr[jj] = pw[jj] = pc[jj] = ps[jj] = 0;
+    if (j < njobs && 2 * lane < D) {
+      const int hd = j < G ? kvh * G + j : (j == G ? a.Hq + kvh : a.Hq + a.Hkv + kvh);
+      pr[jj] = *reinterpret_cast<const uint32_t*>(row + (size_t)hd * D + 2 * lane);
+      if (j <= G) {
+        pw[jj] = *reinterpret_cast<const uint32_t*>((j < G ? a.qn_w : a.kn_w) + 2 * lane);
+        if (a.cos_t) {
+          pc[jj] = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
+          ps[jj] = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
+        }
+      }
+    }
+  }
+  if constexpr (!PF) {
+    if (kbeg <= pos) load_keys(kbeg);
+  }
 
   // ---- prologue math ----
 #pragma unroll

@@ -95,6 +95,8 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->ao_part, attn_o_ws_floats(H, Hkv))) || (rc = e->alloc(&e->ao_cnt, (size_t)attn_o_chunks(H))))
     return rc;
   if (hipMemset(e->ao_cnt, 0, attn_o_chunks(H) * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
+  if ((rc = e->alloc(&e->qsync, 16))) return rc;
+  if (hipMemset(e->qsync, 0, 16 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   // persistent decode launch: per-layer pointers (the caches move with the capacity) + counters
   {
     std::vector<MegaLayer> ml(c.layers);
@@ -154,6 +156,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
   if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
   if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
+  if (const char* v = getenv("MTTS_QA")) e->qa = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -234,6 +237,14 @@ extern "C" int mtts_mega_workgroups(const mtts_engine* e) {
 extern "C" int mtts_attn_o_active(const mtts_engine* e, int B) {
   return e && e->ao && e->c.max_ctx <= AO_MAX_CTX &&
          attn_o_supported(B, e->c.n_heads, e->c.n_kv, e->c.head_dim, e->c.hidden) ? 1 : 0;
+}
+extern "C" int mtts_qkv_attn_active(const mtts_engine* e, int B) {
+  if (!e || !e->qa || e->ao || e->fused_ao || e->unfused_attn || B > QA_MAXB || B <= 0) return 0;
+  GemvArgs g = gemv_args(e->L[0].qkv, e->h, e->c.hidden, e->qkvb, e->qkv_rows, B, e->qkv_rows, e->c.hidden);
+  g.ss_in = norm_lds_bytes(B, e->c.hidden) <= NORM_LDS_MAX && !e->unfused_norm ? e->ss : nullptr;
+  DecAttnArgs da{};
+  da.Hq = e->c.n_heads; da.Hkv = e->c.n_kv; da.D = e->c.head_dim; da.Cmax = e->c.max_ctx;
+  return qkv_attn_supported(g, da, B) ? 1 : 0;
 }
 extern "C" int mtts_mega_trace(mtts_engine* e, uint64_t* host, size_t n) {
   if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
@@ -418,7 +429,7 @@ Stack backbone_stack(mtts_engine* e) {
   st.cos_t = e->cos_t; st.sin_t = e->sin_t; st.mask = e->mask;
   st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
   st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt; st.fsync = e->fsync;
-  st.ao_part = e->ao_part; st.ao_cnt = e->ao_cnt;
+  st.ao_part = e->ao_part; st.ao_cnt = e->ao_cnt; st.qsync = e->qsync;
   return st;
 }
 
@@ -473,7 +484,18 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     GemvArgs g = gemv_args(w.qkv, st.xn, H, st.qkvb, st.qkv_rows, M, st.qkv_rows, H);
     if (int rc = normed_input(e, st, g, w.in_norm, M, s)) return rc;
     g.force_nw = e->nw[0];
-    HIPCHK(proj(e, g, EPI_STORE, s));
+    DecAttnArgs da{};
+    da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
+    da.kc = kc; da.vc = vc; da.mask = st.mask + (size_t)b0 * st.Cmax; da.pos = pos_base; da.out = st.attnb;
+    da.part = st.part; da.cnt = st.att_cnt;
+    // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
+    da.publish_only = fuse_attn ? 1 : 0;
+    da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
+    // decode, small batch: q|k|v projection + attention in one launch (qa.hip)
+    const bool use_qa = S == 1 && fuse_attn && e->qa && st.qsync && !use_ao && !e->fused_ao && B <= QA_MAXB &&
+                        qkv_attn_supported(g, da, B);
+    if (use_qa) HIPCHK(qkv_attn(g, da, st.qsync, B, s));
+    else HIPCHK(proj(e, g, EPI_STORE, s));
     // decode, small batch: attention + o_proj in one launch (fused.hip)
     const bool fused_ao = fuse_attn && e->fused_ao && st.fsync &&
                           fused_attn_splits(st.Cmax) * Hkv * B <= 1024;
@@ -487,14 +509,9 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       static const int ao_probe = getenv("MTTS_AO_PROBE") ? atoi(getenv("MTTS_AO_PROBE")) : 0;
       aa.probe = ao_probe;
       HIPCHK(attn_o(aa, s));
+    } else if (use_qa) {
+      // attention ran with the projection
     } else if (S == 1) {
-      DecAttnArgs da{};
-      da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
-      da.kc = kc; da.vc = vc; da.mask = st.mask + (size_t)b0 * st.Cmax; da.pos = pos_base; da.out = st.attnb;
-      da.part = st.part; da.cnt = st.att_cnt;
-      // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
-      da.publish_only = fuse_attn ? 1 : 0;
-      da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
       if (fused_ao) {
         GemvArgs go = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
         go.res = st.h; go.ldres = H; go.ss_out = st.ss; go.ld_ss_out = NT;

@@ -48,6 +48,7 @@ struct Stack {
   int* fsync = nullptr;     // 4 ticket words of the fused attention + o_proj launch (zero between launches)
   float* ao_part = nullptr; // attention + o_proj launch (ao.hip): split-K partials and row-chunk tickets
   int* ao_cnt = nullptr;
+  int* qsync = nullptr;     // 16 counter words of the q|k|v + attention launch (qa.hip; zero between launches)
 };
 
 constexpr int AO_MAX_CTX = 2048;  // largest KV capacity that decodes through ao.hip
@@ -90,6 +91,9 @@ struct mtts_engine {
   bool ao = false;
   float* ao_part = nullptr;
   int* ao_cnt = nullptr;
+  // q|k|v GEMV + decode attention as one launch (qa.hip); MTTS_QA=1 turns it on (A/B; off: slower)
+  bool qa = false;
+  int* qsync = nullptr;
   // persistent decode launch (mega.hip): MTTS_MEGA=1 turns it on (A/B; off until it wins)
   bool mega = false;
   MegaLayer* mega_L = nullptr;   // device [layers]

@@ -17,7 +17,9 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
   return o;
 }
 
-template <int NB, int RT, int EPI, int PRO, int NW, bool PIPE, class Wait>
+// WT: outputs are stored write-through (sc1) for a consumer inside the same launch (qa.hip),
+// which then needs no release fence from this block, only a drain (cdna_hip_programming.md G16 R1)
+template <int NB, int RT, int EPI, int PRO, int NW, bool PIPE, class Wait, bool WT = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
   // bytes in flight per wave for more resident waves (the default for 17-32 rows)
@@ -208,7 +210,13 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
           const float s = rbf(g / (1.0f + expf(-g)));
           out = f2bf(s * u);
         }
-        if (b < a.B && n < a.N) a.y[(size_t)b * a.ldy + n] = out;
+        if (b < a.B && n < a.N) {
+          if constexpr (WT)
+            __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(a.y + (size_t)b * a.ldy + n), out,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else
+            a.y[(size_t)b * a.ldy + n] = out;
+        }
       }
     }
   }

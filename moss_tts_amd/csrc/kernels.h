@@ -207,6 +207,13 @@ size_t attn_o_ws_floats(int H, int Hkv);
 bool attn_o_supported(int B, int Hq, int Hkv, int D, int H);
 hipError_t attn_o(const AOArgs& a, hipStream_t s);
 
+// qa.hip: the q|k|v GEMV (fused input RMSNorm) and the decode attention as one launch (block
+// attention units prefetch K / V, then wait for the projection); sync = 16 zeroed ints owned
+// by the caller (word 9: a wait timed out).  Partials as attn_decode's publish-only form.
+constexpr int QA_MAXB = 8;
+bool qkv_attn_supported(const GemvArgs& g, const DecAttnArgs& da, int B);
+hipError_t qkv_attn(const GemvArgs& g, const DecAttnArgs& da, int* sync, int B, hipStream_t s);
+
 // mega.hip: the decoder-layer stack of one decode step as one persistent launch
 constexpr int MEGA_MAXB = 2;
 constexpr size_t MEGA_LDS_LIMIT = 160 * 1024;

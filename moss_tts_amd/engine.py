@@ -139,6 +139,10 @@ class Engine:
         """Whether a decode step of `batch` rows runs attention + o_proj as one launch (ao.hip)."""
         return bool(N.load().mtts_attn_o_active(self._h, batch))
 
+    def qkv_attn_active(self, batch: int) -> bool:
+        """Whether a decode step of `batch` rows runs q|k|v + attention as one launch (qa.hip)."""
+        return bool(N.load().mtts_qkv_attn_active(self._h, batch))
+
     def weight_bytes(self):
         v = ctypes.c_uint64()
         N.check(N.load().mtts_engine_weight_bytes(self._h, ctypes.byref(v)), "weight_bytes")

@@ -6,6 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/ao_probe
 mkdir -p $O
 export TMPDIR=/tmp
+export MTTS_AO=1
 for m in ${MODES:-0 1 2 3}; do
   MTTS_AO_PROBE=$m timeout -k 10 200 rocprofv3 --kernel-trace --stats -d /tmp/pp$m -o run --output-format csv -- \
       python3 bench.py --steps 1 --warmup 0 --decode-steps 64 --no-cpu-baseline --no-roofline --no-codec --extra-batches "" > $O/b$m.json 2> $O/e$m.txt
