@@ -181,6 +181,15 @@ int mtts_k_gemv(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y
 int mtts_k_gemv_ex(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                    int ldres, int B, int N, int K, int epi, const float* ss_in, int ld_ss, int n_ss,
                    const uint16_t* norm_w, float eps, float* ss_out, int ld_ss_out, int force_nw, void* stream);
+/* split-K form of the residual GEMV (epi 1) for projections with few 16-row output tiles:
+ * y[B,N] = res + bf16(x . W^T), ss_out per-16-column sums of squares (NULL: skip); B <= 16,
+ * splits >= 2 (mtts_k_gemv_splitk_splits gives the engine's choice, 1 = not worth splitting);
+ * ws_dev: mtts_k_gemv_splitk_ws_bytes bytes, zero-filled before the first call (kept zero). */
+size_t mtts_k_gemv_splitk_ws_bytes(int N, int splits);
+int mtts_k_gemv_splitk_splits(int N, int K, int B);
+int mtts_k_gemv_splitk(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
+                       int ldres, int B, int N, int K, int splits, float* ss_out, int ld_ss_out, void* ws_dev,
+                       void* stream);
 /* prefill form: y[M,N] = epi(x[M,K] . W^T) for any token count M (epi 0 store, 1 residual
  * add + per-16-column sums of squares into ss_out when non-NULL, 2 swiglu) */
 int mtts_k_gemm(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,

@@ -95,6 +95,8 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->ao_part, attn_o_ws_floats(H, Hkv))) || (rc = e->alloc(&e->ao_cnt, (size_t)attn_o_chunks(H))))
     return rc;
   if (hipMemset(e->ao_cnt, 0, attn_o_chunks(H) * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
+  if ((rc = e->alloc(&e->sk_part, SK_PART_FLOATS)) || (rc = e->alloc(&e->sk_cnt, (size_t)SK_TILES))) return rc;
+  if (hipMemset(e->sk_cnt, 0, SK_TILES * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if ((rc = e->alloc(&e->qsync, 16))) return rc;
   if (hipMemset(e->qsync, 0, 16 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   // persistent decode launch: per-layer pointers (the caches move with the capacity) + counters
@@ -157,6 +159,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
   if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
   if (const char* v = getenv("MTTS_QA")) e->qa = v[0] == '1';
+  if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
@@ -448,6 +451,13 @@ static int gemm_min_rows() {  // MTTS_GEMM_MIN_ROWS (A/B): token rows from which
 }
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
   if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill) return gemm_ex(g, epi, s);
+  // residual projections with too few output tiles to fill the chip (MossTTSLocal's depth
+  // down_proj: 96 tiles): split K over workgroups (splitk.hip)
+  if (epi == EPI_RESADD && e->splitk && e->sk_part && g.res && !g.ss_in && !g.attn.part && !g.gate && !g.tile0) {
+    const int tiles = (g.N + 15) / 16, S = gemv_splitk_splits(tiles, g.K / 32, g.B);
+    if (S > 1 && tiles <= SK_TILES && gemv_splitk_ws_floats(tiles, S) <= SK_PART_FLOATS)
+      return gemv_splitk(g, S, e->sk_part, e->sk_cnt, s);
+  }
   return gemv_ex(g, epi, s);
 }
 
@@ -961,6 +971,24 @@ extern "C" int mtts_k_attn_decode(const uint16_t* qkv, const uint16_t* qn_w, con
   HIPCHK(attn_decode(a, B, (hipStream_t)stream));
   return 0;
 }
+
+extern "C" size_t mtts_k_gemv_splitk_ws_bytes(int N, int splits) {
+  const int tiles = (N + 15) / 16;
+  return ((size_t)tiles * sizeof(int) + 255) / 256 * 256 + gemv_splitk_ws_floats(tiles, splits) * sizeof(float);
+}
+extern "C" int mtts_k_gemv_splitk(const uint16_t* w, const uint16_t* x, int ldx, uint16_t* y, int ldy,
+                                  const uint16_t* res, int ldres, int B, int N, int K, int splits, float* ss_out,
+                                  int ld_ss_out, void* ws, void* stream) {
+  if (!ws || !res || K % 32 || B <= 0 || B > 16 || splits < 2) return fail(MTTS_E_INVALID, "bad split-K GEMV args");
+  GemvArgs a = gemv_args(w, x, ldx, y, ldy, B, N, K);
+  a.res = res; a.ldres = ldres; a.ss_out = ss_out; a.ld_ss_out = ld_ss_out;
+  const int tiles = (N + 15) / 16;
+  int* cnt = reinterpret_cast<int*>(ws);
+  float* part = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + ((size_t)tiles * sizeof(int) + 255) / 256 * 256);
+  HIPCHK(gemv_splitk(a, splits, part, cnt, (hipStream_t)stream));
+  return 0;
+}
+extern "C" int mtts_k_gemv_splitk_splits(int N, int K, int B) { return gemv_splitk_splits((N + 15) / 16, K / 32, B); }
 
 extern "C" int mtts_k_gemm(const uint16_t* w, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                            int ldres, int M, int N, int K, int epi, float* ss_out, int ld_ss_out, void* stream) {

@@ -51,7 +51,9 @@ struct Stack {
   int* qsync = nullptr;     // 16 counter words of the q|k|v + attention launch (qa.hip; zero between launches)
 };
 
-constexpr int AO_MAX_CTX = 2048;  // largest KV capacity that decodes through ao.hip
+constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip
+constexpr int SK_TILES = 256;                   // split-K GEMV: most output tiles, and
+constexpr size_t SK_PART_FLOATS = 1024 * 256;   // its partial workspace (tiles x splits x 256)
 
 inline size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
 
@@ -91,6 +93,10 @@ struct mtts_engine {
   bool ao = false;
   float* ao_part = nullptr;
   int* ao_cnt = nullptr;
+  // split-K residual GEMV for few-tile projections (splitk.hip); MTTS_SPLITK=0 turns it off (A/B)
+  bool splitk = true;
+  float* sk_part = nullptr;  // SK_PART_FLOATS
+  int* sk_cnt = nullptr;     // SK_TILES tickets, zero between launches
   // q|k|v GEMV + decode attention as one launch (qa.hip); MTTS_QA=1 turns it on (A/B; off: slower)
   bool qa = false;
   int* qsync = nullptr;

@@ -207,6 +207,12 @@ size_t attn_o_ws_floats(int H, int Hkv);
 bool attn_o_supported(int B, int Hq, int Hkv, int D, int H);
 hipError_t attn_o(const AOArgs& a, hipStream_t s);
 
+// splitk.hip: split-K decode GEMV with the residual epilogue (projections with few 16-row tiles):
+// splits > 1 from gemv_splitk_splits; part: gemv_splitk_ws_floats fp32, cnt: n_tiles zeroed ints
+int gemv_splitk_splits(int n_tiles, int KT, int B);
+size_t gemv_splitk_ws_floats(int n_tiles, int S);
+hipError_t gemv_splitk(const GemvArgs& a, int S, float* part, int* cnt, hipStream_t s);
+
 // qa.hip: the q|k|v GEMV (fused input RMSNorm) and the decode attention as one launch (block
 // attention units prefetch K / V, then wait for the projection); sync = 16 zeroed ints owned
 // by the caller (word 9: a wait timed out).  Partials as attn_decode's publish-only form.

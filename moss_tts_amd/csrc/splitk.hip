@@ -1,0 +1,130 @@
+// Split-K decode GEMV with the residual epilogue, for projections with too few 16-row output
+// tiles to fill the chip: y[B,N] = res + bf16(x[B,K] . W[N,K]^T), plus the per-16-column sums of
+// squares of y (the EPI_RESADD epilogue of gemv_body.h; TF/models/qwen3/modeling_qwen3.py:
+// 311, 322 residual adds after o_proj / down_proj).
+//
+// Why: the one-block-per-tile GEMV runs MossTTSLocal's depth-transformer down projection
+// (N 1,536 = 96 tiles, K 8,960) on 96 of the 256 CUs, each wave walking 3 dependent 8-tile
+// batches -- 15.3 us for 27.5 MB, 1.8 TB/s.  Here workgroup (tile, split) handles K/S of the
+// tile (S chosen so that tiles x S >= the CU count and each wave issues one batch), its NW
+// waves reduce through LDS in a fixed order, and the fp32 tile partial is published
+// (write-through stores, drained, arrival ticket per tile).  The last of the S arrivals sums
+// the S partials in split order (deterministic), adds the residual and writes y and the sums
+// of squares, then resets its ticket for the next launch (graph replay).
+// Layout: the packed weight tiles of gemv.hip ([row tile][k tile], 1 KiB each); x rows from L2.
+#include <algorithm>
+#include <cstdlib>
+
+#include "kernels.h"
+
+namespace mtts {
+
+namespace {
+constexpr int SK_NW = 8;  // waves per workgroup
+constexpr int SK_U = 8;   // k-tiles per load batch
+typedef __attribute__((address_space(1))) float gf32;
+}  // namespace
+
+__global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int S, float* part, int* cnt) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, t = threadIdx.x;
+  const int bt = blockIdx.x / S, si = blockIdx.x - bt * S;
+  const int KT = a.KT;
+  const int KS = (KT + S - 1) / S;
+  const int k0 = si * KS, k1 = min(KT, k0 + KS);
+  const int per = (k1 - k0 + SK_NW - 1) / SK_NW;
+  const int kw0 = k0 + wave * per, kw1 = min(k1, kw0 + per);
+
+  const u32x4* wbase = reinterpret_cast<const u32x4*>(a.w) + ((size_t)bt * KT) * 64 + lane;
+  const int b = lane & 15;
+  const bool xok = b < a.B;
+  const u32x4* xbase = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok ? b : 0) * a.ldx + (lane >> 4) * 8);
+  f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int k = kw0; k < kw1; k += SK_U) {
+    u32x4 wv[SK_U], xv[SK_U];
+    // a batch is always SK_U loads: the surplus re-reads the wave's last tile (zero A operand)
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u) wv[u] = __builtin_nontemporal_load(wbase + (size_t)min(k + u, kw1 - 1) * 64);
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u) xv[u] = xok ? xbase[(size_t)min(k + u, kw1 - 1) * 4] : (u32x4){0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int u = 0; u < SK_U; ++u) {
+      const u32x4 w = k + u < kw1 ? wv[u] : (u32x4){0u, 0u, 0u, 0u};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w), __builtin_bit_cast(bf16x8, xv[u]),
+                                                    acc, 0, 0, 0);
+    }
+  }
+  // ---- fixed-order reduction of the waves' partial tiles; the tile partial goes out sc1 ----
+  __shared__ float red[SK_NW][256];
+  __shared__ float sq[16][17];
+  __shared__ int last_s;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) red[wave][lane * 4 + i] = acc[i];
+  __syncthreads();
+  float* pt = part + (size_t)blockIdx.x * 256;  // [tile][split][256]: element t = (row, b) as the MFMA lays it out
+  if (t < 256) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < SK_NW; ++w) s += red[w][t];
+    __hip_atomic_store((gf32*)(pt + t), s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) last_s = __hip_atomic_fetch_add(cnt + bt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
+  __syncthreads();
+  if (!last_s) return;
+  // ---- the last arrival: sum the S partials in split order, + residual, sums of squares ----
+  if (t < 256) {
+    // element t: lane = t/4, reg = t%4 -> row n = ((lane>>4)*4 + reg), b = lane & 15
+    const int ln = t >> 2, nl = ((ln >> 4) << 2) + (t & 3), bl = ln & 15;
+    const int n = bt * 16 + nl;
+    const float* p0 = part + (size_t)bt * S * 256 + t;
+    float s = 0.f;
+    for (int j = 0; j < S; ++j)
+      s += __hip_atomic_load((gf32*)(p0 + (size_t)j * 256), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    bf16_t out = 0;
+    if (bl < a.B && n < a.N) {
+      // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
+      out = f2bf(bf2f(a.res[(size_t)bl * a.ldres + n]) + rbf(s));
+      a.y[(size_t)bl * a.ldy + n] = out;
+    }
+    const float ho = bf2f(out);
+    sq[bl][nl] = ho * ho;
+  }
+  __syncthreads();
+  if (a.ss_out && t < 16 && t < a.B) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s += sq[t][i];
+    a.ss_out[(size_t)t * a.ld_ss_out + bt] = s;
+  }
+  if (t == 0) cnt[bt] = 0;
+}
+
+int gemv_splitk_splits(int n_tiles, int KT, int B) {
+  // worth it when the tiles alone leave most CUs idle and K is long enough to split
+  if (B > 16 || n_tiles >= 160 || KT < 128) return 1;
+  static const int force = getenv("MTTS_SPLITK_S") ? atoi(getenv("MTTS_SPLITK_S")) : 0;  // A/B sweeps
+  if (force >= 2) return force;
+  // at least one workgroup per CU and one load batch per wave, but a single round of at most
+  // two workgroups per CU (MossTTSLocal down_proj, 96 tiles x K 8,960, frame ms by S:
+  // 1: 11.21, 3: 10.86, 5: 10.45, 6: 11.02, 8: 11.49 -- 576+ workgroups need a second round)
+  int S = std::max((256 + n_tiles - 1) / n_tiles, (KT + SK_NW * SK_U - 1) / (SK_NW * SK_U));
+  while (S > 2 && n_tiles * S > 512) --S;
+  while (S > 1 && KT / S < 4 * SK_NW) --S;  // >= 4 k-tiles per wave
+  return S;
+}
+
+size_t gemv_splitk_ws_floats(int n_tiles, int S) { return (size_t)n_tiles * S * 256; }
+
+hipError_t gemv_splitk(const GemvArgs& a0, int S, float* part, int* cnt, hipStream_t s) {
+  GemvArgs a = a0;
+  if (a.K % 32 || a.B <= 0 || a.B > 16 || a.N <= 0 || S < 2 || !part || !cnt || !a.res || a.ss_in || a.attn.part ||
+      a.tile0 || a.gate)
+    return hipErrorInvalidValue;
+  a.KT = a.K / 32;
+  const int n_tiles = (a.N + 15) / 16;
+  hipLaunchKernelGGL(gemv_splitk_kernel, dim3(n_tiles * S), dim3(SK_NW * 64), 0, s, a, S, part, cnt);
+  return hipGetLastError();
+}
+
+}  // namespace mtts

@@ -189,6 +189,42 @@ def test_gemm_prefill(N, M, Nr, K, epi):
         assert np.allclose(ss.cpu().numpy(), want_ss, rtol=1e-5, atol=1e-6)
 
 
+@pytest.mark.parametrize("B,Nr,K,splits", [(8, 1536, 8960, 0), (1, 1536, 8960, 3), (16, 1000, 4096, 2),
+                                           (3, 64, 2048, 7)])
+def test_gemv_splitk(N, B, Nr, K, splits):
+    """Split-K residual GEMV (csrc/splitk.hip; MossTTSLocal's depth down_proj shape first, at
+    the engine's own split choice) against the oracle linear + residual add, and its per-16-column
+    sums of squares; run twice on the same workspace (tickets reset by the last arrival) with
+    bit-identical results."""
+    S = splits or N.load().mtts_k_gemv_splitk_splits(Nr, K, B)
+    assert S >= 2
+    rng = np.random.default_rng(B + Nr + K)
+    ctx = O._Ctx("bf16")
+    x = rand_bf16(rng, (B, K))
+    W = rand_bf16(rng, (Nr, K), K ** -0.5)
+    packed = torch.zeros(N.load().mtts_k_packed_bytes(Nr, K) // 2, dtype=torch.bfloat16, device="cuda")
+    wd = dev_bf16(W)
+    N.call("mtts_k_pack", P(wd), P(packed), Nr, K, 0, 0, 0, None)
+    xd = dev_bf16(x)
+    res = rand_bf16(rng, (B, Nr))
+    nt = (Nr + 15) // 16
+    ws = torch.zeros(N.load().mtts_k_gemv_splitk_ws_bytes(Nr, S), dtype=torch.uint8, device="cuda")
+    outs = []
+    for _ in range(2):
+        y = dev_bf16(res)
+        ss = torch.zeros(B, nt, dtype=torch.float32, device="cuda")
+        N.call("mtts_k_gemv_splitk", P(packed), P(xd), K, P(y), Nr, P(y), Nr, B, Nr, K, S, P(ss), nt, P(ws), None)
+        torch.cuda.synchronize()
+        outs.append((host(y), ss.cpu().numpy()))
+    got, ssg = outs[0]
+    assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
+    want = ctx.r(res + O.linear(ctx, x, W))
+    rowscale = np.abs(want).max(axis=1, keepdims=True)
+    assert within_band(got, want, 2.0, scale=np.maximum(np.abs(want), rowscale / 4)).all(), np.abs(got - want).max()
+    g2 = np.pad(got, ((0, 0), (0, nt * 16 - Nr))).reshape(B, nt, 16)
+    assert np.allclose(ssg, (g2.astype(np.float64) ** 2).sum(-1), rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("M,H", [(1, 64), (7, 4096), (3, 12288)])
 def test_rmsnorm(N, M, H):
     rng = np.random.default_rng(M + H)
