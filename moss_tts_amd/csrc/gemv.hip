@@ -60,11 +60,11 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
 // ---------------------------------------------------------------------------
 template <int NB, int RT, int EPI, int PRO>
 static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
-  constexpr bool NORM = PRO == PRO_NORM;
+  constexpr bool NORM = PRO == PRO_NORM || PRO == PRO_NORM_PRE;
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
-  const size_t lds = PRO == PRO_NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN ? (size_t)a.B * a.K * 2 : 0);
+  const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN ? (size_t)a.B * a.K * 2 : 0);
   // 17-32 rows (NB = 2): 4 waves of 4-deep batches (in-context B=32 sweep: 5.62 vs 6.03 ms/step)
   int nw = a.force_nw;
   // fused-norm launches stage (B+1)*K*2 bytes of LDS per block: 8 waves keep 2 blocks per CU
@@ -111,7 +111,11 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
     }
   }
   const bool norm = a.ss_in != nullptr;
+  // batch-1 decode (q|k|v, gate|up at K 4096): the norm prologue's inputs load before the first
+  // weight batch (B=1 3.285 -> 3.216 ms/step; MTTS_NO_PRELOAD=1 for A/B)
+  static const bool no_pre = getenv("MTTS_NO_PRELOAD") && atoi(getenv("MTTS_NO_PRELOAD"));
   if (two) norm ? launch_nw<2, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<2, RT, EPI, PRO_NONE>(a, n_tiles, s);
+  else if (norm && !no_pre && norm_preload_fits(a.B, a.K)) launch_nw<1, RT, EPI, PRO_NORM_PRE>(a, n_tiles, s);
   else norm ? launch_nw<1, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<1, RT, EPI, PRO_NONE>(a, n_tiles, s);
 }
 

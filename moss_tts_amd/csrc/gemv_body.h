@@ -19,8 +19,10 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
 
 // WT: outputs are stored write-through (sc1) for a consumer inside the same launch (qa.hip),
 // which then needs no release fence from this block, only a drain (cdna_hip_programming.md G16 R1)
-template <int NB, int RT, int EPI, int PRO, int NW, bool PIPE, class Wait, bool WT = false>
+template <int NB, int RT, int EPI, int PRO0, int NW, bool PIPE, class Wait, bool WT = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
+  constexpr bool PREL = PRO0 == PRO_NORM_PRE;  // norm prologue inputs loaded before the weights
+  constexpr int PRO = PREL ? PRO_NORM : PRO0;
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
   // bytes in flight per wave for more resident waves (the default for 17-32 rows)
   constexpr int U = PIPE ? 4 : 8;
@@ -51,6 +53,44 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     xok[nb] = b < a.B;
     xbase[nb] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
   }
+  // Small norm prologues (B = 1 at K 4096, the batch-1 decode step's q|k|v and gate|up) load
+  // their inputs -- x rows, the norm weight, the sums of squares -- into registers BEFORE the
+  // first weight batch: a wave's vmcnt counts in order, so a prologue load issued after the
+  // weight loads could only be waited for together with them (the whole first batch would have
+  // to land before the prologue could start).
+  // (the host picks PRO_NORM_PRE only when norm_preload_fits: (B+1)*K/8 <= 1024 chunks)
+  constexpr int XPT = PREL ? (1024 + NW * 64 - 1) / (NW * 64) : 1;  // chunks per thread
+  const int K8p = KT * 4;
+  const int n8p = a.B * K8p + K8p;
+  u32x4 xr[XPT], nr[XPT], sr[2];
+  if constexpr (PREL) {
+    {
+      // branch-free buffer loads (out-of-range offsets read zero): a load under a divergent
+      // branch is waited for at once (vmcnt(0)) by the compiler
+      constexpr uint32_t OOB = 0x7ffffff0u;
+      const int nx = a.B * K8p;
+      const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<bf16_t*>(a.x), 0, (int)(((size_t)(a.B - 1) * a.ldx + a.K) * 2), 0x00020000);
+      const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.nw), 0, a.K * 2, 0x00020000);
+      const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+          const_cast<float*>(a.ss_in), 0, (int)(((size_t)(a.B - 1) * a.ld_ss + a.n_ss) * 4), 0x00020000);
+#pragma unroll
+      for (int j = 0; j < XPT; ++j) {
+        const int i = threadIdx.x + j * NW * 64;
+        const int b = i / K8p, c = i - b * K8p;
+        const uint32_t xo = i < nx ? (uint32_t)(b * a.ldx + c * 8) * 2u : OOB;
+        const uint32_t no = (i >= nx && i < n8p) ? (uint32_t)(c * 16) : OOB;
+        xr[j] = __builtin_amdgcn_raw_buffer_load_b128(xrs, xo, 0, 0);
+        nr[j] = __builtin_amdgcn_raw_buffer_load_b128(nrs, no, 0, 0);
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int b = wave + m * NW;
+        const uint32_t so = (b < a.B && lane * 4 < a.n_ss) ? (uint32_t)(b * a.ld_ss + lane * 4) * 4u : OOB;
+        sr[m] = __builtin_amdgcn_raw_buffer_load_b128(srs, so, 0, 0);
+      }
+    }
+  }
   // all weight loads of the first k-batch go out before the (latency-bound) norm prologue
   int kt = kt0;
   u32x4 wa[RT][U];
@@ -65,7 +105,10 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       for (int r = 0; r < RT; ++r)
         wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)min(k + u, kt1 - 1) * 64);
   };
-  if (kt < kt1) issue_w(kt);
+  // unconditional (a wave with an empty K range re-reads its row's last tile, in bounds): a load
+  // issue under a branch makes the compiler wait for the preloads with everything else at the
+  // join (B=4 also 3.56 -> 3.53 ms/step)
+  issue_w(kt);
   wait();  // fused launches: the producer of x (e.g. the attention blocks) has finished
 
   // Prologues (PRO) stage the block's B activation rows in LDS once; the MFMA B fragments
@@ -80,6 +123,20 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   if constexpr (PRO == PRO_NORM) {
     __shared__ float r_s[32];
     const int n8x = a.B * K8;
+    if constexpr (PREL) {
+#pragma unroll
+      for (int j = 0; j < XPT; ++j) {
+        const int i = threadIdx.x + j * NW * 64;
+        if (i < n8x + K8) xs_dyn[i] = xr[j] | nr[j];  // one of the two is zero (out of range)
+      }
+#pragma unroll
+      for (int m = 0; m < 2; ++m) {
+        const int b = wave + m * NW;
+        const float ss = wave_sum((__uint_as_float(sr[m][0]) + __uint_as_float(sr[m][1])) +
+                                  (__uint_as_float(sr[m][2]) + __uint_as_float(sr[m][3])));
+        if (b < a.B && lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+      }
+    } else {
     for (int i = threadIdx.x; i < n8x + K8; i += NW * 64) {
       const int b = i / K8, c = i - b * K8;
       xs_dyn[i] = i < n8x ? reinterpret_cast<const u32x4*>(a.x + (size_t)b * a.ldx)[c]
@@ -94,6 +151,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       }
       ss = wave_sum(ss);
       if (lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+    }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < n8x; i += NW * 64) {

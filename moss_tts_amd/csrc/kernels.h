@@ -9,7 +9,10 @@ constexpr int MAXK = 64;  // largest top-k handled on device
 
 enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 
-enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2 };
+// PRO_NORM_PRE: PRO_NORM whose inputs fit one register load per thread ((B+1)*K <= 8192,
+// K <= 4096), loaded before the first weight batch (gemv_body.h)
+enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2, PRO_NORM_PRE = 3 };
+inline bool norm_preload_fits(int B, int K) { return (size_t)(B + 1) * K <= 8192 && K <= 4096; }
 
 // decode-attention split partials as read by the o_proj prologue (PRO_ATTN)
 struct AttnPartView {
