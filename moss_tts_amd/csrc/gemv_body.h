@@ -22,7 +22,8 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
 template <int NB, int RT, int EPI, int PRO0, int NW, bool PIPE, class Wait, bool WT = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
   constexpr bool PREL = PRO0 == PRO_NORM_PRE;  // norm prologue inputs loaded before the weights
-  constexpr int PRO = PREL ? PRO_NORM : PRO0;
+  constexpr bool PREA = PRO0 == PRO_ATTN_PRE;  // attention partials (2 splits) loaded before the weights
+  constexpr int PRO = PREL ? PRO_NORM : (PREA ? PRO_ATTN : PRO0);
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
   // bytes in flight per wave for more resident waves (the default for 17-32 rows)
   constexpr int U = PIPE ? 4 : 8;
@@ -91,6 +92,36 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       }
     }
   }
+  // PREA: this thread's element of the attention output -- (m, l) of its head and 8 dims of o --
+  // for splits 0 and 1, loaded now (a third and later split, contexts > 512, load after)
+  float4 pa_o[2][2];
+  float2 pa_ml[2];
+  int pa_h = 0, pa_d0 = 0, pa_kvh = 0, pa_hg = 0, pa_b = 0;
+  if constexpr (PREA) {
+    constexpr uint32_t OOB = 0x7ffffff0u;
+    const AttnPartView& v = a.attn;
+    const int G = v.G, D = v.D, PS = G * (D + 2);
+    const int i = threadIdx.x;
+    const int K8a = KT * 4;
+    pa_b = i / K8a;
+    const int k0 = (i - pa_b * K8a) * 8;
+    pa_h = k0 / D; pa_d0 = k0 - pa_h * D; pa_kvh = pa_h / G; pa_hg = pa_h - pa_kvh * G;
+    const bool ok = i < a.B * K8a;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(v.part), 0, (int)((size_t)a.B * v.Hkv * v.ns * PS * 4), 0x00020000);
+    const uint32_t base = (uint32_t)(((pa_b * v.Hkv + pa_kvh) * v.ns) * PS) * 4u;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bool sok = ok && s2 < v.ns;
+      const uint32_t so = base + (uint32_t)(s2 * PS) * 4u;
+      const auto m = __builtin_amdgcn_raw_buffer_load_b64(prs, sok ? so + (uint32_t)(G * D + 2 * pa_hg) * 4u : OOB, 0, 0);
+      const u32x4 o0 = __builtin_amdgcn_raw_buffer_load_b128(prs, sok ? so + (uint32_t)(pa_hg * D + pa_d0) * 4u : OOB, 0, 0);
+      const u32x4 o1 = __builtin_amdgcn_raw_buffer_load_b128(prs, sok ? so + (uint32_t)(pa_hg * D + pa_d0 + 4) * 4u : OOB, 0, 0);
+      pa_ml[s2] = make_float2(__uint_as_float(m[0]), __uint_as_float(m[1]));
+      pa_o[s2][0] = make_float4(__uint_as_float(o0[0]), __uint_as_float(o0[1]), __uint_as_float(o0[2]), __uint_as_float(o0[3]));
+      pa_o[s2][1] = make_float4(__uint_as_float(o1[0]), __uint_as_float(o1[1]), __uint_as_float(o1[2]), __uint_as_float(o1[3]));
+    }
+  }
   // all weight loads of the first k-batch go out before the (latency-bound) norm prologue
   int kt = kt0;
   u32x4 wa[RT][U];
@@ -105,6 +136,8 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       for (int r = 0; r < RT; ++r)
         wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)min(k + u, kt1 - 1) * 64);
   };
+  // the preloads must be ISSUED first: stop the scheduler from hoisting the weight loads above them
+  if constexpr (PREL || PREA) __builtin_amdgcn_sched_barrier(0);
   // unconditional (a wave with an empty K range re-reads its row's last tile, in bounds): a load
   // issue under a branch makes the compiler wait for the preloads with everything else at the
   // join (B=4 also 3.56 -> 3.53 ms/step)
@@ -157,6 +190,38 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     for (int i = threadIdx.x; i < n8x; i += NW * 64) {
       const int b = i / K8;
       xs_dyn[i] = norm8(xs_dyn[i], xs_dyn[n8x + i - b * K8], r_s[b]);
+    }
+    __syncthreads();
+  } else if constexpr (PREA) {
+    const AttnPartView& v = a.attn;
+    const int nact = *v.pos / v.kb + 1;
+    const int G = v.G, D = v.D, PS = G * (D + 2);
+    const int i = threadIdx.x;
+    if (i < a.B * K8) {
+      const float* pp = v.part + ((size_t)pa_b * v.Hkv + pa_kvh) * v.ns * PS;
+      float M = -INFINITY;
+      for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, s2 < 2 ? pa_ml[s2 & 1].x : pp[(size_t)s2 * PS + G * D + 2 * pa_hg]);
+      float L = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int s2 = 0; s2 < nact; ++s2) {
+        float ms, ls;
+        float4 o0, o1;
+        if (s2 < 2) {
+          ms = pa_ml[s2 & 1].x; ls = pa_ml[s2 & 1].y; o0 = pa_o[s2 & 1][0]; o1 = pa_o[s2 & 1][1];
+        } else {
+          const float* q = pp + (size_t)s2 * PS;
+          ms = q[G * D + 2 * pa_hg]; ls = q[G * D + 2 * pa_hg + 1];
+          o0 = *reinterpret_cast<const float4*>(q + pa_hg * D + pa_d0);
+          o1 = *reinterpret_cast<const float4*>(q + pa_hg * D + pa_d0 + 4);
+        }
+        const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
+        L += f * ls;
+        o[0] += f * o0.x; o[1] += f * o0.y; o[2] += f * o0.z; o[3] += f * o0.w;
+        o[4] += f * o1.x; o[5] += f * o1.y; o[6] += f * o1.z; o[7] += f * o1.w;
+      }
+      u32x4 r;
+#pragma unroll
+      for (int q2 = 0; q2 < 4; ++q2) r[q2] = L > 0.f ? pack2(o[2 * q2] / L, o[2 * q2 + 1] / L) : 0u;
+      xs_dyn[i] = r;
     }
     __syncthreads();
   } else if constexpr (PRO == PRO_ATTN) {
