@@ -14,7 +14,8 @@ enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 // PRO_ATTN_PRE: PRO_ATTN with one merged element per thread (B*Hq*D/8 <= threads) whose first
 // two splits' partials load before the first weight batch
 enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2, PRO_NORM_PRE = 3, PRO_ATTN_PRE = 4 };
-inline bool norm_preload_fits(int B, int K) { return (size_t)(B + 1) * K <= 8192 && K <= 4096; }
+// (B <= 8: the sums of squares of row b load in wave b % NW, two rows per wave at NW = 4)
+inline bool norm_preload_fits(int B, int K) { return B <= 8 && (size_t)(B + 1) * K <= 8192 && K <= 4096; }
 
 // decode-attention split partials as read by the o_proj prologue (PRO_ATTN)
 struct AttnPartView {

@@ -113,7 +113,7 @@ def test_gemv_epilogues(N):
 
 
 @pytest.mark.parametrize("B,Nr,K,epi", [(1, 4096, 4096, 0), (4, 6144, 4096, 0), (2, 512, 4096, 2), (5, 96, 1024, 0),
-                                        (3, 4100, 512, 0)])
+                                        (3, 4100, 512, 0), (8, 96, 512, 0), (12, 96, 64, 0), (16, 64, 128, 2)])
 def test_gemv_fused_norm(N, B, Nr, K, epi):
     """Qwen3RMSNorm folded into the GEMV prologue (small decode batches): y = linear(rmsnorm(x)),
     r from per-16-column sums of squares as the residual epilogue writes them."""
