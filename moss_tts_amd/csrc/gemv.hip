@@ -60,7 +60,7 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
 // ---------------------------------------------------------------------------
 template <int NB, int RT, int EPI, int PRO>
 static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
-  constexpr bool NORM = PRO == PRO_NORM || PRO == PRO_NORM_PRE;
+  constexpr bool NORM = PRO == PRO_NORM || PRO == PRO_NORM_PRE || PRO == PRO_NORM_PREROW;
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
@@ -124,6 +124,9 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // weight batch (B=1 3.285 -> 3.216 ms/step; MTTS_NO_PRELOAD=1 for A/B)
   static const bool no_pre = getenv("MTTS_NO_PRELOAD") && atoi(getenv("MTTS_NO_PRELOAD"));
   if (two) norm ? launch_nw<2, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<2, RT, EPI, PRO_NONE>(a, n_tiles, s);
+  else if (norm && !no_pre && a.B <= PREROW_MAXB && a.K == 4096 && (a.force_nw == 0 || a.force_nw == 8) &&
+           norm_lds_bytes(a.B, a.K) <= NORM_LDS_MAX)  // launch_nw gives fused-norm launches 8 waves: K/8 == 512 threads
+    launch_nw<1, RT, EPI, PRO_NORM_PREROW>(a, n_tiles, s);
   else if (norm && !no_pre && norm_preload_fits(a.B, a.K)) launch_nw<1, RT, EPI, PRO_NORM_PRE>(a, n_tiles, s);
   else norm ? launch_nw<1, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<1, RT, EPI, PRO_NONE>(a, n_tiles, s);
 }

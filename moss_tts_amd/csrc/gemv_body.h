@@ -21,7 +21,8 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
 // which then needs no release fence from this block, only a drain (cdna_hip_programming.md G16 R1)
 template <int NB, int RT, int EPI, int PRO0, int NW, bool PIPE, class Wait, bool WT = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
-  constexpr bool PREL = PRO0 == PRO_NORM_PRE;  // norm prologue inputs loaded before the weights
+  constexpr bool PRER = PRO0 == PRO_NORM_PREROW;  // the same, one row per load (K / 8 == threads)
+  constexpr bool PREL = PRO0 == PRO_NORM_PRE || PRER;  // norm prologue inputs loaded before the weights
   constexpr bool PREA = PRO0 == PRO_ATTN_PRE;  // attention partials (2 splits) loaded before the weights
   constexpr int PRO = PREL ? PRO_NORM : (PREA ? PRO_ATTN : PRO0);
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
@@ -60,11 +61,28 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   // weight loads could only be waited for together with them (the whole first batch would have
   // to land before the prologue could start).
   // (the host picks PRO_NORM_PRE only when norm_preload_fits: (B+1)*K/8 <= 1024 chunks)
-  constexpr int XPT = PREL ? (1024 + NW * 64 - 1) / (NW * 64) : 1;  // chunks per thread
+  constexpr int XPT = PRER ? PREROW_MAXB + 1 : (PREL ? (1024 + NW * 64 - 1) / (NW * 64) : 1);  // chunks per thread
   const int K8p = KT * 4;
   const int n8p = a.B * K8p + K8p;
-  u32x4 xr[XPT], nr[XPT], sr[2];
-  if constexpr (PREL) {
+  u32x4 xr[XPT], nr[PRER ? 1 : XPT], sr[2];
+  if constexpr (PRER) {
+    // chunk j of every thread is row j (x rows, then the norm weight): the source is uniform
+    constexpr uint32_t OOB = 0x7ffffff0u;
+#pragma unroll
+    for (int j = 0; j < XPT; ++j) {
+      const bf16_t* src = j < a.B ? a.x + (size_t)j * a.ldx : a.nw;
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(src), 0, a.K * 2, 0x00020000);
+      xr[j] = __builtin_amdgcn_raw_buffer_load_b128(rs, j <= a.B ? (uint32_t)threadIdx.x * 16u : OOB, 0, 0);
+    }
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(a.ss_in), 0, (int)(((size_t)(a.B - 1) * a.ld_ss + a.n_ss) * 4), 0x00020000);
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int b = wave + m * NW;
+      const uint32_t so = (b < a.B && lane * 4 < a.n_ss) ? (uint32_t)(b * a.ld_ss + lane * 4) * 4u : OOB;
+      sr[m] = __builtin_amdgcn_raw_buffer_load_b128(srs, so, 0, 0);
+    }
+  } else if constexpr (PREL) {
     {
       // branch-free buffer loads (out-of-range offsets read zero): a load under a divergent
       // branch is waited for at once (vmcnt(0)) by the compiler
@@ -157,10 +175,16 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     __shared__ float r_s[32];
     const int n8x = a.B * K8;
     if constexpr (PREL) {
+      if constexpr (PRER) {
 #pragma unroll
-      for (int j = 0; j < XPT; ++j) {
-        const int i = threadIdx.x + j * NW * 64;
-        if (i < n8x + K8) xs_dyn[i] = xr[j] | nr[j];  // one of the two is zero (out of range)
+        for (int j = 0; j < XPT; ++j)
+          if (j <= a.B) xs_dyn[j * K8 + threadIdx.x] = xr[j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < XPT; ++j) {
+          const int i = threadIdx.x + j * NW * 64;
+          if (i < n8x + K8) xs_dyn[i] = xr[j] | nr[j];  // one of the two is zero (out of range)
+        }
       }
 #pragma unroll
       for (int m = 0; m < 2; ++m) {
