@@ -96,6 +96,7 @@ static int alloc_capacity(mtts_engine* e) {
     return rc;
   if (hipMemset(e->ao_cnt, 0, attn_o_chunks(H) * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if ((rc = e->alloc(&e->sk_part, SK_PART_FLOATS)) || (rc = e->alloc(&e->sk_cnt, (size_t)SK_TILES))) return rc;
+  if ((rc = e->alloc(&e->gk_ws, GK_WS_FLOATS))) return rc;
   if (hipMemset(e->sk_cnt, 0, SK_TILES * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if ((rc = e->alloc(&e->qsync, 16))) return rc;
   if (hipMemset(e->qsync, 0, 16 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
@@ -450,7 +451,12 @@ static int gemm_min_rows() {  // MTTS_GEMM_MIN_ROWS (A/B): token rows from which
   return v;
 }
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
-  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill) return gemm_ex(g, epi, s);
+  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill) {
+    GemvArgs gg = g;  // short prompts split K over workgroups (gemm.hip)
+    gg.ws = e->gk_ws;
+    gg.ws_floats = e->gk_ws ? GK_WS_FLOATS : 0;
+    return gemm_ex(gg, epi, s);
+  }
   // residual projections with too few output tiles to fill the chip (MossTTSLocal's depth
   // down_proj: 96 tiles): split K over workgroups (splitk.hip)
   if (epi == EPI_RESADD && e->splitk && e->sk_part && g.res && !g.ss_in && !g.attn.part && !g.gate && !g.tile0) {

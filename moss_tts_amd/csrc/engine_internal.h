@@ -54,6 +54,7 @@ struct Stack {
 constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip
 constexpr int SK_TILES = 256;                   // split-K GEMV: most output tiles, and
 constexpr size_t SK_PART_FLOATS = 1024 * 256;   // its partial workspace (tiles x splits x 256)
+constexpr size_t GK_WS_FLOATS = 8u << 20;       // prefill GEMM split-K partials (32 MB)
 
 inline size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }
 
@@ -95,6 +96,7 @@ struct mtts_engine {
   int* ao_cnt = nullptr;
   // split-K residual GEMV for few-tile projections (splitk.hip); MTTS_SPLITK=0 turns it off (A/B)
   bool splitk = true;
+  float* gk_ws = nullptr;    // prefill GEMM split-K partials (GK_WS_FLOATS; gemm.hip)
   float* sk_part = nullptr;  // SK_PART_FLOATS
   int* sk_cnt = nullptr;     // SK_TILES tickets, zero between launches
   // q|k|v GEMV + decode attention as one launch (qa.hip); MTTS_QA=1 turns it on (A/B; off: slower)

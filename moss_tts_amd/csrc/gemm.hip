@@ -129,7 +129,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemvArgs a) {
 // 16-byte fragment a wave loads feeds WN (weights) or WR (activations) MFMAs.  The two
 // waves that share a weight (or token) stripe read it through the CU's L1.  SwiGLU takes
 // WR/2 gate|up tile pairs per wave.
-template <int WR, int WN, int EPI, int U>
+template <int WR, int WN, int EPI, int U, bool SPLIT = false>
 __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
   // U: k-tiles in flight per wave (the k loop is latency-bound for short prompts)
   const int lane = threadIdx.x & 63;
@@ -159,7 +159,14 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
     xok[j] = m < a.B;
     xbase[j] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[j] ? m : 0) * a.ldx + g4 * 8);
   }
-  for (int kt = 0; kt < KT; kt += U) {  // KT % U == 0 (checked by the launcher)
+  // SPLIT: blockIdx.z takes k-tiles [z*KS, (z+1)*KS) and writes its fp32 partial tile
+  int kbeg = 0, kend = KT;
+  if constexpr (SPLIT) {
+    const int KS = KT / gridDim.z;  // KT % (U * S) == 0 (checked by the launcher)
+    kbeg = blockIdx.z * KS;
+    kend = kbeg + KS;
+  }
+  for (int kt = kbeg; kt < kend; kt += U) {  // KT % U == 0 (checked by the launcher)
     u32x4 wa[WR][U], xb[WN][U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -176,6 +183,22 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
         for (int j = 0; j < WN; ++j)
           acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[r][u]),
                                                              __builtin_bit_cast(bf16x8, xb[j][u]), acc[r][j], 0, 0, 0);
+  }
+  if constexpr (SPLIT) {
+    // partial [z][token][packed row] (fp32): lane -> token (tt0+j)*16 + c16, rows +g4*4 .. +3
+    const size_t ld = (size_t)n_rt * 16;
+    float* wsz = a.ws + (size_t)blockIdx.z * a.B * ld;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      if (rt0 + r >= n_rt) continue;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int m = (tt0 + j) * 16 + c16;
+        if (m < a.B)
+          *reinterpret_cast<f32x4*>(wsz + (size_t)m * ld + (rt0 + r) * 16 + g4 * 4) = acc[r][j];
+      }
+    }
+    return;
   }
   constexpr int OT = EPI == EPI_SWIGLU ? WR / 2 : WR;  // output column tiles per wave
 #pragma unroll
@@ -236,11 +259,84 @@ static void gemm_launch(const GemvArgs& a, int n_tiles, hipStream_t s) {
   }
 }
 
+// Split-K reduce + epilogue: thread (token m, 16-column output tile) sums the S partials in
+// split order (deterministic) and applies the same epilogue as gemm2_kernel (bf16 rounding
+// points of TF/models/qwen3/modeling_qwen3.py:81-83, 311, 322).
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
+  const int n_ot = (a.N + 15) / 16;
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  if (id >= a.B * n_ot) return;
+  const int m = id / n_ot, ot = id - m * n_ot;
+  const size_t ld = (size_t)a.n_row_tiles * 16;
+  const float* p = a.ws + (size_t)m * ld;
+  const size_t zs = (size_t)a.B * ld;
+  float o[16];
+  float ssq = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    f32x4 g = (f32x4){0.f, 0.f, 0.f, 0.f}, u = (f32x4){0.f, 0.f, 0.f, 0.f};
+    const int c = (EPI == EPI_SWIGLU ? 2 * ot : ot) * 16 + q * 4;
+    for (int z = 0; z < S; ++z) {
+      g += *reinterpret_cast<const f32x4*>(p + z * zs + c);
+      if constexpr (EPI == EPI_SWIGLU) u += *reinterpret_cast<const f32x4*>(p + z * zs + c + 16);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int n = ot * 16 + q * 4 + i;
+      float v;
+      if constexpr (EPI == EPI_STORE) {
+        v = rbf(g[i]);
+      } else if constexpr (EPI == EPI_RESADD) {
+        v = n < a.N ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(g[i])) : 0.f;
+      } else {
+        const float gg = rbf(g[i]), uu = rbf(u[i]);
+        v = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
+      }
+      o[q * 4 + i] = v;
+    }
+  }
+  bf16_t* yr = a.y + (size_t)m * a.ldy + ot * 16;
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (ot * 16 + i < a.N) yr[i] = f2bf(o[i]);
+  if constexpr (EPI == EPI_RESADD) {
+    // per 4-column groups as the GEMM epilogue adds them (then across the 4 groups)
+    float s4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      s4[q] = (o[4 * q] * o[4 * q] + o[4 * q + 1] * o[4 * q + 1]) + (o[4 * q + 2] * o[4 * q + 2] + o[4 * q + 3] * o[4 * q + 3]);
+    ssq = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    if (a.ss_out) a.ss_out[(size_t)m * a.ld_ss_out + ot] = ssq;
+  }
+}
+
+// split count for a short prompt: the GEMM's per-workgroup latency is ~constant in N, so
+// split K until the grid covers the CUs (cdna_hip_programming.md "Projection GEMM at M = 256"),
+// keeping >= 16 k-tiles per split and the partials inside the workspace
+template <int WR, int WN, int U>
+static int gemm_splits(const GemvArgs& a, int nx, int ny) {
+  static const int force = getenv("MTTS_GEMM_SPLITK") ? atoi(getenv("MTTS_GEMM_SPLITK")) : -1;
+  if (!a.ws || force == 0) return 1;
+  int S = force > 0 ? force : 1;
+  if (force < 0)
+    while (nx * ny * S < 256 && a.KT / (2 * S) >= 16) S *= 2;
+  while (S > 1 && (a.KT % (U * S) || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
+  return S;
+}
+
 template <int WR, int WN, int EPI>
 static void gemm2_launch(GemvArgs a, hipStream_t s) {
   a.n_row_tiles = (EPI == EPI_SWIGLU ? 2 : 1) * ((a.N + 15) / 16);
   const int mt = (a.B + 15) / 16;
   const dim3 grid((a.n_row_tiles + 2 * WR - 1) / (2 * WR), (mt + 2 * WN - 1) / (2 * WN));
+  const int S = gemm_splits<WR, WN, 4>(a, (int)grid.x, (int)grid.y);
+  if (S > 1) {
+    hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4, true>), dim3(grid.x, grid.y, S), dim3(256), 0, s, a);
+    const int n = a.B * ((a.N + 15) / 16);
+    hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
+    return;
+  }
   static const int u = getenv("MTTS_GEMM_U") ? atoi(getenv("MTTS_GEMM_U")) : 4;
   if (u == 8 && a.KT % 8 == 0) hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 8>), grid, dim3(256), 0, s, a);
   else if (u >= 4 && a.KT % 4 == 0) hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4>), grid, dim3(256), 0, s, a);

@@ -54,6 +54,8 @@ struct GemvArgs {
   const int* gate;     // device flag: the launch does nothing when *gate == 0 (nullptr: always on)
   int n_row_tiles;     // packed 16-row weight tiles (set by the GEMM launcher)
   AttnPartView attn;   // PRO_ATTN (o_proj): x is merged from these partials; attn.part == nullptr: off
+  float* ws;           // prefill GEMM split-K workspace (gemm_ex; nullptr: no split)
+  size_t ws_floats;
 };
 
 inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {

@@ -13,6 +13,8 @@ from moss_tts_amd import _native as N  # noqa: E402
 from moss_tts_amd.engine import Engine, EngineConfig, sampling_params  # noqa: E402
 
 shapes = [(1, 181), (1, 512), (4, 181), (32, 181), (1, 2048)]
+if os.environ.get("PREFILL_SHAPES"):  # e.g. "1x181,4x181"
+    shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["PREFILL_SHAPES"].split(",")]
 e = Engine(EngineConfig(max_batch=32, max_ctx=2304, max_prefill_tokens=8192), 0)
 e.init_random(0)
 sp = sampling_params(text_temperature=0, audio_temperature=0)
