@@ -39,7 +39,8 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
   constexpr int KW = DEC_KW, KB = KW * NWV;
   constexpr int QS = (D + 31) / 32;  // 32-dim MFMA steps of q.k
   constexpr int DT = (D + 15) / 16;  // 16-dim output tiles of p.v
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform (scalar resources)
   const int g4 = lane >> 4, c16 = lane & 15;
   const int pos = *a.pos;
   const int nact = pos / KB + 1;
@@ -68,6 +69,14 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
   u32x4 kt[2][QS];
   u32x4 vt[DT];
   uint32_t mk[2];
+  // Branch-free buffer loads: an out-of-range offset reads zero.  A per-lane "load or zero"
+  // select makes hipcc branch around each load and wait for it (cdna_hip_programming.md, GEMM
+  // trap (c)), so the K / V^T / mask loads would each cost a round trip.
+  constexpr uint32_t OOBA = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(kcache, 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(vcache, 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mrow), 0, Cmax, 0x00020000);
   auto load_keys = [&](int k0) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -75,23 +84,24 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
 #pragma unroll
       for (int st = 0; st < QS; ++st) {
         const int d0 = st * 32 + 8 * g4;
-        kt[t][st] = (key < pos && d0 < D) ? *reinterpret_cast<const u32x4*>(kcache + (size_t)key * D + d0)
-                                          : (u32x4){0u, 0u, 0u, 0u};
+        kt[t][st] = __builtin_amdgcn_raw_buffer_load_b128(
+            krs, (key < pos && d0 < D) ? (uint32_t)(key * D + d0) * 2u : OOBA, 0, 0);
       }
       // 16-key tiles that start at or before pos lie inside the row (Cmax % 64 == 0)
-      mk[t] = (k0 + t * 16 <= pos) ? *reinterpret_cast<const uint32_t*>(mrow + k0 + t * 16 + g4 * 4) : 0u;
+      mk[t] = __builtin_amdgcn_raw_buffer_load_b32(
+          mrs, (k0 + t * 16 <= pos) ? (uint32_t)(k0 + t * 16 + g4 * 4) : OOBA, 0, 0);
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int dim = dt * 16 + c16;
       const int kb = k0 + 8 * g4;  // lane's keys kb .. kb+7
-      vt[dt] = (dim < D && kb < pos) ? *reinterpret_cast<const u32x4*>(vcache + (size_t)dim * Cmax + kb)
-                                     : (u32x4){0u, 0u, 0u, 0u};
+      vt[dt] = __builtin_amdgcn_raw_buffer_load_b128(
+          vrs, (dim < D && kb < pos) ? (uint32_t)(dim * Cmax + kb) * 2u : OOBA, 0, 0);
     }
   };
   const int kbeg = sp * KB + wave * KW;
   if constexpr (PF) {
-    if (kbeg <= pos) load_keys(kbeg);
+    load_keys(kbeg);  // waves past the new token: every offset out of range, no traffic
     wait();
   }
 
@@ -100,25 +110,33 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
   constexpr int JOBS = (G + 2 + NWV - 1) / NWV;
   const int njobs = G + (owner ? 2 : 0);
   uint32_t pr[JOBS], pw[JOBS], pc[JOBS], ps[JOBS];
+  {
+    // same branch-free form: unused jobs / lanes / tables read zero
+    const __amdgpu_buffer_rsrc_t rrs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(row), 0, heads * D * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t qws =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.qn_w), 0, D * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t kws =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.kn_w), 0, D * 2, 0x00020000);
+    const bool rope = a.cos_t != nullptr;
+    const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(rope ? a.cos_t + (size_t)pos * D : row), 0, D * 2, 0x00020000);
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(rope ? a.sin_t + (size_t)pos * D : row), 0, D * 2, 0x00020000);
 #pragma unroll
-  for (int jj = 0; jj < JOBS; ++jj) {
-    const int j = wave + jj * NWV;
-    pr[jj] = pw[jj] = pc[jj] = ps[jj] = 0;
-    if (j < njobs && 2 * lane < D) {
+    for (int jj = 0; jj < JOBS; ++jj) {
+      const int j = wave + jj * NWV;
+      const bool on = j < njobs && 2 * lane < D;
       const int hd = j < G ? kvh * G + j : (j == G ? a.Hq + kvh : a.Hq + a.Hkv + kvh);
-      pr[jj] = *reinterpret_cast<const uint32_t*>(row + (size_t)hd * D + 2 * lane);
-      if (j <= G) {
-        pw[jj] = *reinterpret_cast<const uint32_t*>((j < G ? a.qn_w : a.kn_w) + 2 * lane);
-        if (a.cos_t) {
-          pc[jj] = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
-          ps[jj] = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
-        }
-      }
+      const uint32_t lo = 4u * lane;  // byte offset of the lane's two dims
+      pr[jj] = __builtin_amdgcn_raw_buffer_load_b32(rrs, on ? (uint32_t)hd * D * 2u + lo : OOBA, 0, 0);
+      const bool nw = on && j <= G;
+      pw[jj] = __builtin_amdgcn_raw_buffer_load_b32(j < G ? qws : kws, nw ? lo : OOBA, 0, 0);
+      pc[jj] = __builtin_amdgcn_raw_buffer_load_b32(crs, nw && rope ? lo : OOBA, 0, 0);
+      ps[jj] = __builtin_amdgcn_raw_buffer_load_b32(srs, nw && rope ? lo : OOBA, 0, 0);
     }
   }
-  if constexpr (!PF) {
-    if (kbeg <= pos) load_keys(kbeg);
-  }
+  if constexpr (!PF) load_keys(kbeg);  // waves past the new token: every offset out of range
 
   // ---- prologue math ----
 #pragma unroll

@@ -278,8 +278,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   }
   // (k < kt1 and the row clamp keep every LDS address inside the staged rows)
   auto load_x = [&](int k, int nb) -> u32x4 {
-    if (!xok[nb]) return (u32x4){0u, 0u, 0u, 0u};
-    if constexpr (PRO != PRO_NONE) return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
+    if constexpr (PRO != PRO_NONE) {
+      if (!xok[nb]) return (u32x4){0u, 0u, 0u, 0u};
+      return xs_dyn[((lane & 15) + 16 * nb) * K8 + k * 4 + (lane >> 4)];
+    }
+    // unconditional global load: a "load or zero" select would branch and wait on every load
+    // (cdna_hip_programming.md trap (c)); token columns >= B read row 0 and are never stored
     return xbase[nb][k * 4];
   };
 

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int
 #pragma unroll
     for (int u = 0; u < SK_U; ++u) wv[u] = __builtin_nontemporal_load(wbase + (size_t)min(k + u, kw1 - 1) * 64);
 #pragma unroll
-    for (int u = 0; u < SK_U; ++u) xv[u] = xok ? xbase[(size_t)min(k + u, kw1 - 1) * 4] : (u32x4){0u, 0u, 0u, 0u};
+    for (int u = 0; u < SK_U; ++u) xv[u] = xbase[(size_t)min(k + u, kw1 - 1) * 4];
 #pragma unroll
     for (int u = 0; u < SK_U; ++u) {
       const u32x4 w = k + u < kw1 ? wv[u] : (u32x4){0u, 0u, 0u, 0u};
