@@ -30,3 +30,9 @@ print(f"step {step}: span {span:.1f} us, kernels {b - a}")
 for n in sorted(tot_dur, key=lambda k: -tot_dur[k]):
     print(f"  {n:70s} n={cnt[n]:3d} dur/call {tot_dur[n] / cnt[n]:7.2f}  gap/call {tot_gap[n] / cnt[n]:6.2f}")
 print(f"  total dur {sum(tot_dur.values()):.1f}  total gap {sum(tot_gap.values()):.1f}")
+# in-order listing of the step's first kernels (one layer and the lead-in): KTRACE_SEQ=N
+import os
+nseq = int(os.environ.get("KTRACE_SEQ", "0"))
+for r in rows[a:a + nseq]:
+    print(f"    {short(r['Kernel_Name']):48s} g{r['Grid_Size_X']}x{r['Grid_Size_Y']}x{r['Grid_Size_Z']}"
+          f"  {(int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1000:7.2f} us")
