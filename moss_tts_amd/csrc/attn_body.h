@@ -319,7 +319,7 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       o += f * acc_s[w][h][d];
     }
     if (single) {
-      bf16_t* op = a.out + (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e;
+      bf16_t* op = a.out + (a.out_packed ? xpk_index(b, kvh * G * D + e) : (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e);
       if constexpr (SC1) {
         typedef __attribute__((address_space(1))) uint16_t g16;
         __hip_atomic_store((g16*)op, f2bf(L > 0.f ? o / L : 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -383,7 +383,7 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       L += f * mlp[(s2 * G + h) * 2 + 1];
       o += f * p0[(size_t)s2 * PS + e];
     }
-    bf16_t* op = a.out + (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e;
+    bf16_t* op = a.out + (a.out_packed ? xpk_index(b, kvh * G * D + e) : (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e);
     if constexpr (SC1) {
       typedef __attribute__((address_space(1))) uint16_t g16;
       __hip_atomic_store((g16*)op, f2bf(L > 0.f ? o / L : 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -160,6 +160,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
   if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
   if (const char* v = getenv("MTTS_QA")) e->qa = v[0] == '1';
+  if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
   auto bail = [&](int rc) {
@@ -412,15 +413,15 @@ extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
 // into the GEMV prologue (normalised rows staged in LDS per block, no extra launch); larger
 // ones run the single-pass rmsnorm_ss kernel into e->xn first.  Both read the residual
 // stream's per-16-column sums of squares e->ss.
-int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s) {
+int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s, bool packed) {
   const int H = st.H, NT = H / 16;
   if (norm_lds_bytes(M, H) <= NORM_LDS_MAX && !e->unfused_norm) {
     g.x = st.h; g.ldx = H;
     g.ss_in = st.ss; g.ld_ss = NT; g.n_ss = NT; g.nw = nw; g.eps = e->c.rms_eps;
     return 0;
   }
-  HIPCHK(rmsnorm_ss(st.h, 0, H, st.ss, 0, NT, nw, st.xn, M, H, e->c.rms_eps, s));
-  g.x = st.xn; g.ldx = H;
+  HIPCHK(rmsnorm_ss(st.h, 0, H, st.ss, 0, NT, nw, st.xn, M, H, e->c.rms_eps, s, packed));
+  g.x = st.xn; g.ldx = H; g.x_packed = packed ? 1 : 0;
   return 0;
 }
 
@@ -432,6 +433,7 @@ Stack backbone_stack(mtts_engine* e) {
   st.kc = e->kc; st.vc = e->vc; st.layer_kv = e->layer_kv; st.Cmax = c.max_ctx;
   st.cos_t = e->cos_t; st.sin_t = e->sin_t; st.mask = e->mask;
   st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
+  st.rows = e->Mmax;
   st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt; st.fsync = e->fsync;
   st.ao_part = e->ao_part; st.ao_cnt = e->ao_cnt; st.qsync = e->qsync;
   return st;
@@ -451,7 +453,7 @@ static int gemm_min_rows() {  // MTTS_GEMM_MIN_ROWS (A/B): token rows from which
   return v;
 }
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
-  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill) {
+  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill && !g.x_packed && !g.y_packed) {
     GemvArgs gg = g;  // short prompts split K over workgroups (gemm.hip)
     gg.ws = e->gk_ws;
     gg.ws_floats = e->gk_ws ? GK_WS_FLOATS : 0;
@@ -459,7 +461,8 @@ hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
   }
   // residual projections with too few output tiles to fill the chip (MossTTSLocal's depth
   // down_proj: 96 tiles): split K over workgroups (splitk.hip)
-  if (epi == EPI_RESADD && e->splitk && e->sk_part && g.res && !g.ss_in && !g.attn.part && !g.gate && !g.tile0) {
+  if (epi == EPI_RESADD && e->splitk && e->sk_part && g.res && !g.ss_in && !g.attn.part && !g.gate && !g.tile0 &&
+      !g.x_packed) {
     const int tiles = (g.N + 15) / 16, S = gemv_splitk_splits(tiles, g.K / 32, g.B);
     if (S > 1 && tiles <= SK_TILES && gemv_splitk_ws_floats(tiles, S) <= SK_PART_FLOATS)
       return gemv_splitk(g, S, e->sk_part, e->sk_cnt, s);
@@ -493,12 +496,16 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   // their KV head from L2 once per o_proj row chunk, so long contexts keep the split form
   const bool use_ao = S == 1 && e->ao && st.ao_part && st.cos_t && st.Cmax <= AO_MAX_CTX &&
                       attn_o_supported(B, Hq, Hkv, D, H);
+  // 17-32 row decode: the GEMV inputs (xn, the attention output, the SwiGLU output) travel in
+  // the fragment-packed layout, so each x fragment is one 1 KiB load (B=32 per layer: x loads
+  // cost ~22 of 129 us row-major)
+  const bool xpk = S == 1 && M > 16 && M <= 32 && st.rows >= 32 && e->xpack && !use_ao && !e->fused_ao;
   for (int l = 0; l < st.layers; ++l) {
     const LayerW& w = st.L[l];
     bf16_t* kc = st.kc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     bf16_t* vc = st.vc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     GemvArgs g = gemv_args(w.qkv, st.xn, H, st.qkvb, st.qkv_rows, M, st.qkv_rows, H);
-    if (int rc = normed_input(e, st, g, w.in_norm, M, s)) return rc;
+    if (int rc = normed_input(e, st, g, w.in_norm, M, s, xpk)) return rc;
     g.force_nw = e->nw[0];
     DecAttnArgs da{};
     da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
@@ -506,6 +513,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     da.part = st.part; da.cnt = st.att_cnt;
     // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
     da.publish_only = fuse_attn ? 1 : 0;
+    da.out_packed = xpk ? 1 : 0;
     da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
     // decode, small batch: q|k|v projection + attention in one launch (qa.hip)
     const bool use_qa = S == 1 && fuse_attn && e->qa && st.qsync && !use_ao && !e->fused_ao && B <= QA_MAXB &&
@@ -553,6 +561,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     if (!(S == 1 && fused_ao) && !use_ao) {
       g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
       g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
+      g.x_packed = xpk ? 1 : 0;
       if (fuse_attn) {
         g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
         g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
@@ -560,11 +569,13 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       HIPCHK(proj(e, g, EPI_RESADD, s));
     }
     g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
-    if (int rc = normed_input(e, st, g, w.post_norm, M, s)) return rc;
+    if (int rc = normed_input(e, st, g, w.post_norm, M, s, xpk)) return rc;
     g.force_nw = e->nw[2];
+    g.y_packed = xpk ? 1 : 0;
     HIPCHK(proj(e, g, EPI_SWIGLU, s));
     g = gemv_args(w.down, st.act, I, st.h, H, M, H, I);
     g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
+    g.x_packed = xpk ? 1 : 0;
     HIPCHK(proj(e, g, EPI_RESADD, s));
   }
   return 0;

@@ -49,6 +49,7 @@ struct Stack {
   float* ao_part = nullptr; // attention + o_proj launch (ao.hip): split-K partials and row-chunk tickets
   int* ao_cnt = nullptr;
   int* qsync = nullptr;     // 16 counter words of the q|k|v + attention launch (qa.hip; zero between launches)
+  int rows = 0;             // row capacity of xn / attnb / act (>= 32: 17-32 row decode may use the packed layout)
 };
 
 constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip
@@ -101,6 +102,8 @@ struct mtts_engine {
   int* sk_cnt = nullptr;     // SK_TILES tickets, zero between launches
   // q|k|v GEMV + decode attention as one launch (qa.hip); MTTS_QA=1 turns it on (A/B; off: slower)
   bool qa = false;
+  // 17-32 row decode: xn / attnb / act in the fragment-packed layout (xpk_index; MTTS_XPACK=0: row-major)
+  bool xpack = true;
   int* qsync = nullptr;
   // persistent decode launch (mega.hip): MTTS_MEGA=1 turns it on (A/B; off until it wins)
   bool mega = false;
@@ -160,7 +163,8 @@ bool layer_target(const LayerW& w, const std::string& rest, int H, int I, int Hq
 int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void* src, size_t bytes, int on_dev);
 int ensure_staging(mtts_engine* e, size_t bytes);
 bool parse_layer(const char* name, int* layer, std::string* rest);
-int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s);
+int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s,
+                 bool packed = false);
 Stack backbone_stack(mtts_engine* e);
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s);
 int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int* pos_base, int CH, int n_split,

@@ -133,6 +133,9 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
 
 hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   if (a0.K % 32 != 0 || a0.B <= 0 || a0.N <= 0) return hipErrorInvalidValue;
+  // the packed layout holds 32 token slots and is read by the 2-half (NB = 2) body only
+  if ((a0.x_packed || a0.y_packed) && (a0.B <= 16 || a0.B > 32)) return hipErrorInvalidValue;
+  if (a0.x_packed && (a0.ss_in || a0.attn.part)) return hipErrorInvalidValue;
   if (a0.ss_in && (a0.n_ss % 4 || a0.ld_ss % 4 || a0.ldx % 8 || norm_lds_bytes(std::min(a0.B, 32), a0.K) > NORM_LDS_MAX))
     return hipErrorInvalidValue;
   if (a0.attn.part && (epi != EPI_RESADD || a0.B > 16 || (size_t)a0.B * a0.K * 2 > NORM_LDS_MAX || a0.attn.D % 8 ||

@@ -47,13 +47,16 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   for (int r = 0; r < RT; ++r)
     wbase[r] = reinterpret_cast<const u32x4*>(a.w) + ((size_t)(bt * RT + r) * KT) * 64 + lane;
   // B operand: x rows (b = lane&15 + 16 nb), 8 consecutive k at 8*(lane>>4)
+  // (x_packed, 17-32 rows: fragment-packed x, xpk_index -- k tile kt of half nb is 1 KiB at (2 kt + nb) KiB)
   const u32x4* xbase[NB];
   bool xok[NB];
+  const int xs = a.x_packed ? 128 : 4;  // u32x4 stride per k tile
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int b = (lane & 15) + 16 * nb;
     xok[nb] = b < a.B;
-    xbase[nb] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
+    xbase[nb] = a.x_packed ? reinterpret_cast<const u32x4*>(a.x) + nb * 64 + lane
+                           : reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
   }
   // Small norm prologues (B = 1 at K 4096, the batch-1 decode step's q|k|v and gate|up) load
   // their inputs -- x rows, the norm weight, the sums of squares -- into registers BEFORE the
@@ -284,7 +287,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     }
     // unconditional global load: a "load or zero" select would branch and wait on every load
     // (cdna_hip_programming.md trap (c)); token columns >= B read row 0 and are never stored
-    return xbase[nb][k * 4];
+    return xbase[nb][k * xs];
   };
 
   auto compute = [&](u32x4 (&w)[RT][U], int k) {
@@ -362,7 +365,9 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
           out = f2bf(s * u);
         }
         if (b < a.B && n < a.N) {
-          if constexpr (WT)
+          if (a.y_packed)
+            a.y[xpk_index(b, n)] = out;
+          else if constexpr (WT)
             __hip_atomic_store((__attribute__((address_space(1))) uint16_t*)(a.y + (size_t)b * a.ldy + n), out,
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else

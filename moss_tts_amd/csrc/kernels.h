@@ -56,7 +56,18 @@ struct GemvArgs {
   AttnPartView attn;   // PRO_ATTN (o_proj): x is merged from these partials; attn.part == nullptr: off
   float* ws;           // prefill GEMM split-K workspace (gemm_ex; nullptr: no split)
   size_t ws_floats;
+  // 17-32 row decode (NB = 2): x / y in the fragment-packed layout (xpk_index) instead of [B, ld]
+  int x_packed, y_packed;
 };
+
+// Fragment-packed activations of the 17-32 row decode GEMVs: the MFMA B-operand order of
+// v_mfma_f32_16x16x32_bf16 for 32 token slots -- [k tile][token half][lane][8 k] -- so a
+// wave's x fragment of one k tile is ONE contiguous 1 KiB load (row-major x puts the 16
+// tokens of a fragment 16 rows apart: 16 half-used cache lines per load).  u16 index of
+// (token b < 32, column k); the buffer holds 32 * K elements.
+__host__ __device__ inline size_t xpk_index(int b, int k) {
+  return ((((size_t)(k >> 5) * 2 + (b >> 4)) * 64 + (b & 15) + 16 * ((k & 31) >> 3)) << 3) + (k & 7);
+}
 
 inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {
   GemvArgs a{};
@@ -115,6 +126,7 @@ struct DecAttnArgs {
   float eps, scale;
   int publish_only;     // 1: every block writes its (m, l, o) partial; the o_proj GEMV merges them
   int probe;            // timing probe (MTTS_ATTN_PROBE): 0 full; 1 exit after pos; 2 after loads + prologue; 3 no combine
+  int out_packed;       // out in the fragment-packed layout (xpk_index; self-combining form, B <= 32)
 };
 
 struct GenDev {
@@ -175,7 +187,7 @@ hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t
 hipError_t rmsnorm(const bf16_t* x, size_t x_off, size_t x_stride, const bf16_t* w, bf16_t* y, int M, int H, float eps,
                    hipStream_t s);
 hipError_t rmsnorm_ss(const bf16_t* x, size_t x_off, size_t x_stride, const float* ss, size_t ss_off, size_t ss_stride,
-                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s);
+                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s, bool y_packed = false);
 hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s);
 // attention.hip
 size_t attn_smem_bytes(int G, int D, int CH);

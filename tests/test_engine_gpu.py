@@ -192,3 +192,64 @@ def test_text_head_gating_is_exact(gpu, golden):
                                         sampling_params(text_temperature=0, audio_temperature=0)).cpu().numpy())
             eng.close()
         assert res[0].shape == res[1].shape and (res[0] == res[1]).all(), name
+
+
+@pytest.mark.parametrize("unfused_norm", ["0", "1"])
+def test_packed_activations_17_32_rows(gpu, golden, unfused_norm):
+    """17-32 row decode keeps the GEMV inputs (normed x, attention output, SwiGLU output) in
+    the fragment-packed layout (kernels.h xpk_index).  Teacher-forced over a golden case tiled
+    to 24 rows: every decode step's logits are bit-identical to the row-major layout
+    (MTTS_XPACK=0) and within the bf16 band of the oracle.  MTTS_UNFUSED_NORM=1 routes the
+    RMSNorms through the standalone kernel, which then writes the packed layout itself."""
+    import os
+    name = "g_nvq4_bf16"
+    g, c, cfg, W = case(golden, name)
+    ids, mask = g[name + "/input_ids"], g[name + "/mask"]
+    tr = O.StepTrace()
+    ref = O.generate(W, cfg, ids, mask, max_new_tokens=6, text_temperature=0, audio_temperature=0,
+                     dtype="bf16", trace=tr)
+    B0, T, C = ids.shape
+    starts = O.find_last_equal_C(ids[..., 0], cfg.im_start_token_id) + 3
+    gen = np.stack([np.concatenate([ids[b, :starts[b]], ref[b][1]], 0) for b in range(B0)])
+    full_mask = np.concatenate([mask, np.ones((B0, gen.shape[1] - T), bool)], 1)
+    for s in range(gen.shape[1] - T):
+        stopped = (gen[:, T:T + s + 1, 0] == cfg.im_end_token_id).any(axis=1)
+        full_mask[:, T + s] = ~stopped
+    rep = (24 + B0 - 1) // B0
+    genr, maskr = np.tile(gen, (rep, 1, 1)), np.tile(full_mask, (rep, 1))
+    B = genr.shape[0]
+    assert 16 < B <= 32
+    n_steps = min(len(tr.audio_logits), 5)
+    runs = []
+    for flag in ("1", "0"):
+        os.environ["MTTS_XPACK"] = flag
+        os.environ["MTTS_UNFUSED_NORM"] = unfused_norm
+        try:
+            eng = make_engine(cfg, W, max_batch=B)
+        finally:
+            os.environ.pop("MTTS_XPACK")
+            os.environ.pop("MTTS_UNFUSED_NORM")
+        out = []
+        for s in range(n_steps):
+            if s == 0:
+                lg = eng.forward(torch.from_numpy(genr[:, :T].copy()), torch.from_numpy(maskr[:, :T].astype(np.uint8)), 0)
+            else:
+                p = T + s - 1
+                lg = eng.forward(torch.from_numpy(genr[:, p:p + 1].copy()),
+                                 torch.from_numpy(maskr[:, :p + 1].astype(np.uint8)), p)
+            out.append(lg.cpu())
+        runs.append(out)
+        eng.close()
+    for s in range(n_steps):
+        assert torch.equal(runs[0][s].view(torch.int16), runs[1][s].view(torch.int16)), f"step {s}"
+    # the packed run against the oracle (rows repeat the B0 golden rows)
+    for s in range(1, n_steps):
+        lg = runs[0][s].float().numpy()
+        want = np.tile(tr.audio_logits[s], (rep, 1, 1))
+        V = cfg.vocab
+        got = lg[:, V:].reshape(B, cfg.n_vq, -1)[:, :, :want.shape[-1]]
+        fin = np.isfinite(want)
+        assert (np.isfinite(got) == fin).all(), s
+        scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
+        tol = 8 * ulp_bf16(np.broadcast_to(scale, want.shape))
+        assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), (s, float(np.abs(got[fin] - want[fin]).max()))
