@@ -69,8 +69,9 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   int nw = a.force_nw;
   // fused-norm launches stage (B+1)*K*2 bytes of LDS per block: 8 waves keep 2 blocks per CU
   // (q|k|v: 3.46 vs 3.53 ms/step with 16)
+  // packed 17-32 row inputs (one 1 KiB load per x fragment): 8 waves (B=32 4.51 -> 4.44 ms/step)
   if (nw != 4 && nw != 8 && nw != 16)
-    nw = (a.KT < 64 || NB == 2) ? 4 : ((rows >= 8192 || a.KT < 128 || NORM) ? 8 : 16);
+    nw = a.KT < 64 ? 4 : (NB == 2 ? (a.x_packed ? 8 : 4) : ((rows >= 8192 || a.KT < 128 || NORM) ? 8 : 16));
   // MTTS_GEMV_PIPE bit 0 / bit 1 flips the batch depth (8 <-> 4 k-tiles) for <= 16 / > 16 rows
   static const int pipe = getenv("MTTS_GEMV_PIPE") ? atoi(getenv("MTTS_GEMV_PIPE")) : 0;
   if ((NB == 1 && (pipe & 1)) || (NB == 2 && !(pipe & 2))) {
