@@ -285,9 +285,14 @@ __global__ __launch_bounds__(G * 64) void attn_prefill_kernel(AttnArgs a) {
   for (int i = 0; i < 4; ++i) {
     const int tq = s0 + g4 * 4 + i;
     if (tq >= a.S) continue;
-    bf16_t* dst = a.out + ((size_t)b * a.S + tq) * a.Hq * D + (size_t)hq * D;
+    const int mrow = b * a.S + tq;
+    bf16_t* dst = a.out + (size_t)mrow * a.Hq * D + (size_t)hq * D;
 #pragma unroll
-    for (int dt = 0; dt < DT; ++dt) dst[dt * 16 + c16] = f2bf(l_run[i] > 0.f ? o_run[dt][i] / l_run[i] : 0.f);
+    for (int dt = 0; dt < DT; ++dt) {
+      const bf16_t v = f2bf(l_run[i] > 0.f ? o_run[dt][i] / l_run[i] : 0.f);
+      if (a.out_tiles) a.out[xpkT_index(mrow, hq * D + dt * 16 + c16, a.out_tiles)] = v;
+      else dst[dt * 16 + c16] = v;
+    }
   }
 }
 

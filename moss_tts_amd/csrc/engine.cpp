@@ -413,15 +413,16 @@ extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
 // into the GEMV prologue (normalised rows staged in LDS per block, no extra launch); larger
 // ones run the single-pass rmsnorm_ss kernel into e->xn first.  Both read the residual
 // stream's per-16-column sums of squares e->ss.
-int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s, bool packed) {
+int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s, int tiles) {
   const int H = st.H, NT = H / 16;
   if (norm_lds_bytes(M, H) <= NORM_LDS_MAX && !e->unfused_norm) {
     g.x = st.h; g.ldx = H;
     g.ss_in = st.ss; g.ld_ss = NT; g.n_ss = NT; g.nw = nw; g.eps = e->c.rms_eps;
     return 0;
   }
-  HIPCHK(rmsnorm_ss(st.h, 0, H, st.ss, 0, NT, nw, st.xn, M, H, e->c.rms_eps, s, packed));
-  g.x = st.xn; g.ldx = H; g.x_packed = packed ? 1 : 0;
+  HIPCHK(rmsnorm_ss(st.h, 0, H, st.ss, 0, NT, nw, st.xn, M, H, e->c.rms_eps, s, tiles));
+  g.x = st.xn; g.ldx = H; g.x_packed = tiles ? 1 : 0;
+  g.pk_tiles = tiles > 2 ? tiles : 0;  // > 2: the prefill GEMM's form
   return 0;
 }
 
@@ -453,7 +454,7 @@ static int gemm_min_rows() {  // MTTS_GEMM_MIN_ROWS (A/B): token rows from which
   return v;
 }
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
-  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill && !g.x_packed && !g.y_packed) {
+  if (g.B >= gemm_min_rows() && !g.ss_in && !e->gemv_prefill && (!(g.x_packed || g.y_packed) || g.pk_tiles > 0)) {
     GemvArgs gg = g;  // short prompts split K over workgroups (gemm.hip)
     gg.ws = e->gk_ws;
     gg.ws_floats = e->gk_ws ? GK_WS_FLOATS : 0;
@@ -500,12 +501,17 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   // the fragment-packed layout, so each x fragment is one 1 KiB load (B=32 per layer: x loads
   // cost ~22 of 129 us row-major)
   const bool xpk = S == 1 && M > 16 && M <= 32 && st.rows >= 32 && e->xpack && !use_ao && !e->fused_ao;
+  // long prefills (the 32-utterance batch): the same for the 128 x 128 GEMM, T = M / 16 token
+  // tiles (its x loads were 81 of 191 ms row-major)
+  const int pkT = (S > 1 && M >= 1024 && e->xpack && !e->gemv_prefill && !e->old_prefill_attn &&
+                   M >= gemm_min_rows() && (M + 15) / 16 * 16 <= st.rows) ? (M + 15) / 16 : 0;
+  const int ntiles = xpk ? 2 : pkT;  // packed activations of this call (0: row-major)
   for (int l = 0; l < st.layers; ++l) {
     const LayerW& w = st.L[l];
     bf16_t* kc = st.kc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     bf16_t* vc = st.vc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     GemvArgs g = gemv_args(w.qkv, st.xn, H, st.qkvb, st.qkv_rows, M, st.qkv_rows, H);
-    if (int rc = normed_input(e, st, g, w.in_norm, M, s, xpk)) return rc;
+    if (int rc = normed_input(e, st, g, w.in_norm, M, s, ntiles)) return rc;
     g.force_nw = e->nw[0];
     DecAttnArgs da{};
     da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
@@ -554,6 +560,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       aa.q = st.qb; aa.kc = kc; aa.vc = vc; aa.mask = st.mask + (size_t)b0 * st.Cmax; aa.pos_base = pos_base;
       aa.part_o = st.part; aa.part_ml = st.part + (size_t)M * n_split * Hq * D; aa.out = st.attnb;
       aa.S = S; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = st.Cmax; aa.CH = CH; aa.n_split = n_split; aa.M = M;
+      aa.out_tiles = pkT;
       aa.scale = 1.0f / std::sqrt((float)D);
       if (e->old_prefill_attn) HIPCHK(attention(aa, s));
       else HIPCHK(attention_prefill(aa, s));
@@ -561,7 +568,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     if (!(S == 1 && fused_ao) && !use_ao) {
       g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
       g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
-      g.x_packed = xpk ? 1 : 0;
+      g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
       if (fuse_attn) {
         g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
         g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
@@ -569,13 +576,13 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       HIPCHK(proj(e, g, EPI_RESADD, s));
     }
     g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
-    if (int rc = normed_input(e, st, g, w.post_norm, M, s, xpk)) return rc;
+    if (int rc = normed_input(e, st, g, w.post_norm, M, s, ntiles)) return rc;
     g.force_nw = e->nw[2];
-    g.y_packed = xpk ? 1 : 0;
+    g.y_packed = ntiles ? 1 : 0;
     HIPCHK(proj(e, g, EPI_SWIGLU, s));
     g = gemv_args(w.down, st.act, I, st.h, H, M, H, I);
     g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
-    g.x_packed = xpk ? 1 : 0;
+    g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
     HIPCHK(proj(e, g, EPI_RESADD, s));
   }
   return 0;
@@ -872,7 +879,7 @@ extern "C" size_t mtts_k_attention_ws_bytes(int M, int Hq, int D, int n_split) {
 extern "C" int mtts_k_attention(const uint16_t* q, const uint16_t* kc, const uint16_t* vc, const uint8_t* mask,
                                 const int32_t* pos, uint16_t* out, void* ws, int M, int S, int Hq, int Hkv, int D,
                                 int Cmax, int CH, int n_split, void* stream) {
-  AttnArgs a;
+  AttnArgs a{};
   a.q = q; a.kc = kc; a.vc = vc; a.mask = mask; a.pos_base = pos;
   a.part_o = reinterpret_cast<float*>(ws);
   a.part_ml = a.part_o + (size_t)M * n_split * Hq * D;

@@ -164,7 +164,7 @@ int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void*
 int ensure_staging(mtts_engine* e, size_t bytes);
 bool parse_layer(const char* name, int* layer, std::string* rest);
 int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s,
-                 bool packed = false);
+                 int tiles = 0);
 Stack backbone_stack(mtts_engine* e);
 hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s);
 int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int* pos_base, int CH, int n_split,

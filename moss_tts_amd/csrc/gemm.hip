@@ -151,13 +151,16 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
 #pragma unroll
   for (int r = 0; r < WR; ++r)
     wbase[r] = reinterpret_cast<const u32x4*>(a.w) + ((size_t)min(rt0 + r, n_rt - 1) * KT) * 64 + lane;
+  // x_packed (pk_tiles = T): the fragment of token tile t at k tile kt is 1 KiB at (kt T + t) KiB
   const u32x4* xbase[WN];
   bool xok[WN];
+  const int xs = a.x_packed ? a.pk_tiles * 64 : 4;  // u32x4 stride per k tile
 #pragma unroll
   for (int j = 0; j < WN; ++j) {
     const int m = (tt0 + j) * 16 + c16;
     xok[j] = m < a.B;
-    xbase[j] = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[j] ? m : 0) * a.ldx + g4 * 8);
+    xbase[j] = a.x_packed ? reinterpret_cast<const u32x4*>(a.x) + (tt0 + j) * 64 + lane
+                          : reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[j] ? m : 0) * a.ldx + g4 * 8);
   }
   // SPLIT: blockIdx.z takes k-tiles [z*KS, (z+1)*KS) and writes its fp32 partial tile
   int kbeg = 0, kend = KT;
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
 #pragma unroll
       for (int r = 0; r < WR; ++r) wa[r][u] = wbase[r][(size_t)(kt + u) * 64];
 #pragma unroll
-      for (int j = 0; j < WN; ++j) xb[j][u] = xok[j] ? xbase[j][(kt + u) * 4] : (u32x4){0u, 0u, 0u, 0u};
+      for (int j = 0; j < WN; ++j) xb[j][u] = xok[j] ? xbase[j][(kt + u) * xs] : (u32x4){0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int u = 0; u < U; ++u)
@@ -223,7 +226,11 @@ __global__ __launch_bounds__(256) void gemm2_kernel(GemvArgs a) {
           o[i] = rbf(rbf(g / (1.0f + expf(-g))) * u);
         }
       }
-      if (mok) {
+      if (mok && a.y_packed) {  // SwiGLU output for the packed down-projection input
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (n0 + i < a.N) a.y[xpkT_index(m, n0 + i, a.pk_tiles)] = f2bf(o[i]);
+      } else if (mok) {
         bf16_t* yr = a.y + (size_t)m * a.ldy;
         if (n0 + 3 < a.N && (a.ldy % 4) == 0) {
           uint2 pk;
@@ -330,7 +337,8 @@ static void gemm2_launch(GemvArgs a, hipStream_t s) {
   a.n_row_tiles = (EPI == EPI_SWIGLU ? 2 : 1) * ((a.N + 15) / 16);
   const int mt = (a.B + 15) / 16;
   const dim3 grid((a.n_row_tiles + 2 * WR - 1) / (2 * WR), (mt + 2 * WN - 1) / (2 * WN));
-  const int S = gemm_splits<WR, WN, 4>(a, (int)grid.x, (int)grid.y);
+  // (the split-K reduce writes row-major: packed launches do not split)
+  const int S = (a.x_packed || a.y_packed) ? 1 : gemm_splits<WR, WN, 4>(a, (int)grid.x, (int)grid.y);
   if (S > 1) {
     hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4, true>), dim3(grid.x, grid.y, S), dim3(256), 0, s, a);
     const int n = a.B * ((a.N + 15) / 16);
@@ -349,6 +357,8 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   a.KT = a0.K / 32;
   const int n_tiles = (a0.N + 15) / 16;
   static const int big = getenv("MTTS_GEMM_SMALL") && getenv("MTTS_GEMM_SMALL")[0] == '1' ? 1 << 30 : 128;
+  // the packed layout is read / written by the 128 x 128 form only
+  if ((a0.x_packed || a0.y_packed) && (a0.B < big || a0.K % 64 || a0.pk_tiles * 16 < a0.B)) return hipErrorInvalidValue;
   if (a.B >= big && a.K % 64 == 0) {  // 128 x 128 block tiles
     switch (epi) {
       case EPI_STORE: gemm2_launch<4, 4, EPI_STORE>(a, s); break;

@@ -58,6 +58,7 @@ struct GemvArgs {
   size_t ws_floats;
   // 17-32 row decode (NB = 2): x / y in the fragment-packed layout (xpk_index) instead of [B, ld]
   int x_packed, y_packed;
+  int pk_tiles;        // prefill GEMM (gemm2): token tiles T of the packed x / y (0: decode form, T = 2)
 };
 
 // Fragment-packed activations of the 17-32 row decode GEMVs: the MFMA B-operand order of
@@ -65,9 +66,11 @@ struct GemvArgs {
 // wave's x fragment of one k tile is ONE contiguous 1 KiB load (row-major x puts the 16
 // tokens of a fragment 16 rows apart: 16 half-used cache lines per load).  u16 index of
 // (token b < 32, column k); the buffer holds 32 * K elements.
-__host__ __device__ inline size_t xpk_index(int b, int k) {
-  return ((((size_t)(k >> 5) * 2 + (b >> 4)) * 64 + (b & 15) + 16 * ((k & 31) >> 3)) << 3) + (k & 7);
+// The prefill GEMM's form holds T token tiles of 16 (T = ceil(M / 16)); the decode form is T = 2.
+__host__ __device__ inline size_t xpkT_index(int b, int k, int T) {
+  return ((((size_t)(k >> 5) * T + (b >> 4)) * 64 + (b & 15) + 16 * ((k & 31) >> 3)) << 3) + (k & 7);
 }
+__host__ __device__ inline size_t xpk_index(int b, int k) { return xpkT_index(b, k, 2); }
 
 inline GemvArgs gemv_args(const bf16_t* w, const bf16_t* x, int ldx, bf16_t* y, int ldy, int B, int N, int K) {
   GemvArgs a{};
@@ -104,6 +107,7 @@ struct AttnArgs {
   bf16_t* out;           // [M, Hq*D]
   int S, Hq, Hkv, D, Cmax, CH, n_split, M;
   float scale;
+  int out_tiles;         // > 0: out fragment-packed with this many 16-token tiles (xpkT_index)
 };
 
 // fused decode attention: one new token per row
@@ -187,7 +191,7 @@ hipError_t embed(const int64_t* ids, int C, const bf16_t* emb_text, const bf16_t
 hipError_t rmsnorm(const bf16_t* x, size_t x_off, size_t x_stride, const bf16_t* w, bf16_t* y, int M, int H, float eps,
                    hipStream_t s);
 hipError_t rmsnorm_ss(const bf16_t* x, size_t x_off, size_t x_stride, const float* ss, size_t ss_off, size_t ss_stride,
-                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s, bool y_packed = false);
+                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s, int y_tiles = 0);
 hipError_t qk_norm_rope(const QKRopeArgs& a, hipStream_t s);
 // attention.hip
 size_t attn_smem_bytes(int G, int D, int CH);

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(const bf16_t* __restrict__
 __global__ __launch_bounds__(512) void rmsnorm_ss_kernel(const bf16_t* __restrict__ x, size_t x_off, size_t x_stride,
                                                          const float* __restrict__ ss, size_t ss_off, size_t ss_stride,
                                                          const bf16_t* __restrict__ w, bf16_t* __restrict__ y, int H,
-                                                         float eps, int y_packed) {
+                                                         float eps, int y_tiles) {
   const int m = blockIdx.x;
   const int lane = threadIdx.x & 63;
   const int c = threadIdx.x;
@@ -127,16 +127,16 @@ __global__ __launch_bounds__(512) void rmsnorm_ss_kernel(const bf16_t* __restric
   for (int i = 0; i < 8; ++i) q[i] = g[i] * rbf(v[i] * r);
   uint4 o;
   o.x = pack2(q[0], q[1]); o.y = pack2(q[2], q[3]); o.z = pack2(q[4], q[5]); o.w = pack2(q[6], q[7]);
-  *reinterpret_cast<uint4*>(y + (y_packed ? xpk_index(m, c * 8) : (size_t)m * H + c * 8)) = o;
+  *reinterpret_cast<uint4*>(y + (y_tiles ? xpkT_index(m, c * 8, y_tiles) : (size_t)m * H + c * 8)) = o;
 }
 
 hipError_t rmsnorm_ss(const bf16_t* x, size_t x_off, size_t x_stride, const float* ss, size_t ss_off, size_t ss_stride,
-                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s, bool y_packed) {
+                      const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s, int y_tiles) {
   if (H % 16 || H > 4096) return hipErrorInvalidValue;  // one 16-byte chunk per thread, <= 512 threads
-  if (y_packed && (M > 32 || H % 32)) return hipErrorInvalidValue;
+  if (y_tiles && (M > 16 * y_tiles || H % 32)) return hipErrorInvalidValue;
   const int threads = ((H / 8 + 63) / 64) * 64;
   hipLaunchKernelGGL(rmsnorm_ss_kernel, dim3(M), dim3(threads < 64 ? 64 : threads), 0, s, x, x_off, x_stride, ss,
-                     ss_off, ss_stride, w, y, H, eps, y_packed ? 1 : 0);
+                     ss_off, ss_stride, w, y, H, eps, y_tiles);
   return hipGetLastError();
 }
 

@@ -253,3 +253,38 @@ def test_packed_activations_17_32_rows(gpu, golden, unfused_norm):
         scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
         tol = 8 * ulp_bf16(np.broadcast_to(scale, want.shape))
         assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), (s, float(np.abs(got[fin] - want[fin]).max()))
+
+
+def test_packed_activations_long_prefill(gpu, golden):
+    """Prefills of >= 1024 token rows keep the GEMM inputs fragment-packed (xpkT_index with
+    T = M / 16 token tiles): logits bit-identical to the row-major layout (MTTS_XPACK=0),
+    and within the oracle's bf16 band (a golden case tiled to > 1024 prompt rows)."""
+    import os
+    name = "g_nvq4_bf16"
+    g, c, cfg, W = case(golden, name)
+    ids, mask = g[name + "/input_ids"], g[name + "/mask"]
+    tr = O.StepTrace()
+    O.generate(W, cfg, ids, mask, max_new_tokens=1, text_temperature=0, audio_temperature=0, dtype="bf16", trace=tr)
+    B0, T, C = ids.shape
+    rep = (1024 // T + B0) // B0 + 1
+    idr, mkr = np.tile(ids, (rep, 1, 1)), np.tile(mask, (rep, 1))
+    B = idr.shape[0]
+    assert B * T >= 1024
+    runs = []
+    for flag in ("1", "0"):
+        os.environ["MTTS_XPACK"] = flag
+        try:
+            eng = make_engine(cfg, W, max_batch=B, max_prefill_tokens=max(2048, (B * T + 15) // 16 * 16))
+        finally:
+            os.environ.pop("MTTS_XPACK")
+        runs.append(eng.forward(torch.from_numpy(idr), torch.from_numpy(mkr.astype(np.uint8)), 0).cpu())
+        eng.close()
+    assert torch.equal(runs[0].view(torch.int16), runs[1].view(torch.int16))
+    lg = runs[0].float().numpy()
+    want = np.tile(tr.audio_logits[0], (rep, 1, 1))
+    got = lg[:, cfg.vocab:].reshape(B, cfg.n_vq, -1)[:, :, :want.shape[-1]]
+    fin = np.isfinite(want)
+    assert (np.isfinite(got) == fin).all()
+    scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
+    tol = 8 * ulp_bf16(np.broadcast_to(scale, want.shape))
+    assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), float(np.abs(got[fin] - want[fin]).max())
