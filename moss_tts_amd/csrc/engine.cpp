@@ -608,7 +608,9 @@ int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const
   // final norm on the last token of each row, then the 1+n_vq heads (audio pad column -inf)
   GemvArgs g = gemv_args(e->heads, e->xn, H, logits_out, e->heads_ld, B, e->heads_rows, H);
   if (S == 1) {
-    if (int rc = normed_input(e, st, g, e->final_norm, B, s)) return rc;
+    // 17-32 rows: the heads' input packed too (one 1 KiB load per x fragment)
+    const bool hpk = B > 16 && B <= 32 && st.rows >= 32 && e->xpack;
+    if (int rc = normed_input(e, st, g, e->final_norm, B, s, hpk ? 2 : 0)) return rc;
   } else {
     HIPCHK(rmsnorm_ss(e->h, (size_t)(S - 1) * H, (size_t)S * H, e->ss, (size_t)(S - 1) * NT, (size_t)S * NT,
                       e->final_norm, e->xn, B, H, eps, s));
