@@ -331,6 +331,8 @@ def main_local(args, world, rank, local):
         res = {
             "metric": METRIC, "value": round(audio_total / dt_max, 4), "unit": "audio-s/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(per_utt_ms, 3),
+            "step_def": f"one bench step = one generate() call over the batch ({frames} frames); the per-frame "
+                        "time is ms_per_frame",
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init bf16 weights at the MossTTSLocal-1.7B shape; synthetic clone prompts)",
             "config": {"workload": f"MossTTSLocal bf16 batch={B} on 1xMI355X (depth transformer, 1+32 channels/frame)",
@@ -541,7 +543,10 @@ def main():
         res = {
             "metric": METRIC, "value": round(audio_total / dt_max, 4), "unit": "audio-s/s",
             "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": round(per_utt_ms, 3), "higher_is_better": True, "scaling": "weak",
+            "ms_per_step": round(per_utt_ms, 3), "step_def": (
+                f"one bench step = one generate() call over the batch (prefill + {n_steps} decode steps); "
+                "the per-decode-step time is ms_per_decode_step"),
+            "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init bf16 weights at the MossTTSDelay-8B shape; synthetic clone prompts)",
             "config": {"workload": (("MOSS-TTSD long form (n_vq 16, 2000-token script, 7500 frames) bf16 batch="

@@ -133,6 +133,10 @@ int mtts_generate(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_
                   int* n_rows, void* stream);
 /* copy generation_ids [B, T + n_rows, 1+n_vq] (prompt included) to out_dev */
 int mtts_generate_fetch(mtts_engine* eng, int64_t* out_dev, int n_rows, void* stream);
+/* parity hook: copy the logits the last sampled step drew from (bf16 [B, heads_ld], the
+ * layout of mtts_forward; when no row sampled text outside audio mode, only the text tiles
+ * holding the special ids are current) to out_dev */
+int mtts_generate_logits(mtts_engine* eng, uint16_t* out_dev, void* stream);
 
 /* ---- MossTTSLocal (model_kind == MTTS_MODEL_LOCAL) -------------------------------------
  * Weights load by the reference names of moss_tts_local/modeling_moss_tts.py

@@ -86,6 +86,7 @@ _SIGS = {
     "mtts_k_moss_rmsnorm": (I, [P, P, P, I, I, F, P]),
     "mtts_k_local_pick": (I, [P, I, I, I, P, P, I, I, I, F, I, F, F, U64, I, P]),
     "mtts_generate_fetch": (I, [P, P, I, P]),
+    "mtts_generate_logits": (I, [P, P, P]),
     "mtts_k_pack": (I, [P, P, I, I, I, I, I, P]),
     "mtts_k_packed_bytes": (SZ, [I, I]),
     "mtts_k_gemv": (I, [P, P, I, P, I, P, I, I, I, I, I, I, I, I, P]),

@@ -368,6 +368,14 @@ __global__ __launch_bounds__(AO_T) void attn_o_kernel(AOArgs a) {
   }
   __syncthreads();
   if (!last_s) return;
+  // Hand-off form "sc1 payload, drained, relaxed agent ticket; every consumer load sc1"
+  // (cdna_hip_programming.md Guideline 16, R1 with sc1 loads): the producer side is the
+  // sc1 (write-through) stores above + the asm vmcnt(0) drain before the ticket; on this
+  // side every read of a partial is an agent-scope atomic (sc1) load, so no L1 line can be
+  // stale and the acquire reduces to a wavefront-scope fence that keeps the compiler from
+  // hoisting those loads above the ticket.  Plain stores or plain loads of the partials
+  // would need an agent-scope release / acquire pair instead.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // ---- the last arrival: sum the Hkv partials in head order, + residual, sums of squares ----
   const int n0 = rc * AO_ROWS;
   float (*sq_s)[AO_ROWS] = reinterpret_cast<float (*)[AO_ROWS]>(&p_s[0][0][0]);  // p_s is free by now

@@ -122,7 +122,7 @@ static int alloc_capacity(mtts_engine* e) {
   const int B = c.max_batch;
   if ((rc = e->alloc(&e->st, 1)) || (rc = e->alloc(&e->is_stopping, B)) || (rc = e->alloc(&e->is_audio, B)) ||
       (rc = e->alloc(&e->text_cand, B)) || (rc = e->alloc(&e->audio_cand, (size_t)B * c.n_vq)) ||
-      (rc = e->alloc(&e->part_idx, (size_t)B * TEXT_PARTS * MAXK)) || (rc = e->alloc(&e->part_val, (size_t)B * TEXT_PARTS * MAXK)) ||
+      (rc = e->alloc(&e->part_idx, (size_t)B * TEXT_PARTS)) || (rc = e->alloc(&e->part_val, (size_t)B * TEXT_PARTS)) ||
       (rc = e->alloc(&e->audio_len, B)) || (rc = e->alloc(&e->delayed, B)) || (rc = e->alloc(&e->cur_ids, (size_t)B * (c.n_vq + 1))) ||
       (rc = e->alloc(&e->gen_ids, (size_t)B * c.max_ctx * (c.n_vq + 1))) || (rc = e->alloc(&e->seen, 2 * e->audio_rows)))
     return rc;
@@ -734,9 +734,11 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   g.ids.audio_start = c.audio_start_token_id; g.ids.audio_end = c.audio_end_token_id;
   g.ids.user_slot = c.audio_user_slot_token_id; g.ids.gen_slot = c.audio_assistant_gen_slot_token_id;
   g.ids.delay_slot = c.audio_assistant_delay_slot_token_id; g.ids.audio_pad = c.audio_pad_code;
-  if ((g.text_sample && (sp->text_top_k > MAXK || sp->text_top_k <= 0)) ||
-      (g.audio_sample && (sp->audio_top_k > MAXK || sp->audio_top_k <= 0)))
-    return fail(MTTS_E_UNSUPPORTED, "top_k must be in [1, 64] when sampling");
+  // sampled text keeps at most TOPK_CAP candidates (top_k <= 0 would be the whole 151,936-id
+  // vocab); audio rows have 1,025 codes, so any audio top_k (<= 0: no filter) fits
+  if (g.text_sample && (sp->text_top_k <= 0 || sp->text_top_k > TOPK_CAP))
+    return fail(MTTS_E_UNSUPPORTED, "sampled text needs 1 <= text_top_k <= 2048");
+  if (e->audio_rows > TOPK_CAP) return fail(MTTS_E_UNSUPPORTED, "audio vocab above 2048");
   e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = forced;
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(e->seen, 0, 2 * e->audio_rows, s));
@@ -797,6 +799,8 @@ extern "C" int mtts_generate_poll(mtts_engine* e, int* steps, int* done_step, vo
       return fail(MTTS_E_HIP, "persistent decode launch: a stage wait timed out (results invalid)");
     }
   }
+  if (g.topk_overflow)
+    return fail(MTTS_E_UNSUPPORTED, "top-k: ties at the k-th score exceed 2048 candidates (lower top_k)");
   if (steps) *steps = g.step;
   if (done_step) *done_step = g.done_step;
   (void)stream;
@@ -838,6 +842,16 @@ extern "C" int mtts_generate_fetch(mtts_engine* e, int64_t* out, int n_rows, voi
   const size_t w = (size_t)(e->gen_T + n_rows) * C * sizeof(int64_t);
   HIPCHK(hipMemcpy2DAsync(out, w, e->gen_ids, (size_t)e->c.max_ctx * C * sizeof(int64_t), w, e->gen_B,
                           hipMemcpyDeviceToDevice, s));
+  leave(e, stream);
+  return 0;
+}
+
+extern "C" int mtts_generate_logits(mtts_engine* e, uint16_t* out, void* stream) {
+  if (!e || !out) return fail(MTTS_E_INVALID, "null argument");
+  if (e->lp) return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal engine: logits are per channel");
+  if (e->gen_B <= 0) return fail(MTTS_E_INVALID, "generate_begin not called");
+  hipStream_t s = enter(e, stream);
+  HIPCHK(hipMemcpyAsync(out, e->logits, (size_t)e->gen_B * e->heads_ld * sizeof(bf16_t), hipMemcpyDeviceToDevice, s));
   leave(e, stream);
   return 0;
 }

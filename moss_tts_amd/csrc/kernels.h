@@ -5,7 +5,6 @@
 namespace mtts {
 
 constexpr int64_t I64MAX = 0x7fffffffffffffffLL;
-constexpr int MAXK = 64;  // largest top-k handled on device
 
 enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 
@@ -133,6 +132,8 @@ struct DecAttnArgs {
   int out_packed;       // out in the fragment-packed layout (xpk_index; self-combining form, B <= 32)
 };
 
+constexpr int TOPK_CAP = 2048;  // largest sampler candidate set (topk.h); the host rejects top_k above it
+
 struct GenDev {
   // scalars
   int T0;          // prompt length
@@ -150,6 +151,7 @@ struct GenDev {
   int text_top_k, audio_top_k, text_sample, audio_sample;
   unsigned long long seed;
   MttsIds ids;
+  int topk_overflow;  // a sampler cut threshold ties at TOPK_CAP (reported by poll)
 };
 
 struct GenBufs {
@@ -163,7 +165,7 @@ struct GenBufs {
   int64_t* gen_ids;      // [B, Ltot, C]
   uint8_t* mask;         // [B, Cmax]
   uint8_t* seen;         // [2, audio_rows] union of the audio history (ch 1 | ch >= 2)
-  float* part_val;       // [B, P, K]
+  float* part_val;       // [B, P] greedy text slice argmax
   int* part_idx;
   int* text_cand;        // [B]
   int* audio_cand;       // [B, n_vq]
@@ -292,7 +294,7 @@ hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, 
 hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, uint8_t* seen,
                           int B, int C, int n_ch, int eos, int pad, hipStream_t s);
 // channel token: argmax (greedy) or HF penalty/temperature/top-k/top-p + draw (sampled)
-hipError_t local_pick(const GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
+hipError_t local_pick(GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
                       int C, int B, hipStream_t s);
 // init.hip
 hipError_t fill_uniform_bf16(bf16_t* dst, size_t n, unsigned long long seed, unsigned long long tensor_id, float scale,

@@ -512,8 +512,10 @@ extern "C" int mtts_k_local_pick(const uint16_t* logits, int ld, int V, int ch, 
   HIPCHK(hipMallocAsync((void**)&d, sizeof(GenDev), s));
   HIPCHK(hipMemcpyAsync(d, &g, sizeof(g), hipMemcpyHostToDevice, s));
   hipError_t err = local_pick(d, reinterpret_cast<const bf16_t*>(logits), ld, V, ch, seen, out, C, B, s);
+  if (err == hipSuccess) err = hipMemcpyAsync(&g, d, sizeof(g), hipMemcpyDeviceToHost, s);
   HIPCHK(hipFreeAsync(d, s));
   HIPCHK(err);
   HIPCHK(hipStreamSynchronize(s));
+  if (g.topk_overflow) return fail(MTTS_E_UNSUPPORTED, "top-k: ties at the k-th score exceed 2048 candidates");
   return 0;
 }

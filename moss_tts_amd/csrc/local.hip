@@ -3,6 +3,7 @@
 // of CustomMixin._sample (:377-456).  The projections and the depth transformer reuse the
 // GEMV / decode-attention kernels of the backbone.
 #include "kernels.h"
+#include "topk.h"
 
 namespace mtts {
 
@@ -92,23 +93,17 @@ hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld
 //   TopPLogitsWarper: ascending sort, bf16 softmax, cumsum; drop cum <= bf16(1 - top_p),
 //     the largest always kept
 // The k-th largest is found by a two-pass radix select on the 16-bit order-preserving keys
-// of the (bf16-exact) processed scores, so the whole vocab is never sorted.  The draw uses
+// of the (bf16-exact) processed scores (topk.h, TIES_KEEP_ALL), so the whole vocab is never
+// sorted; ties beyond TOPK_CAP candidates are cut in index order and reported by
+// mtts_generate_poll as an error (never an arrival-order choice).  The draw uses
 // Philox(seed; frame, row, channel): distribution-level parity (torch's RNG stream is not
 // reproduced).
-constexpr int PICK_CAND = 2048;
-
-__device__ __forceinline__ uint32_t okey(float v) {  // order-preserving key of a bf16-exact float
-  const uint32_t u = __float_as_uint(v) >> 16;
-  return (u & 0x8000u) ? (~u & 0xFFFFu) : (u | 0x8000u);
-}
-
-__global__ __launch_bounds__(1024) void local_pick_kernel(const GenDev* __restrict__ st, const bf16_t* __restrict__ logits,
+__global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ st, const bf16_t* __restrict__ logits,
                                                           int ld, int V, int ch, const uint8_t* __restrict__ seen,
                                                           int64_t* __restrict__ next, int C) {
   __shared__ ArgMax sh[16];
-  __shared__ int hist[256];
-  __shared__ int s_hi, s_need, s_thr, s_n;
-  __shared__ unsigned long long cand[PICK_CAND];
+  __shared__ TopkSmem sm;
+  __shared__ float ev[TOPK_CAP];
   const int b = blockIdx.x, t = threadIdx.x;
   const bf16_t* row = logits + (size_t)b * ld;
   const bool audio = ch > 0;
@@ -137,88 +132,19 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(const GenDev* __restri
     return rbf(v / temp);
   };
   const int K = top_k > 0 ? min(top_k, V) : V;
-  // pass 1: histogram of the high key byte over finite scores
-  for (int i = t; i < 256; i += 1024) hist[i] = 0;
-  __syncthreads();
-  for (int i = t; i < V; i += 1024) {
-    const float v = val(i);
-    if (v > -INFINITY) atomicAdd(&hist[okey(v) >> 8], 1);
+  int over = 0;
+  const int n = block_topk_sorted<1024>(val, V, K, TIES_KEEP_ALL, sm, &over);
+  if (n <= 0) {
+    if (t == 0) next[(size_t)b * C + ch] = 0;
+    return;
   }
+  const float mx = cand_score(sm.cand[0]);
+  for (int i = t; i < n; i += 1024) ev[i] = expf(cand_score(sm.cand[i]) - mx);
   __syncthreads();
   if (t == 0) {
-    int cum = 0, hi;
-    for (hi = 255; hi >= 0; --hi) {
-      if (cum + hist[hi] >= K) break;
-      cum += hist[hi];
-    }
-    s_hi = hi;  // -1: fewer than K finite scores (all are kept)
-    s_need = K - cum;
-  }
-  __syncthreads();
-  const int hi = s_hi;
-  if (hi >= 0) {
-    // pass 2: low byte inside the selected high bin
-    for (int i = t; i < 256; i += 1024) hist[i] = 0;
-    __syncthreads();
-    for (int i = t; i < V; i += 1024) {
-      const float v = val(i);
-      if (v > -INFINITY) {
-        const uint32_t k = okey(v);
-        if ((int)(k >> 8) == hi) atomicAdd(&hist[k & 255], 1);
-      }
-    }
-    __syncthreads();
-    if (t == 0) {
-      int cum = 0, lo;
-      for (lo = 255; lo > 0; --lo) {
-        if (cum + hist[lo] >= s_need) break;
-        cum += hist[lo];
-      }
-      s_thr = (hi << 8) | lo;
-    }
-  } else if (t == 0) {
-    s_thr = 0;
-  }
-  if (t == 0) s_n = 0;
-  __syncthreads();
-  // pass 3: candidates = finite scores with key >= threshold, sort key (score desc, index asc)
-  const uint32_t thr = (uint32_t)s_thr;
-  for (int i = t; i < V; i += 1024) {
-    const float v = val(i);
-    if (v > -INFINITY && okey(v) >= thr) {
-      const int slot = atomicAdd(&s_n, 1);
-      if (slot < PICK_CAND) cand[slot] = ((unsigned long long)(0xFFFFu - okey(v)) << 32) | (unsigned)i;
-    }
-  }
-  __syncthreads();
-  const int n = min(s_n, PICK_CAND);
-  int np = 1;
-  while (np < n) np <<= 1;
-  for (int i = n + t; i < np; i += 1024) cand[i] = ~0ull;
-  __syncthreads();
-  // bitonic sort of np entries (ascending key)
-  for (int k = 2; k <= np; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < np; i += 1024) {
-        const int p = i ^ j;
-        if (p > i) {
-          const unsigned long long x = cand[i], y = cand[p];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) { cand[i] = y; cand[p] = x; }
-        }
-      }
-      __syncthreads();
-    }
-  if (t == 0) {
-    // scores from keys (bf16-exact), largest first
-    auto score = [&](int i) -> float {
-      const uint32_t k = 0xFFFFu - (uint32_t)(cand[i] >> 32);
-      const uint32_t u = (k & 0x8000u) ? (k & 0x7FFFu) : (~k & 0xFFFFu);
-      return __uint_as_float(u << 16);
-    };
-    const float mx = score(0);
+    if (over) st->topk_overflow = 1;  // ties beyond TOPK_CAP: mtts_generate_poll reports it
     float S = 0.f;
-    for (int i = 0; i < n; ++i) S += expf(score(i) - mx);
+    for (int i = 0; i < n; ++i) S += ev[i];
     // HF top-p on the ascending order: cum over candidates from the smallest up
     int keep = n;
     if (top_p < 1.0f) {
@@ -226,25 +152,25 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(const GenDev* __restri
       float cum = 0.f;
       keep = 1;
       for (int i = n - 1; i >= 1; --i) {
-        cum += rbf(expf(score(i) - mx) / S);
+        cum += rbf(ev[i] / S);
         if (rbf(cum) > thr_p) { keep = i + 1; break; }
       }
     }
     float S2 = 0.f;
-    for (int i = 0; i < keep; ++i) S2 += expf(score(i) - mx);
+    for (int i = 0; i < keep; ++i) S2 += ev[i];
     const float u = philox_uniform(st->seed, (uint32_t)st->step, (uint32_t)b, (uint32_t)ch);
     const float target = u * S2;
     float c = 0.f;
-    int pick = (int)(cand[keep - 1] & 0xffffffffu);
+    int pick = cand_index(sm.cand[keep - 1]);
     for (int i = 0; i < keep; ++i) {
-      c += expf(score(i) - mx);
-      if (c > target) { pick = (int)(cand[i] & 0xffffffffu); break; }
+      c += ev[i];
+      if (c > target) { pick = cand_index(sm.cand[i]); break; }
     }
-    next[(size_t)b * C + ch] = n > 0 ? pick : 0;
+    next[(size_t)b * C + ch] = pick;
   }
 }
 
-hipError_t local_pick(const GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
+hipError_t local_pick(GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
                       int C, int B, hipStream_t s) {
   if (B <= 0 || V <= 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(local_pick_kernel, dim3(B), dim3(1024), 0, s, st, logits, ld, V, ch, seen, next, C);

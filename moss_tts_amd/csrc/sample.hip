@@ -8,13 +8,19 @@
 // (moss_tts_delay/inference_utils.py:19-145).
 //
 // Per step:
-//   score         (B, P + n_vq)   blocks y < P: top-K (K = 1 for greedy) of each text vocab slice,
+//   score         (B, P + n_vq)   blocks y < P: greedy text only -- argmax of each text vocab slice,
 //                                 special ids excluded (skipped when no row samples text freely);
-//                                 y >= P: audio channel y-P: temperature, repetition penalty,
-//                                 top-k/top-p, argmax | draw
-//   text_select   (B)            merge partials + allowed special ids under the step's masks
+//                                 y >= P: audio channel y-P of the rows the step samples:
+//                                 temperature, pad ban, repetition penalty, argmax | top-k ->
+//                                 top-p -> draw
+//   text_select   (B)            greedy: merge slice argmaxes + allowed special ids under the
+//                                 step's masks; sampled: top-k over the whole masked row
+//                                 (topk.h radix select), top-p, draw
 //   finalize      (1 block)      state update, next input ids, generation buffer, mask, stop
+// Draws: Philox(seed; step, row, channel) uniforms through torch's bf16 softmax / cumsum
+// arithmetic (torch_draw); distribution-level parity, torch's RNG stream is not reproduced.
 #include "kernels.h"
+#include "topk.h"
 
 namespace mtts {
 
@@ -41,167 +47,174 @@ __device__ __forceinline__ bool is_special_text(int i, const MttsIds& d) {
 __device__ __forceinline__ float scaled(bf16_t v, float temp) { return rbf(bf2f(v) / temp); }
 
 // ---------------------------------------------------------------------------
-// top-K of one text vocab slice (special ids excluded), K = 1 when greedy
+// greedy text: argmax of one text vocab slice (special ids excluded; they are merged by
+// text_select under the step's masks).  Sampled text selects over the whole row in text_select.
 __device__ void text_partial_body(const GenBufs& g, int b, int p) {
   const GenDev& st = *g.st;
-  if (!st.need_text) return;  // every sampling row is in audio mode: partials unused
-  const int K = st.text_sample ? min(st.text_top_k > 0 ? st.text_top_k : MAXK, MAXK) : 1;
+  if (!st.need_text || st.text_sample) return;  // partials unused
   const int lo = p * st.part_len, hi = min(st.vocab, lo + st.part_len);
   const bf16_t* row = g.logits + (size_t)b * st.heads_ld;
-  __shared__ float vals[4096];
   __shared__ ArgMax sh[4];
-  const float temp = st.text_sample ? st.text_temp : 1.0f;
-  const int n = hi - lo;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const int id = lo + i;
-    vals[i] = is_special_text(id, st.ids) ? -INFINITY : scaled(row[id], temp);
-  }
-  __syncthreads();
-  float* ov = g.part_val + ((size_t)b * st.P + p) * MAXK;
-  int* oi = g.part_idx + ((size_t)b * st.P + p) * MAXK;
-  for (int k = 0; k < K; ++k) {
-    ArgMax a{-INFINITY, 0x7fffffff};
-    for (int i = threadIdx.x; i < n; i += 256) a = am_better(a, ArgMax{vals[i], lo + i});
-    a = block_argmax(a, sh);
-    if (threadIdx.x == 0) {
-      ov[k] = a.v;
-      oi[k] = a.i;
-    }
-    if (a.i != 0x7fffffff && threadIdx.x == ((a.i - lo) & 255)) vals[a.i - lo] = -INFINITY;
-    __syncthreads();
+  ArgMax a{-INFINITY, 0x7fffffff};
+  for (int id = lo + (int)threadIdx.x; id < hi; id += 256)
+    if (!is_special_text(id, st.ids)) a = am_better(a, ArgMax{bf2f(row[id]), id});
+  a = block_argmax(a, sh);
+  if (threadIdx.x == 0) {
+    g.part_val[(size_t)b * st.P + p] = a.v;
+    g.part_idx[(size_t)b * st.P + p] = a.i;
   }
 }
 
-// sample from (or argmax over) a candidate list sorted descending (val, idx).
-// top-p restates apply_top_p_optimized (inference_utils.py:44-59): keep the smallest
-// prefix whose cumulative probability exceeds p (the first candidate always kept).
-__device__ int draw_sorted(const float* v, const int* idx, int n, float top_p, float u) {
-  if (n <= 0) return idx[0];
-  const float mx = v[0];
-  float tot = 0.f;
-  for (int i = 0; i < n; ++i) tot += (v[i] == -INFINITY) ? 0.f : expf(v[i] - mx);
+// torch's sample_token tail (inference_utils.py:129-145, apply_top_p_optimized :44-59) over
+// the top-k candidates sorted by score (descending; index ascending among equal scores), the
+// non-candidates being -inf.  ev[i] = exp(s_i - s_0) (fp32).  Every torch op here runs on
+// bf16 tensors with fp32 internals:
+//   probs = bf16(ev / S);  cum = bf16(fp32 cumsum of probs);  remove where cum > top_p,
+//   shifted right by one (the first candidate always stays);
+//   q = bf16(ev / S2) over the survivors;  multinomial(q) as an inverse CDF at u * sum(q).
+// Returns the position of the drawn candidate.  One thread.
+__device__ int torch_draw(const float* ev, int n, float top_p, float u) {
+  float S = 0.f;
+  for (int i = 0; i < n; ++i) S += ev[i];
   int keep = n;
   if (top_p < 1.0f) {
     float cum = 0.f;
     for (int i = 0; i < n; ++i) {
-      const float p = (v[i] == -INFINITY) ? 0.f : expf(v[i] - mx) / tot;
-      cum += p;
-      if (cum > top_p) { keep = i + 1; break; }
+      cum += rbf(ev[i] / S);
+      if (rbf(cum) > top_p) { keep = i + 1; break; }
     }
   }
-  float t2 = 0.f;
-  for (int i = 0; i < keep; ++i) t2 += (v[i] == -INFINITY) ? 0.f : expf(v[i] - mx);
-  const float target = u * t2;
+  float S2 = 0.f;
+  for (int i = 0; i < keep; ++i) S2 += ev[i];
+  float Q = 0.f;
+  for (int i = 0; i < keep; ++i) Q += rbf(ev[i] / S2);
+  const float target = u * Q;
   float c = 0.f;
   for (int i = 0; i < keep; ++i) {
-    c += (v[i] == -INFINITY) ? 0.f : expf(v[i] - mx);
-    if (c > target) return idx[i];
+    c += rbf(ev[i] / S2);
+    if (c > target) return i;
   }
-  return idx[keep - 1];
+  return keep - 1;
 }
 
-// text decision for rows that sample the text channel (modeling_moss_tts.py:453-471)
-__global__ __launch_bounds__(256) void text_select_kernel(GenBufs g) {
+// candidates in sm.cand[0..n) -> exp terms (all threads), then the draw (thread 0)
+template <int NT>
+__device__ int draw_candidates(TopkSmem& sm, float* ev, int n, float top_p, float u) {
+  if (n <= 0) return -1;
+  const float mx = cand_score(sm.cand[0]);
+  for (int i = threadIdx.x; i < n; i += NT) ev[i] = expf(cand_score(sm.cand[i]) - mx);
+  __syncthreads();
+  return threadIdx.x == 0 ? cand_index(sm.cand[torch_draw(ev, n, top_p, u)]) : -1;
+}
+
+// row b samples its text channel at this step (modeling_moss_tts.py:457)
+__device__ __forceinline__ bool samples_text(const GenBufs& g, int b) {
+  return g.is_stopping[b] == 0 && g.delayed[b] > (int64_t)g.st->n_vq;
+}
+
+// text decision for rows that sample the text channel (modeling_moss_tts.py:453-471).
+//   greedy: merge the slice argmaxes with the allowed special ids;
+//   sampled, audio mode: the two allowed ids {gen_slot, delay_slot} (delay banned at step 0);
+//   sampled, text mode: top-k over the whole masked row (radix select), then top-p + draw.
+constexpr int TSEL_NT = 1024;
+__global__ __launch_bounds__(TSEL_NT) void text_select_kernel(GenBufs g) {
   const GenDev& st = *g.st;
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x;
+  if (!samples_text(g, b)) return;  // finalize does not read text_cand for this row
   const MttsIds& d = st.ids;
   const int step = st.step;
   const bool isa = g.is_audio[b] != 0;
   const bf16_t* row = g.logits + (size_t)b * st.heads_ld;
   const float temp = st.text_sample ? st.text_temp : 1.0f;
-  __shared__ float cv[MAXK * 64 + 8];
-  __shared__ int ci[MAXK * 64 + 8];
-  __shared__ float sv[MAXK];
-  __shared__ int si[MAXK];
-  __shared__ ArgMax sh[4];
-  const int K = st.text_sample ? min(st.text_top_k > 0 ? st.text_top_k : MAXK, MAXK) : 1;
-  // candidates: general partials (only when not in audio mode) + allowed specials
-  int nc = 0;
-  if (!isa) {
-    const int np = st.P * K;
-    for (int i = threadIdx.x; i < np; i += 256) {
-      const int p = i / K, k = i % K;
-      cv[i] = g.part_val[((size_t)b * st.P + p) * MAXK + k];
-      ci[i] = g.part_idx[((size_t)b * st.P + p) * MAXK + k];
-    }
-    nc = np;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    // masks: ~is_audio -> ban {pad, gen, delay, audio_end}; is_audio -> only {gen, delay};
-    // step 0 bans delay (151662); step <= n_vq bans im_end  (:459-464)
-    int k = nc;
-    if (isa) {
-      cv[k] = scaled(row[d.gen_slot], temp); ci[k++] = d.gen_slot;
-      cv[k] = (step == 0) ? -INFINITY : scaled(row[d.delay_slot], temp); ci[k++] = d.delay_slot;
-    } else {
-      cv[k] = (step <= st.n_vq) ? -INFINITY : scaled(row[d.im_end], temp); ci[k++] = d.im_end;
-    }
-    sv[0] = (float)k;  // stash count
-  }
-  __syncthreads();
-  const int ntot = (int)sv[0];
-  __syncthreads();
-  // select top-K of the candidates (iterative block argmax), sorted descending;
-  // candidate token ids are unique (disjoint vocab slices + excluded specials)
-  for (int k = 0; k < K; ++k) {
+  __shared__ TopkSmem sm;
+  __shared__ float ev[TOPK_CAP];
+  __shared__ ArgMax sh[TSEL_NT / 64];
+  // masks: ~is_audio bans {pad, gen, delay, audio_end}; is_audio allows only {gen, delay};
+  // step 0 bans 151662; step <= n_vq bans im_end (:459-464)
+  const bool ban_im_end = step <= st.n_vq;
+  if (!st.text_sample) {
     ArgMax a{-INFINITY, 0x7fffffff};
-    for (int i = threadIdx.x; i < ntot; i += 256) a = am_better(a, ArgMax{cv[i], ci[i]});
-    const ArgMax r = block_argmax(a, sh);
-    for (int i = threadIdx.x; i < ntot; i += 256)
-      if (ci[i] == r.i) cv[i] = -INFINITY;
-    if (threadIdx.x == 0) { sv[k] = r.v; si[k] = r.i; }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    int tok;
-    if (!st.text_sample) {
-      tok = si[0];
+    if (isa) {
+      if (t == 0) a = ArgMax{scaled(row[d.gen_slot], temp), d.gen_slot};
+      if (t == 1 && step != 0) a = ArgMax{scaled(row[d.delay_slot], temp), d.delay_slot};
     } else {
-      const float u = philox_uniform(st.seed, (uint32_t)step, (uint32_t)b, 0u);
-      tok = draw_sorted(sv, si, K, st.text_top_p, u);
+      for (int p = t; p < st.P; p += TSEL_NT)
+        a = am_better(a, ArgMax{g.part_val[(size_t)b * st.P + p], g.part_idx[(size_t)b * st.P + p]});
+      if (t == 0 && !ban_im_end) a = am_better(a, ArgMax{scaled(row[d.im_end], temp), d.im_end});
     }
-    g.text_cand[b] = tok;
+    a = wave_argmax(a);
+    if ((t & 63) == 0) sh[t >> 6] = a;
+    __syncthreads();
+    if (t == 0) {
+      ArgMax r = sh[0];
+      for (int w = 1; w < TSEL_NT / 64; ++w) r = am_better(r, sh[w]);
+      g.text_cand[b] = r.i == 0x7fffffff ? d.pad : r.i;
+    }
+    return;
   }
+  const int K = st.text_top_k;  // validated on the host: 1..TOPK_CAP
+  int n;
+  if (isa) {
+    if (t == 0) {
+      const float vg = scaled(row[d.gen_slot], temp);
+      const float vd = step == 0 ? -INFINITY : scaled(row[d.delay_slot], temp);
+      n = 0;
+      if (vg > -INFINITY) sm.cand[n++] = cand_word(okey16(vg), d.gen_slot);
+      if (vd > -INFINITY) sm.cand[n++] = cand_word(okey16(vd), d.delay_slot);
+      if (n == 2 && sm.cand[1] < sm.cand[0]) { const auto x = sm.cand[0]; sm.cand[0] = sm.cand[1]; sm.cand[1] = x; }
+      sm.s_n = min(n, K);
+    }
+    __syncthreads();
+    n = sm.s_n;
+  } else {
+    auto val = [&](int i) -> float {
+      if (i == d.pad || i == d.gen_slot || i == d.delay_slot || i == d.audio_end) return -INFINITY;
+      if ((ban_im_end && i == d.im_end) || (step == 0 && i == 151662)) return -INFINITY;
+      return scaled(row[i], temp);
+    };
+    n = block_topk_sorted<TSEL_NT>(val, st.vocab, K, TIES_EXACT_K, sm, nullptr);
+  }
+  const float u = philox_uniform(st.seed, (uint32_t)step, (uint32_t)b, 0u);
+  const int tok = draw_candidates<TSEL_NT>(sm, ev, n, st.text_top_p, u);
+  if (t == 0) g.text_cand[b] = n > 0 ? tok : d.pad;
 }
 
-// audio channel j of row b: candidates over 1025 codes (modeling_moss_tts.py:483-503)
+// audio channel j of row b (modeling_moss_tts.py:474-503): temperature, pad code banned,
+// repetition penalty over the batch-wide history (inference_utils.py:79-88), then argmax or
+// top-k (torch.topk) -> top-p -> draw.  Rows/channels the step does not sample are skipped.
 __device__ void audio_select_body(const GenBufs& g, int b, int j) {
   const GenDev& st = *g.st;
+  {
+    const int64_t al = g.audio_len[b], dl = g.delayed[b];
+    const bool pre = al > j, post = dl == I64MAX || (int64_t)j > dl - 1;  // :477-480
+    if (!(pre && post)) return;
+  }
   const int V = st.audio_rows;
   const bf16_t* row = g.logits + (size_t)b * st.heads_ld + st.vocab + (size_t)j * V;
   const uint8_t* seen = g.seen + (j == 0 ? 0 : V);
-  __shared__ float vals[1040];
-  __shared__ ArgMax sh[4];
-  __shared__ float sv[MAXK];
-  __shared__ int si[MAXK];
   const float temp = st.audio_sample ? st.audio_temp : 1.0f;
   const float pen = st.rep_penalty;
-  for (int i = threadIdx.x; i < V; i += 256) {
-    float v = scaled(row[i], temp);
-    if (i == st.ids.audio_pad) v = -INFINITY;  // :486-487
-    if (pen != 1.0f && seen[i]) v = v > 0.f ? rbf(v / pen) : rbf(v * pen);  // inference_utils.py:79-88
-    vals[i] = v;
-  }
-  __syncthreads();
-  const int K = st.audio_sample ? min(st.audio_top_k > 0 ? st.audio_top_k : MAXK, MAXK) : 1;
-  for (int k = 0; k < K; ++k) {
+  const int pad = st.ids.audio_pad;
+  auto val = [&](int i) -> float {
+    if (i == pad) return -INFINITY;  // :486-487
+    const float v = scaled(row[i], temp);
+    return (pen != 1.0f && seen[i]) ? (v > 0.f ? rbf(v / pen) : rbf(v * pen)) : v;
+  };
+  if (!st.audio_sample) {
+    __shared__ ArgMax sh[4];
     ArgMax a{-INFINITY, 0x7fffffff};
-    for (int i = threadIdx.x; i < V; i += 256) a = am_better(a, ArgMax{vals[i], i});
+    for (int i = threadIdx.x; i < V; i += 256) a = am_better(a, ArgMax{val(i), i});
     a = block_argmax(a, sh);
-    if (threadIdx.x == 0) { sv[k] = a.v; si[k] = a.i; }
-    if (a.i != 0x7fffffff && threadIdx.x == (a.i & 255)) vals[a.i] = -INFINITY;
-    __syncthreads();
+    if (threadIdx.x == 0) g.audio_cand[(size_t)b * st.n_vq + j] = a.i == 0x7fffffff ? 0 : a.i;
+    return;
   }
-  if (threadIdx.x == 0) {
-    int tok;
-    if (!st.audio_sample) tok = si[0];
-    else {
-      const float u = philox_uniform(st.seed, (uint32_t)st.step, (uint32_t)b, 1u + (uint32_t)j);
-      tok = draw_sorted(sv, si, K, st.audio_top_p, u);
-    }
-    g.audio_cand[(size_t)b * st.n_vq + j] = tok;
-  }
+  __shared__ TopkSmem sm;
+  __shared__ float ev[TOPK_CAP];
+  const int K = st.audio_top_k > 0 ? st.audio_top_k : V;  // top_k <= 0: no top-k filter
+  const int n = block_topk_sorted<256>(val, V, K, TIES_EXACT_K, sm, nullptr);
+  const float u = philox_uniform(st.seed, (uint32_t)st.step, (uint32_t)b, 1u + (uint32_t)j);
+  const int tok = draw_candidates<256>(sm, ev, n, st.audio_top_p, u);
+  if (threadIdx.x == 0) g.audio_cand[(size_t)b * st.n_vq + j] = n > 0 ? tok : 0;
 }
 
 // state update (one block) -- modeling_moss_tts.py:453-516.  Phase 1: one thread per row
@@ -333,7 +346,7 @@ __global__ __launch_bounds__(256) void score_kernel(GenBufs g, int P) {
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s) {
   if (B > FIN_MAXB) return hipErrorInvalidValue;
   hipLaunchKernelGGL(score_kernel, dim3(B, P + n_vq), dim3(256), 0, s, g, P);
-  hipLaunchKernelGGL(text_select_kernel, dim3(B), dim3(256), 0, s, g);
+  hipLaunchKernelGGL(text_select_kernel, dim3(B), dim3(TSEL_NT), 0, s, g);
   hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, g);
   return hipGetLastError();
 }

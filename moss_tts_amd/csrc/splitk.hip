@@ -72,6 +72,14 @@ __global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int
   if (t == 0) last_s = __hip_atomic_fetch_add(cnt + bt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == S - 1;
   __syncthreads();
   if (!last_s) return;
+  // Hand-off form "sc1 payload, drained, relaxed agent ticket; every consumer load sc1"
+  // (cdna_hip_programming.md Guideline 16, R1 with sc1 loads): the producer side is the
+  // sc1 (write-through) stores above + the asm vmcnt(0) drain before the ticket; on this
+  // side every read of a partial is an agent-scope atomic (sc1) load, so no L1 line can be
+  // stale and the acquire reduces to a wavefront-scope fence that keeps the compiler from
+  // hoisting those loads above the ticket.  Plain stores or plain loads of the partials
+  // would need an agent-scope release / acquire pair instead.
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   // ---- the last arrival: sum the S partials in split order, + residual, sums of squares ----
   if (t < 256) {
     // element t: lane = t/4, reg = t%4 -> row n = ((lane>>4)*4 + reg), b = lane & 15

@@ -152,6 +152,7 @@ class Engine:
     def forward(self, ids: torch.Tensor, mask: torch.Tensor, past: int) -> torch.Tensor:
         """Teacher-forced forward: returns bf16 logits [B, heads_ld] of the last position."""
         B, S, _ = ids.shape
+        _check_mask(mask, B, past + S)
         ids = ids.to(self.device, torch.int64).contiguous()
         mask = mask.to(self.device, torch.uint8).contiguous()
         out = torch.empty(B, self.heads_ld, dtype=torch.bfloat16, device=self.device)
@@ -171,6 +172,7 @@ class Engine:
                      sampling: N.MttsSampling, forced_text: Optional[torch.Tensor] = None, chunk: int = 16):
         """Runs the whole device loop; returns generation_ids [B, T + n, 1+n_vq] (prompt included)."""
         B, T, C = input_ids.shape
+        _check_mask(attention_mask, B, T)
         ids = input_ids.to(self.device, torch.int64).contiguous()
         mask = None if attention_mask is None else attention_mask.to(self.device, torch.uint8).contiguous()
         forced = None
@@ -194,6 +196,7 @@ class Engine:
         c = self.cfg
         n_ch = C if n_vq_for_inference < 0 else min(C, 1 + n_vq_for_inference)
         ld = (c.vocab + 7) // 8 * 8
+        _check_mask(mask, B, past + S)
         ids = ids.to(self.device, torch.int64).contiguous()
         mask = mask.to(self.device, torch.uint8).contiguous()
         forced = forced.to(self.device, torch.int64).contiguous()
@@ -210,6 +213,7 @@ class Engine:
         text_* drive channel 0, audio_* the codebook channels); returns generation_ids
         [B, T + n, 1+n_vq]."""
         B, T, C = input_ids.shape
+        _check_mask(attention_mask, B, T)
         ids = input_ids.to(self.device, torch.int64).contiguous()
         mask = None if attention_mask is None else attention_mask.to(self.device, torch.uint8).contiguous()
         n = ctypes.c_int()
@@ -234,6 +238,7 @@ class GenerateSession:
                  max_new_tokens: int, sampling: N.MttsSampling, forced_text: Optional[torch.Tensor] = None):
         self.eng = eng
         self.B, self.T, self.C = input_ids.shape
+        _check_mask(attention_mask, self.B, self.T)
         self.max_new = max_new_tokens
         self._ids = input_ids.to(eng.device, torch.int64).contiguous()
         self._mask = None if attention_mask is None else attention_mask.to(eng.device, torch.uint8).contiguous()
@@ -265,12 +270,25 @@ class GenerateSession:
             N.check(N.load().mtts_generate_decode(self.eng._h, n, _stream_ptr(self.eng.device)), "generate_decode")
         return self.poll()
 
+    def logits(self) -> torch.Tensor:
+        """bf16 [B, heads_ld]: the logits the last sampled step drew from (parity hook)"""
+        out = torch.empty(self.B, self.eng.heads_ld, dtype=torch.bfloat16, device=self.eng.device)
+        N.check(N.load().mtts_generate_logits(self.eng._h, _ptr(out), _stream_ptr(self.eng.device)), "generate_logits")
+        return out
+
     def fetch(self) -> torch.Tensor:
         """generation_ids [B, T + n_rows, 1 + n_vq] (prompt included) so far"""
         out = torch.empty(self.B, self.T + self.n_rows, self.C, dtype=torch.int64, device=self.eng.device)
         N.check(N.load().mtts_generate_fetch(self.eng._h, _ptr(out), self.n_rows, _stream_ptr(self.eng.device)),
                 "fetch")
         return out
+
+
+def _check_mask(mask, B, L):
+    """the C ABI reads B x L mask bytes ([B, past + S] for a forward, [B, T] for generate):
+    a shorter mask would be read past its end (the reference forwards any mask to Qwen3)"""
+    if mask is not None and tuple(mask.shape) != (B, L):
+        raise ValueError(f"attention_mask must be [batch, past + seq] = [{B}, {L}], got {tuple(mask.shape)}")
 
 
 def sampling_params(text_temperature=1.5, text_top_p=1.0, text_top_k=50, audio_temperature=1.7, audio_top_p=0.8,

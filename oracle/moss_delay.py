@@ -367,14 +367,104 @@ def sampling_distribution(logits, top_k=None, top_p=None):
     return softmax(x)
 
 
+class PhiloxDraw:
+    """Draw source matching the engine: uniform u = Philox(seed; step, row, channel)
+    (`prng.philox_uniform`), channel 0 = text, 1 + j = audio channel j."""
+
+    def __init__(self, seed):
+        self.seed = int(seed)
+
+    def u(self, step, row, ch):
+        return prng.philox_uniform(self.seed, step, row, ch)
+
+
+def topk_candidates(x, k):
+    """`inference_utils.py:19-26` apply_top_k as the candidate list the draw runs over:
+    indices of the min(k, #finite) largest finite scores sorted by (score desc, index asc);
+    among scores equal to the k-th, the lowest indices (torch.topk leaves that order
+    unspecified; this is the convention the engine fixes).  k None / <= 0: every finite."""
+    x = np.asarray(x, np.float32)
+    fin = np.nonzero(x > -np.inf)[0]
+    order = fin[np.lexsort((fin, -x[fin]))]
+    if k is not None and k > 0:
+        order = order[:k]
+    return order
+
+
+def torch_keep_probs(vals, top_p, ids=None):
+    """`apply_top_p_optimized` (`inference_utils.py:44-59`) + the softmax of `sample_token`
+    (:139) on candidates sorted by score (desc; index asc), every torch op on bf16 tensors
+    with fp32 internals:
+      probs = bf16(e / S), e = exp(s - s_0);
+      sort(probs, descending): torch's sort is unstable, so the order inside a run of equal
+      bf16 probabilities is implementation-defined (measured: arbitrary on CPU); the score
+      order used here is one valid outcome (the kept count never depends on it -- equal
+      addends -- only which members of a boundary run survive: the higher scores);
+      cum = bf16(fp32 cumsum);  drop where cum > top_p (fp32 compare, torch's CUDA kernels),
+      shifted right by one;  q = bf16(e / S2) over the survivors.
+    All sums sequential fp32 in score order (the engine's order).  Returns (order, keep, q):
+    the survivors are vals[order[:keep]] (order is the identity; kept for callers)."""
+    r = _bf.rnd
+    f = np.float32
+    v = np.asarray(vals, np.float32)
+    n = v.size
+    ids = np.arange(n) if ids is None else np.asarray(ids)
+    ev = np.exp((v - v[0]).astype(np.float32)).astype(np.float32)
+    S = f(0)
+    for e in ev:
+        S = f(S + e)
+    order = np.arange(n)
+    keep = n
+    if top_p is not None and top_p < 1.0:
+        pb = r(ev / S)
+        cum = f(0)
+        for i in range(n):
+            cum = f(cum + pb[order[i]])
+            if r(cum) > f(top_p):
+                keep = i + 1
+                break
+    S2 = f(0)
+    for i in range(keep):
+        S2 = f(S2 + ev[order[i]])
+    return order, keep, r(np.array([f(ev[order[i]] / S2) for i in range(keep)], np.float32)).reshape(-1)
+
+
+def torch_draw(vals, top_p, u, ids=None):
+    """multinomial(q) of `sample_token` (`inference_utils.py:140`) as the inverse CDF at
+    u * sum(q) over `torch_keep_probs` (in its top-p order; ids = the candidates' token ids).
+    Returns (position in vals, margin): margin is the distance of the target from the nearest
+    CDF step, as a fraction of sum(q)."""
+    f = np.float32
+    order, keep, q = torch_keep_probs(vals, top_p, ids)
+    Q = f(0)
+    for x in q:
+        Q = f(Q + x)
+    target = f(f(u) * Q)
+    c, prev = f(0), f(0)
+    for i in range(keep):
+        prev, c = c, f(c + q[i])
+        if c > target:
+            return int(order[i]), float(min(target - prev, c - target) / Q)
+    return int(order[keep - 1]), 0.0
+
+
 def sample_token(ctx, logits, prev_tokens=None, repetition_penalty=1.0, top_p=None,
-                 top_k=None, do_sample=True, rng=None):
-    """`inference_utils.py:111-145`.  Greedy is exact; with do_sample the draw
-    uses `rng` (the distribution, not torch's RNG stream, is the contract)."""
+                 top_k=None, do_sample=True, rng=None, ctrs=None):
+    """`inference_utils.py:111-145`.  Greedy is exact.  With do_sample and a `PhiloxDraw`
+    rng, row r draws with u = rng.u(*ctrs[r]) through `topk_candidates` + `torch_draw`
+    (the engine's stream); another rng draws from `sampling_distribution` (the
+    distribution, not torch's RNG stream, is the reference contract)."""
     if prev_tokens is not None and repetition_penalty != 1.0:
         logits = repetition_penalty_2d(ctx, logits, prev_tokens, repetition_penalty)
     if not do_sample:
         return argmax_first(logits)
+    if isinstance(rng, PhiloxDraw):
+        out = []
+        for r_, row in enumerate(np.asarray(logits, np.float32)):
+            cand = topk_candidates(row, top_k)
+            pos, _ = torch_draw(row[cand], top_p, rng.u(*ctrs[r_]), ids=cand)
+            out.append(cand[pos])
+        return np.array(out, dtype=np.int64)
     probs = sampling_distribution(logits, top_k, top_p)
     rng = rng or np.random.default_rng(0)
     return np.array([rng.choice(probs.shape[1], p=pr) for pr in probs], dtype=np.int64)
@@ -387,6 +477,106 @@ def sample_token(ctx, logits, prev_tokens=None, repetition_penalty=1.0, top_p=No
 class StepTrace:
     text_logits: list = field(default_factory=list)      # masked text logits per step [B, V]
     audio_logits: list = field(default_factory=list)     # [B, n_vq, 1025] per step (pre-mask)
+
+
+def init_state(cfg, input_ids):
+    """`modeling_moss_tts.py:417-440`: per-row generate() state from the prompt."""
+    input_ids = np.asarray(input_ids, dtype=np.int64)
+    B, T, _ = input_ids.shape
+    last = input_ids[:, -1, 0]
+    is_cont = (last == cfg.audio_start_token_id) | (last == cfg.audio_assistant_gen_slot_token_id)
+    a_start = find_last_equal_C(input_ids[..., 0], cfg.audio_start_token_id)
+    a_mask = is_cont & (a_start != -1)
+    audio_lengths = np.zeros(B, np.int64)
+    audio_lengths[a_mask] = T - a_start[a_mask]
+    return dict(is_stopping=np.zeros(B, bool), audio_lengths=audio_lengths,
+                delayed=np.full(B, INT64_MAX, np.int64), is_audio=a_mask.copy())
+
+
+def decide_step(ctx, cfg, lg, step, st, gen, sp, rng=None, forced_text=None, trace=None):
+    """One step of the generate loop after the forward (`modeling_moss_tts.py:451-509`):
+    temperature, the text-channel schedule and masks, text / audio sampling, the counter
+    updates.  lg: per-head last-position logits [B, V_i]; st: `init_state` dict (updated in
+    place); gen: generation_ids so far [B, L, 1+n_vq] (the penalty history); sp: generate()
+    sampling kwargs.  Returns (next_text [B], next_audio [B, n_vq])."""
+    B = lg[0].shape[0]
+    n_vq = len(lg) - 1
+    ar = np.arange(n_vq)
+    text_do_sample = sp["text_temperature"] > 0
+    audio_do_sample = sp["audio_temperature"] > 0
+    t_temp = sp["text_temperature"] if text_do_sample else 1
+    a_temp = sp["audio_temperature"] if audio_do_sample else 1
+    is_stopping, is_audio = st["is_stopping"], st["is_audio"]
+    audio_lengths, delayed = st["audio_lengths"], st["delayed"]
+    excl0 = [cfg.pad_token_id, cfg.audio_assistant_gen_slot_token_id,
+             cfg.audio_assistant_delay_slot_token_id, cfg.audio_end_token_id]
+    allow1 = [cfg.audio_assistant_gen_slot_token_id, cfg.audio_assistant_delay_slot_token_id]
+
+    lg = [ctx.r(np.asarray(x, np.float32) / np.float32(t_temp if i == 0 else a_temp)) for i, x in enumerate(lg)]
+    nt = np.full(B, cfg.pad_token_id, np.int64)
+    nt[~is_stopping & (delayed < n_vq)] = cfg.audio_assistant_delay_slot_token_id
+    eos = ~is_stopping & (delayed == n_vq)
+    nt[eos] = cfg.audio_end_token_id
+    is_audio[eos] = False
+    samp_text = ~is_stopping & (delayed > n_vq)
+    t = lg[0].copy()
+    t[np.ix_(~is_audio, excl0)] = -np.inf
+    keep = np.zeros(t.shape[1], bool)
+    keep[allow1] = True
+    t[np.ix_(is_audio, ~keep)] = -np.inf
+    if step == 0:
+        t[:, 151662] = -np.inf
+    if step <= n_vq:
+        t[:, cfg.im_end_token_id] = -np.inf
+    if trace is not None:
+        trace.text_logits.append(t.copy())
+        trace.audio_logits.append(np.stack(lg[1:], axis=1).copy())
+    if samp_text.any():
+        rows = np.nonzero(samp_text)[0]
+        nt[samp_text] = sample_token(ctx, t[samp_text], top_p=sp["text_top_p"], top_k=sp["text_top_k"],
+                                     do_sample=text_do_sample, rng=rng, ctrs=[(step, b, 0) for b in rows])
+    if forced_text is not None:
+        f = np.asarray(forced_text)
+        fs = f[:, step] if f.ndim == 2 else np.full(B, f[step] if step < len(f) else -1)
+        sel = (fs >= 0) & ~is_stopping & samp_text
+        nt[sel] = fs[sel]
+    is_audio[nt == cfg.audio_start_token_id] = True
+    is_stopping[nt == cfg.im_end_token_id] = True
+
+    na = np.full((B, n_vq), cfg.audio_pad_code, np.int64)
+    pre = audio_lengths[:, None] > ar[None, :]
+    post = ar[None, :] > (np.where(delayed == INT64_MAX, 0, delayed) - 1)[:, None]
+    post[delayed == INT64_MAX] = True
+    sam = pre & post
+    if sam.sum() > 0:
+        pen = sp["audio_repetition_penalty"]
+        ch0 = lg[1][sam[:, 0]].copy()
+        rest = np.stack(lg[2:], axis=1)[sam[:, 1:]] if n_vq > 1 else np.zeros((0, lg[1].shape[1]), np.float32)
+        ch0[:, cfg.audio_pad_code] = -np.inf
+        rest = rest.copy()
+        rest[:, cfg.audio_pad_code] = -np.inf
+        col0 = na[:, 0]
+        col0[sam[:, 0]] = sample_token(ctx, ch0, prev_tokens=gen[:, :, 1], repetition_penalty=pen,
+                                       top_p=sp["audio_top_p"], top_k=sp["audio_top_k"],
+                                       do_sample=audio_do_sample, rng=rng,
+                                       ctrs=[(step, b, 1) for b in np.nonzero(sam[:, 0])[0]])
+        na[:, 0] = col0
+        if rest.shape[0]:
+            bj = np.argwhere(sam[:, 1:])  # row-major (b, j-1), the order of the boolean index
+            sub = na[:, 1:]
+            sub[sam[:, 1:]] = sample_token(ctx, rest, prev_tokens=gen[:, :, 2:], repetition_penalty=pen,
+                                           top_p=sp["audio_top_p"], top_k=sp["audio_top_k"],
+                                           do_sample=audio_do_sample, rng=rng,
+                                           ctrs=[(step, int(b), 2 + int(j)) for b, j in bj])
+            na[:, 1:] = sub
+    inc = ((nt == cfg.audio_start_token_id) | (nt == cfg.audio_assistant_gen_slot_token_id)
+           | (nt == cfg.audio_assistant_delay_slot_token_id))
+    audio_lengths[inc] += 1
+    audio_lengths[nt == cfg.audio_end_token_id] = 0
+    delayed[(delayed == INT64_MAX) & (nt == cfg.audio_assistant_delay_slot_token_id)] = 0
+    delayed[delayed != INT64_MAX] += 1
+    delayed[delayed > n_vq] = INT64_MAX
+    return nt, na
 
 
 def generate(W, cfg: Cfg, input_ids, attention_mask=None, max_new_tokens=1000,
@@ -406,99 +596,22 @@ def generate(W, cfg: Cfg, input_ids, attention_mask=None, max_new_tokens=1000,
     if attention_mask is None:
         attention_mask = np.ones((B, T), dtype=bool)
     mask = np.asarray(attention_mask, dtype=bool)
-    text_do_sample = text_temperature > 0
-    if not text_do_sample:
-        text_temperature = 1
-    audio_do_sample = audio_temperature > 0
-    if not audio_do_sample:
-        audio_temperature = 1
-
     cache = KVCache(cfg.layers)
     cur = input_ids
     gen = input_ids.copy()
-    is_stopping = np.zeros(B, bool)
-    audio_lengths = np.zeros(B, np.int64)
-    delayed = np.full(B, INT64_MAX, np.int64)
-    last = input_ids[:, -1, 0]
-    is_cont = (last == cfg.audio_start_token_id) | (last == cfg.audio_assistant_gen_slot_token_id)
-    a_start = find_last_equal_C(input_ids[..., 0], cfg.audio_start_token_id)
-    a_mask = is_cont & (a_start != -1)
-    audio_lengths[a_mask] = T - a_start[a_mask]
-    is_audio = a_mask.copy()
-    excl0 = [cfg.pad_token_id, cfg.audio_assistant_gen_slot_token_id,
-             cfg.audio_assistant_delay_slot_token_id, cfg.audio_end_token_id]
-    allow1 = [cfg.audio_assistant_gen_slot_token_id, cfg.audio_assistant_delay_slot_token_id]
-    ar = np.arange(n_vq)
+    st = init_state(cfg, input_ids)
+    sp = dict(text_temperature=text_temperature, text_top_p=text_top_p, text_top_k=text_top_k,
+              audio_temperature=audio_temperature, audio_top_p=audio_top_p, audio_top_k=audio_top_k,
+              audio_repetition_penalty=audio_repetition_penalty)
 
     for step in range(max_new_tokens):
         logits = forward(ctx, W, cfg, cur, mask, cache, last_only=True)
-        lg = [l[:, -1, :] for l in logits]
-        lg = [ctx.r(x / np.float32(text_temperature if i == 0 else audio_temperature)) for i, x in enumerate(lg)]
-        nt = np.full(B, cfg.pad_token_id, np.int64)
-        nt[~is_stopping & (delayed < n_vq)] = cfg.audio_assistant_delay_slot_token_id
-        eos = ~is_stopping & (delayed == n_vq)
-        nt[eos] = cfg.audio_end_token_id
-        is_audio[eos] = False
-        samp_text = ~is_stopping & (delayed > n_vq)
-        t = lg[0].copy()
-        t[np.ix_(~is_audio, excl0)] = -np.inf
-        keep = np.zeros(t.shape[1], bool)
-        keep[allow1] = True
-        t[np.ix_(is_audio, ~keep)] = -np.inf
-        if step == 0:
-            t[:, 151662] = -np.inf
-        if step <= n_vq:
-            t[:, cfg.im_end_token_id] = -np.inf
-        if trace is not None:
-            trace.text_logits.append(t.copy())
-            trace.audio_logits.append(np.stack(lg[1:], axis=1).copy())
-        if samp_text.any():
-            nt[samp_text] = sample_token(ctx, t[samp_text], top_p=text_top_p, top_k=text_top_k,
-                                         do_sample=text_do_sample, rng=rng)
-        if forced_text is not None:
-            f = np.asarray(forced_text)
-            fs = f[:, step] if f.ndim == 2 else np.full(B, f[step] if step < len(f) else -1)
-            sel = (fs >= 0) & ~is_stopping & samp_text
-            nt[sel] = fs[sel]
-        is_audio[nt == cfg.audio_start_token_id] = True
-        is_stopping[nt == cfg.im_end_token_id] = True
-
-        na = np.full((B, n_vq), cfg.audio_pad_code, np.int64)
-        pre = audio_lengths[:, None] > ar[None, :]
-        post = ar[None, :] > (np.where(delayed == INT64_MAX, 0, delayed) - 1)[:, None]
-        post[delayed == INT64_MAX] = True
-        sam = pre & post
-        if sam.sum() > 0:
-            ch0 = lg[1][sam[:, 0]].copy()
-            rest = np.stack(lg[2:], axis=1)[sam[:, 1:]] if n_vq > 1 else np.zeros((0, lg[1].shape[1]), np.float32)
-            ch0[:, cfg.audio_pad_code] = -np.inf
-            rest = rest.copy()
-            rest[:, cfg.audio_pad_code] = -np.inf
-            col0 = na[:, 0]
-            col0[sam[:, 0]] = sample_token(ctx, ch0, prev_tokens=gen[:, :, 1],
-                                           repetition_penalty=audio_repetition_penalty,
-                                           top_p=audio_top_p, top_k=audio_top_k,
-                                           do_sample=audio_do_sample, rng=rng)
-            na[:, 0] = col0
-            if rest.shape[0]:
-                sub = na[:, 1:]
-                sub[sam[:, 1:]] = sample_token(ctx, rest, prev_tokens=gen[:, :, 2:],
-                                               repetition_penalty=audio_repetition_penalty,
-                                               top_p=audio_top_p, top_k=audio_top_k,
-                                               do_sample=audio_do_sample, rng=rng)
-                na[:, 1:] = sub
-        inc = ((nt == cfg.audio_start_token_id) | (nt == cfg.audio_assistant_gen_slot_token_id)
-               | (nt == cfg.audio_assistant_delay_slot_token_id))
-        audio_lengths[inc] += 1
-        audio_lengths[nt == cfg.audio_end_token_id] = 0
-        delayed[(delayed == INT64_MAX) & (nt == cfg.audio_assistant_delay_slot_token_id)] = 0
-        delayed[delayed != INT64_MAX] += 1
-        delayed[delayed > n_vq] = INT64_MAX
-
+        nt, na = decide_step(ctx, cfg, [l[:, -1, :] for l in logits], step, st, gen, sp, rng=rng,
+                             forced_text=forced_text, trace=trace)
         cur = np.concatenate([nt[:, None, None], na[:, None, :]], axis=2)
-        mask = np.concatenate([mask, (~is_stopping)[:, None]], axis=1)
+        mask = np.concatenate([mask, (~st["is_stopping"])[:, None]], axis=1)
         gen = np.concatenate([gen, cur], axis=1)
-        if is_stopping.sum() == B:
+        if st["is_stopping"].sum() == B:
             break
 
     start = find_last_equal_C(input_ids[..., 0], cfg.im_start_token_id) + 3

@@ -40,3 +40,23 @@ def tensor(seed, tensor_id, shape, scale, offset=0.0):
     u = uniform(seed, tensor_id, n)
     v = np.float32(offset) + np.float32(scale) * (np.float32(2.0) * u - np.float32(1.0))
     return v.astype(np.float32).reshape(shape)
+
+
+_M32 = 0xFFFFFFFF
+
+
+def philox_uniform(seed, c0, c1, c2):
+    """Philox4x32-10 uniform in [0, 1) with 24 bits: the counter-based draw the samplers use
+    (`moss_tts_amd/csrc/common.h` philox_uniform; counters (step, row, channel), key = seed).
+    Pure-Python integers (test infrastructure only)."""
+    x0, x1, x2, x3 = int(c0) & _M32, int(c1) & _M32, int(c2) & _M32, 0x5EED
+    k0, k1 = int(seed) & _M32, (int(seed) >> 32) & _M32
+    for _ in range(10):
+        p0 = 0xD2511F53 * x0
+        p1 = 0xCD9E8D57 * x2
+        h0, l0 = p0 >> 32, p0 & _M32
+        h1, l1 = p1 >> 32, p1 & _M32
+        x0, x1, x2, x3 = h1 ^ x1 ^ k0, l1, h0 ^ x3 ^ k1, l0
+        k0 = (k0 + 0x9E3779B9) & _M32
+        k1 = (k1 + 0xBB67AE85) & _M32
+    return np.float32(x0 >> 8) * np.float32(1.0 / 16777216.0)
