@@ -404,6 +404,8 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="utterances per GPU")
     ap.add_argument("--layers", type=int, default=36)
     ap.add_argument("--decode-steps", type=int, default=208)
+    ap.add_argument("--text-tokens", type=int, default=0,
+                    help="override the synthetic prompt's text length (profiling long contexts)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-codec", action="store_true", help="skip the codec-decoder leg")
@@ -436,6 +438,8 @@ def main():
         if args.decode_steps == 208:
             args.decode_steps = 7500 + n_vq + 3
         args.extra_batches = ""
+    if args.text_tokens > 0:
+        text_tokens = args.text_tokens
     n_steps = args.decode_steps
     gen_frames = n_steps - (n_vq + 3)
     extra = [int(x) for x in args.extra_batches.split(",") if x] if args.extra_batches else []

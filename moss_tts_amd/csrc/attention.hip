@@ -390,6 +390,14 @@ static int decode_waves() {
 
 int attn_decode_keys_per_block() { return DEC_KW * decode_waves(); }
 
+// Publish-only decode attention (B <= 16: the o_proj prologue merges the split partials) up to
+// this many blocks per head; beyond it every o_proj workgroup would redo a long merge
+// (MTTS_ATTN_PO_MAX, A/B)
+int attn_publish_max_splits() {
+  static const int v = getenv("MTTS_ATTN_PO_MAX") ? atoi(getenv("MTTS_ATTN_PO_MAX")) : 4;
+  return v;
+}
+
 int attn_decode_splits(int Cmax) { return (Cmax + DEC_KW * decode_waves() - 1) / (DEC_KW * decode_waves()); }
 
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax) {

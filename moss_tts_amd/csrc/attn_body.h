@@ -303,7 +303,10 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
 
   // ---- merge the 16 wave partials (fixed order) into the block's result / partial ----
   const int t = threadIdx.x;
-  const bool single = nact == 1 && !a.publish_only;
+  // publish-only (o_proj merges) while the context spans <= po_max blocks; longer contexts
+  // merge here once instead of in every o_proj workgroup
+  const bool po = a.publish_only && nact <= a.po_max;
+  const bool single = nact == 1 && !po;
   float* part = a.part + (((size_t)b * a.Hkv + kvh) * a.ns + sp) * (G * (D + 2));
   for (int e = t; e < G * D; e += NWV * 64) {
     const int h = e / D, d = e % D;
@@ -326,7 +329,9 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       } else {
         *op = f2bf(L > 0.f ? o / L : 0.f);
       }
-    } else if constexpr (SC1) {
+    } else if (SC1 || !po) {
+      // consumed inside this launch (the last arriver below, or mega.hip): write-through (sc1)
+      // stores, drained before the ticket -- no release fence (cdna_hip_programming.md G16 R1)
       typedef __attribute__((address_space(1))) uint32_t g32;
       __hip_atomic_store((g32*)(part + e), __float_as_uint(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (d == 0) {
@@ -342,34 +347,32 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       }
     }
   }
-  if (single || a.publish_only || a.probe == 3) return;
+  if (single || po || a.probe == 3) return;
 
-  // ---- publish + arrival ticket (agent-scope release / acquire) ----
+  // ---- publish + arrival ticket.  Hand-off form "sc1 payload, drained, relaxed agent ticket;
+  // every consumer load sc1" (cdna_hip_programming.md Guideline 16, R1 with sc1 loads): the
+  // partials above went out write-through, every storing wave drains them before the block
+  // barrier, one lane takes the ticket, and the last arriver reads the partials with agent-scope
+  // atomic (sc1) loads, so no L1 line can be stale and no release / acquire fence is needed (an
+  // agent-scope release would write back this XCD's L2; an acquire invalidates the L1). ----
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   int* cnt = a.cnt + (size_t)b * a.Hkv + kvh;
   if (t == 0) {
-    // SC1: the partials were stored write-through and drained above (Guideline 16 R1), no
-    // release fence needed
-    if constexpr (!SC1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
     const int ticket = __hip_atomic_fetch_add(cnt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     last_s = ticket == nact - 1;
-    if (last_s) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
   }
   __syncthreads();
   if (!last_s) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // keeps the sc1 loads below the ticket
   // ---- the last arriver merges the nact partials in split order: the (m, l) pairs go to
   // LDS with all loads in flight at once, then each thread sums its element over splits ----
+  typedef __attribute__((address_space(1))) float gf32;
+  auto ld1 = [](const float* q) { return __hip_atomic_load((gf32*)q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
   const float* p0 = a.part + ((size_t)b * a.Hkv + kvh) * a.ns * (G * (D + 2));
   constexpr int PS = G * (D + 2);
   float* mlp = &mlp_s[0][0][0];
-  for (int i = t; i < nact * G * 2; i += NWV * 64) mlp[i] = p0[(size_t)(i / (2 * G)) * PS + G * D + i % (2 * G)];
+  for (int i = t; i < nact * G * 2; i += NWV * 64) mlp[i] = ld1(p0 + (size_t)(i / (2 * G)) * PS + G * D + i % (2 * G));
   __syncthreads();
   for (int e = t; e < G * D; e += NWV * 64) {
     const int h = e / D;
@@ -381,7 +384,7 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       const float ms = mlp[(s2 * G + h) * 2];
       const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
       L += f * mlp[(s2 * G + h) * 2 + 1];
-      o += f * p0[(size_t)s2 * PS + e];
+      o += f * ld1(p0 + (size_t)s2 * PS + e);
     }
     bf16_t* op = a.out + (a.out_packed ? xpk_index(b, kvh * G * D + e) : (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e);
     if constexpr (SC1) {

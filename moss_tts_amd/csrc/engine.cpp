@@ -519,6 +519,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     da.part = st.part; da.cnt = st.att_cnt;
     // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
     da.publish_only = fuse_attn ? 1 : 0;
+    da.po_max = attn_publish_max_splits();
     da.out_packed = xpk ? 1 : 0;
     da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
     // decode, small batch: q|k|v projection + attention in one launch (qa.hip)
@@ -572,6 +573,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       if (fuse_attn) {
         g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
         g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
+        g.attn.po_max = use_qa ? ATTN_PO_ALL : attn_publish_max_splits();  // qa.hip publishes every split
       }
       HIPCHK(proj(e, g, EPI_RESADD, s));
     }

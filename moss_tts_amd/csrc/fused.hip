@@ -98,6 +98,7 @@ hipError_t attn_oproj(const DecAttnArgs& da0, const GemvArgs& go0, int* sync, in
   go.attn.D = da.D;
   go.attn.ns = da.ns;
   go.attn.kb = DEC_KW * FUSED_NW;
+  go.attn.po_max = da.po_max = ATTN_PO_ALL;  // every split is published and merged in-launch
   const int n_att = da.ns * da.Hkv * B;
   const int n_o = (go.N + 15) / 16;
   switch (da.D) {

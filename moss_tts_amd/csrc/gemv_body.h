@@ -224,7 +224,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     const int nact = *v.pos / v.kb + 1;
     const int G = v.G, D = v.D, PS = G * (D + 2);
     const int i = threadIdx.x;
-    if (i < a.B * K8) {
+    if (nact > v.po_max) {  // long context: the attention merged its splits into x (bf16 rows)
+      if (i < a.B * K8) {
+        const int b = i / K8, c = i - b * K8;
+        xs_dyn[i] = reinterpret_cast<const u32x4*>(a.x + (size_t)b * a.ldx)[c];
+      }
+    } else if (i < a.B * K8) {
       const float* pp = v.part + ((size_t)pa_b * v.Hkv + pa_kvh) * v.ns * PS;
       float M = -INFINITY;
       for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, s2 < 2 ? pa_ml[s2 & 1].x : pp[(size_t)s2 * PS + G * D + 2 * pa_hg]);
@@ -255,6 +260,12 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     const AttnPartView& v = a.attn;
     const int nact = *v.pos / v.kb + 1;
     const int G = v.G, D = v.D, PS = G * (D + 2);
+    if (nact > v.po_max)  // long context: the attention merged its splits into x (bf16 rows)
+      for (int i = threadIdx.x; i < a.B * K8; i += NW * 64) {
+        const int b = i / K8, c = i - b * K8;
+        xs_dyn[i] = reinterpret_cast<const u32x4*>(a.x + (size_t)b * a.ldx)[c];
+      }
+    else
     for (int i = threadIdx.x; i < a.B * K8; i += NW * 64) {
       const int b = i / K8, k0 = (i - b * K8) * 8;
       const int h = k0 / D, d0 = k0 - h * D, kvh = h / G, hg = h - kvh * G;

@@ -20,10 +20,13 @@ constexpr int PREROW_MAXB = 5;
 inline bool norm_preload_fits(int B, int K) { return B <= 8 && (size_t)(B + 1) * K <= 8192 && K <= 4096; }
 
 // decode-attention split partials as read by the o_proj prologue (PRO_ATTN)
+constexpr int ATTN_PO_ALL = 1 << 30;  // po_max: every split publishes, the consumer merges
+
 struct AttnPartView {
   const float* part;   // [B][Hkv][ns][G*(D+2)]: o[G][D], then (m, l) per head
   const int* pos;      // device: position of the new token
   int Hkv, G, D, ns, kb;  // kb = keys per attention block
+  int po_max;             // contexts of more than po_max blocks were merged by the attention (read x)
 };
 
 struct GemvArgs {
@@ -128,6 +131,7 @@ struct DecAttnArgs {
   int nwv;              // waves per block (32 keys each; set by attn_decode)
   float eps, scale;
   int publish_only;     // 1: every block writes its (m, l, o) partial; the o_proj GEMV merges them
+  int po_max;           // publish_only applies up to po_max blocks per head; longer contexts merge here
   int probe;            // timing probe (MTTS_ATTN_PROBE): 0 full; 1 exit after pos; 2 after loads + prologue; 3 no combine
   int out_packed;       // out in the fragment-packed layout (xpk_index; self-combining form, B <= 32)
 };
@@ -203,6 +207,7 @@ hipError_t attention_prefill(const AttnArgs& a, hipStream_t s);
 hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s);
 int attn_decode_splits(int Cmax);
 int attn_decode_keys_per_block();
+int attn_publish_max_splits();
 // workspace of attn_decode: ticket counters (zero-filled once by the owner) + partials
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
 // fused.hip: decode attention + o_proj as one launch (block roles by arrival ticket);

@@ -108,6 +108,7 @@ hipError_t qkv_attn(const GemvArgs& g0, const DecAttnArgs& da0, int* sync, int B
   da.nwv = QA_NW;
   da.ns = attn_decode_splits(da.Cmax);
   da.publish_only = 1;
+  da.po_max = ATTN_PO_ALL;  // the o_proj GEMV merges every split (engine: g.attn.po_max)
   da.probe = 0;
   const int n_gemv = g.N / 16;
   const int n_att = da.ns * da.Hkv * B;

@@ -288,3 +288,36 @@ def test_packed_activations_long_prefill(gpu, golden):
     scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
     tol = 8 * ulp_bf16(np.broadcast_to(scale, want.shape))
     assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), float(np.abs(got[fin] - want[fin]).max())
+
+
+def test_long_context_decode_logits(gpu, golden):
+    """Decode steps at contexts of 5-6 attention blocks per KV head: past the publish-only
+    threshold (attn_publish_max_splits) the attention merges its split partials itself and
+    o_proj reads the merged rows.  Teacher-forced logits vs the oracle, ragged batch."""
+    name = "g_nvq4_bf16"
+    g, c, cfg, W = case(golden, name)
+    rng = np.random.default_rng(5)
+    B, T, steps = 2, 1290, 6
+    ids = np.full((B, T + steps, cfg.n_vq + 1), cfg.audio_pad_code, np.int64)
+    ids[..., 0] = rng.integers(200, 20000, (B, T + steps))
+    ids[:, :, 1:] = rng.integers(0, 1024, (B, T + steps, cfg.n_vq))
+    mask = np.ones((B, T + steps), bool)
+    mask[1, :37] = False  # left padding of row 1
+    ids[1, :37, 0] = cfg.pad_token_id
+    eng = make_engine(cfg, W, max_ctx=1408, max_prefill_tokens=4096)
+    ctx = O._Ctx("bf16")
+    cache = O.KVCache(cfg.layers)
+    for s in range(steps + 1):
+        p0, p1 = (0, T) if s == 0 else (T + s - 1, T + s)
+        want = O.forward(ctx, W, cfg, ids[:, p0:p1], mask[:, :p1], cache, last_only=True)
+        lg = eng.forward(torch.from_numpy(ids[:, p0:p1].copy()), torch.from_numpy(mask[:, :p1].astype(np.uint8)), p0)
+        got = [x.float().cpu().numpy() for x in eng.split_logits(lg)]
+        for j in range(1, cfg.n_vq + 1):
+            w = want[j][:, -1]
+            fin = np.isfinite(w)
+            assert (np.isfinite(got[j]) == fin).all()
+            scale = np.max(np.abs(np.where(fin, w, 0)), axis=-1, keepdims=True)
+            tol = 8 * ulp_bf16(np.broadcast_to(scale, w.shape))
+            err = np.abs(got[j][fin] - w[fin])
+            assert (err <= tol[fin]).all(), (s, j, float(err.max()))
+    eng.close()
