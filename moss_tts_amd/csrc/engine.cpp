@@ -415,7 +415,8 @@ extern "C" int mtts_engine_init_random(mtts_engine* e, uint64_t seed) {
 // stream's per-16-column sums of squares e->ss.
 int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s, int tiles) {
   const int H = st.H, NT = H / 16;
-  if (norm_lds_bytes(M, H) <= NORM_LDS_MAX && !e->unfused_norm) {
+  // (packed prefills, tiles > 2, run the GEMM, which has no norm prologue)
+  if (tiles <= 2 && norm_lds_bytes(M, H) <= NORM_LDS_MAX && !e->unfused_norm) {
     g.x = st.h; g.ldx = H;
     g.ss_in = st.ss; g.ld_ss = NT; g.n_ss = NT; g.nw = nw; g.eps = e->c.rms_eps;
     return 0;
@@ -503,7 +504,11 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   const bool xpk = S == 1 && M > 16 && M <= 32 && st.rows >= 32 && e->xpack && !use_ao && !e->fused_ao;
   // long prefills (the 32-utterance batch): the same for the 128 x 128 GEMM, T = M / 16 token
   // tiles (its x loads were 81 of 191 ms row-major)
-  const int pkT = (S > 1 && M >= 1024 && e->xpack && !e->gemv_prefill && !e->old_prefill_attn &&
+  // prefills of >= 128 token rows (the 128 x 128 GEMM's range): packed GEMM inputs.  B=1 clone
+  // prompt (181 rows) 12.6 -> 9.5 ms with the split-K partial launches reading them packed
+  // (MTTS_PK_MIN / MTTS_PK_SPLIT=0 for A/B)
+  static const int pk_min = getenv("MTTS_PK_MIN") ? atoi(getenv("MTTS_PK_MIN")) : 128;
+  const int pkT = (S > 1 && M >= pk_min && e->xpack && !e->gemv_prefill && !e->old_prefill_attn &&
                    M >= gemm_min_rows() && (M + 15) / 16 * 16 <= st.rows) ? (M + 15) / 16 : 0;
   const int ntiles = xpk ? 2 : pkT;  // packed activations of this call (0: row-major)
   for (int l = 0; l < st.layers; ++l) {

@@ -337,8 +337,9 @@ static void gemm2_launch(GemvArgs a, hipStream_t s) {
   a.n_row_tiles = (EPI == EPI_SWIGLU ? 2 : 1) * ((a.N + 15) / 16);
   const int mt = (a.B + 15) / 16;
   const dim3 grid((a.n_row_tiles + 2 * WR - 1) / (2 * WR), (mt + 2 * WN - 1) / (2 * WN));
-  // (the split-K reduce writes row-major: packed launches do not split)
-  const int S = (a.x_packed || a.y_packed) ? 1 : gemm_splits<WR, WN, 4>(a, (int)grid.x, (int)grid.y);
+  // (the split-K reduce writes row-major, so packed OUTPUTS do not split; packed inputs do)
+  static const int pk_split = getenv("MTTS_PK_SPLIT") ? atoi(getenv("MTTS_PK_SPLIT")) : 1;  // A/B
+  const int S = (a.y_packed || (a.x_packed && !pk_split)) ? 1 : gemm_splits<WR, WN, 4>(a, (int)grid.x, (int)grid.y);
   if (S > 1) {
     hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4, true>), dim3(grid.x, grid.y, S), dim3(256), 0, s, a);
     const int n = a.B * ((a.N + 15) / 16);

@@ -22,6 +22,7 @@ namespace mtts {
 namespace {
 constexpr int SK_NW = 8;  // waves per workgroup
 constexpr int SK_U = 8;   // k-tiles per load batch
+constexpr int SK_MAXS = 16;  // most K splits (the last arrival keeps all partial loads in flight)
 typedef __attribute__((address_space(1))) float gf32;
 }  // namespace
 
@@ -85,10 +86,18 @@ __global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int
     // element t: lane = t/4, reg = t%4 -> row n = ((lane>>4)*4 + reg), b = lane & 15
     const int ln = t >> 2, nl = ((ln >> 4) << 2) + (t & 3), bl = ln & 15;
     const int n = bt * 16 + nl;
-    const float* p0 = part + (size_t)bt * S * 256 + t;
+    // sc1 (device-scope) buffer loads (aux 16), all S in flight (atomic loads went one at a time)
+    const __amdgpu_buffer_rsrc_t prs =
+        __builtin_amdgcn_make_buffer_rsrc(part + (size_t)bt * S * 256, 0, S * 256 * 4, 0x00020000);
+    float pv[SK_MAXS];
+#pragma unroll
+    for (int j = 0; j < SK_MAXS; ++j)
+      pv[j] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          prs, j < S ? (uint32_t)(j * 256 + t) * 4u : 0x7ffffff0u, 0, 16));
     float s = 0.f;
-    for (int j = 0; j < S; ++j)
-      s += __hip_atomic_load((gf32*)(p0 + (size_t)j * 256), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int j = 0; j < SK_MAXS; ++j)
+      if (j < S) s += pv[j];
     bf16_t out = 0;
     if (bl < a.B && n < a.N) {
       // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
@@ -112,21 +121,21 @@ int gemv_splitk_splits(int n_tiles, int KT, int B) {
   // worth it when the tiles alone leave most CUs idle and K is long enough to split
   if (B > 16 || n_tiles >= 160 || KT < 128) return 1;
   static const int force = getenv("MTTS_SPLITK_S") ? atoi(getenv("MTTS_SPLITK_S")) : 0;  // A/B sweeps
-  if (force >= 2) return force;
+  if (force >= 2) return std::min(force, SK_MAXS);
   // at least one workgroup per CU and one load batch per wave, but a single round of at most
   // two workgroups per CU (MossTTSLocal down_proj, 96 tiles x K 8,960, frame ms by S:
   // 1: 11.21, 3: 10.86, 5: 10.45, 6: 11.02, 8: 11.49 -- 576+ workgroups need a second round)
   int S = std::max((256 + n_tiles - 1) / n_tiles, (KT + SK_NW * SK_U - 1) / (SK_NW * SK_U));
   while (S > 2 && n_tiles * S > 512) --S;
   while (S > 1 && KT / S < 4 * SK_NW) --S;  // >= 4 k-tiles per wave
-  return S;
+  return std::min(S, SK_MAXS);
 }
 
 size_t gemv_splitk_ws_floats(int n_tiles, int S) { return (size_t)n_tiles * S * 256; }
 
 hipError_t gemv_splitk(const GemvArgs& a0, int S, float* part, int* cnt, hipStream_t s) {
   GemvArgs a = a0;
-  if (a.K % 32 || a.B <= 0 || a.B > 16 || a.N <= 0 || S < 2 || !part || !cnt || !a.res || a.ss_in || a.attn.part ||
+  if (a.K % 32 || a.B <= 0 || a.B > 16 || a.N <= 0 || S < 2 || S > SK_MAXS || !part || !cnt || !a.res || a.ss_in || a.attn.part ||
       a.tile0 || a.gate)
     return hipErrorInvalidValue;
   a.KT = a.K / 32;

@@ -255,10 +255,12 @@ def test_packed_activations_17_32_rows(gpu, golden, unfused_norm):
         assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), (s, float(np.abs(got[fin] - want[fin]).max()))
 
 
-def test_packed_activations_long_prefill(gpu, golden):
-    """Prefills of >= 1024 token rows keep the GEMM inputs fragment-packed (xpkT_index with
-    T = M / 16 token tiles): logits bit-identical to the row-major layout (MTTS_XPACK=0),
-    and within the oracle's bf16 band (a golden case tiled to > 1024 prompt rows)."""
+@pytest.mark.parametrize("rows", [160, 1024])
+def test_packed_activations_long_prefill(gpu, golden, rows):
+    """Prefills of >= 128 token rows keep the GEMM inputs fragment-packed (xpkT_index with
+    T = M / 16 token tiles; split-K partial launches read them packed): logits bit-identical to
+    the row-major layout (MTTS_XPACK=0), and within the oracle's bf16 band (a golden case tiled
+    to >= rows prompt rows)."""
     import os
     name = "g_nvq4_bf16"
     g, c, cfg, W = case(golden, name)
@@ -266,10 +268,10 @@ def test_packed_activations_long_prefill(gpu, golden):
     tr = O.StepTrace()
     O.generate(W, cfg, ids, mask, max_new_tokens=1, text_temperature=0, audio_temperature=0, dtype="bf16", trace=tr)
     B0, T, C = ids.shape
-    rep = (1024 // T + B0) // B0 + 1
+    rep = (rows // T + B0) // B0 + 1
     idr, mkr = np.tile(ids, (rep, 1, 1)), np.tile(mask, (rep, 1))
     B = idr.shape[0]
-    assert B * T >= 1024
+    assert B * T >= max(rows, 128)
     runs = []
     for flag in ("1", "0"):
         os.environ["MTTS_XPACK"] = flag
