@@ -64,7 +64,7 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
-  const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN || PRO == PRO_ATTN_PRE ? (size_t)a.B * a.K * 2 : 0);
+  const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN || PRO == PRO_ATTN_PRE || PRO == PRO_ATTN_PRE2 ? (size_t)a.B * a.K * 2 : 0);
   // 17-32 rows (NB = 2): 4 waves of 4-deep batches (in-context B=32 sweep: 5.62 vs 6.03 ms/step)
   int nw = a.force_nw;
   // fused-norm launches stage (B+1)*K*2 bytes of LDS per block: 8 waves keep 2 blocks per CU
@@ -107,14 +107,17 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
   const bool two = a.B > 16;
   if constexpr (EPI == EPI_RESADD) {
     if (a.attn.part) {  // o_proj reading the attention partials (B <= 16)
-      // one merged element per thread (B * K / 8 <= the NW = 16 launch's 1024 threads): the
-      // partials load before the first weight batch
+      // up to two merged elements per thread (B * K / 8 <= 2 x the NW = 16 launch's 1024
+      // threads: B <= 4 at K 4096): the partials load before the first weight batch
+      // (B=4 o_proj 12.5 us with PRO_ATTN, whose partial loads queue behind the weight batch)
       static const bool no_pre = getenv("MTTS_NO_PRELOAD") && atoi(getenv("MTTS_NO_PRELOAD"));
       const int rows = n_tiles * RT * 16;
       const int nw = (a.force_nw == 4 || a.force_nw == 8 || a.force_nw == 16)
                          ? a.force_nw : (a.KT < 64 ? 4 : ((rows >= 8192 || a.KT < 128) ? 8 : 16));  // = launch_nw's
       if (!no_pre && a.B * a.K / 8 <= nw * 64)
         launch_nw<1, RT, EPI, PRO_ATTN_PRE>(a, n_tiles, s);
+      else if (!no_pre && a.B * a.K / 8 <= 2 * nw * 64)  // two elements per thread
+        launch_nw<1, RT, EPI, PRO_ATTN_PRE2>(a, n_tiles, s);
       else
         launch_nw<1, RT, EPI, PRO_ATTN>(a, n_tiles, s);
       return;

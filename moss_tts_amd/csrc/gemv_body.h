@@ -23,7 +23,7 @@ template <int NB, int RT, int EPI, int PRO0, int NW, bool PIPE, class Wait, bool
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
   constexpr bool PRER = PRO0 == PRO_NORM_PREROW;  // the same, one row per load (K / 8 == threads)
   constexpr bool PREL = PRO0 == PRO_NORM_PRE || PRER;  // norm prologue inputs loaded before the weights
-  constexpr bool PREA = PRO0 == PRO_ATTN_PRE;  // attention partials (2 splits) loaded before the weights
+  constexpr bool PREA = PRO0 == PRO_ATTN_PRE || PRO0 == PRO_ATTN_PRE2;  // attention partials (2 splits) loaded before the weights
   constexpr int PRO = PREL ? PRO_NORM : (PREA ? PRO_ATTN : PRO0);
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
   // bytes in flight per wave for more resident waves (the default for 17-32 rows)
@@ -113,34 +113,40 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       }
     }
   }
-  // PREA: this thread's element of the attention output -- (m, l) of its head and 8 dims of o --
-  // for splits 0 and 1, loaded now (a third and later split, contexts > 512, load after)
-  float4 pa_o[2][2];
-  float2 pa_ml[2];
-  int pa_h = 0, pa_d0 = 0, pa_kvh = 0, pa_hg = 0, pa_b = 0;
+  // PREA: this thread's elements (up to PA_E: threadIdx.x + e * NW * 64) of the attention output
+  // -- (m, l) of its head and 8 dims of o -- for splits 0 and 1, loaded now (a third and later
+  // split, contexts > 512, load after)
+  constexpr int PA_E = PRO0 == PRO_ATTN_PRE2 ? 2 : 1;
+  float4 pa_o[PA_E][2][2];
+  float2 pa_ml[PA_E][2];
+  int pa_d0[PA_E], pa_kvh[PA_E], pa_hg[PA_E], pa_b[PA_E];
   if constexpr (PREA) {
     constexpr uint32_t OOB = 0x7ffffff0u;
     const AttnPartView& v = a.attn;
     const int G = v.G, D = v.D, PS = G * (D + 2);
-    const int i = threadIdx.x;
     const int K8a = KT * 4;
-    pa_b = i / K8a;
-    const int k0 = (i - pa_b * K8a) * 8;
-    pa_h = k0 / D; pa_d0 = k0 - pa_h * D; pa_kvh = pa_h / G; pa_hg = pa_h - pa_kvh * G;
-    const bool ok = i < a.B * K8a;
     const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<float*>(v.part), 0, (int)((size_t)a.B * v.Hkv * v.ns * PS * 4), 0x00020000);
-    const uint32_t base = (uint32_t)(((pa_b * v.Hkv + pa_kvh) * v.ns) * PS) * 4u;
 #pragma unroll
-    for (int s2 = 0; s2 < 2; ++s2) {
-      const bool sok = ok && s2 < v.ns;
-      const uint32_t so = base + (uint32_t)(s2 * PS) * 4u;
-      const auto m = __builtin_amdgcn_raw_buffer_load_b64(prs, sok ? so + (uint32_t)(G * D + 2 * pa_hg) * 4u : OOB, 0, 0);
-      const u32x4 o0 = __builtin_amdgcn_raw_buffer_load_b128(prs, sok ? so + (uint32_t)(pa_hg * D + pa_d0) * 4u : OOB, 0, 0);
-      const u32x4 o1 = __builtin_amdgcn_raw_buffer_load_b128(prs, sok ? so + (uint32_t)(pa_hg * D + pa_d0 + 4) * 4u : OOB, 0, 0);
-      pa_ml[s2] = make_float2(__uint_as_float(m[0]), __uint_as_float(m[1]));
-      pa_o[s2][0] = make_float4(__uint_as_float(o0[0]), __uint_as_float(o0[1]), __uint_as_float(o0[2]), __uint_as_float(o0[3]));
-      pa_o[s2][1] = make_float4(__uint_as_float(o1[0]), __uint_as_float(o1[1]), __uint_as_float(o1[2]), __uint_as_float(o1[3]));
+    for (int e = 0; e < PA_E; ++e) {
+      const int i = threadIdx.x + e * NW * 64;
+      pa_b[e] = i / K8a;
+      const int k0 = (i - pa_b[e] * K8a) * 8;
+      const int h = k0 / D;
+      pa_d0[e] = k0 - h * D; pa_kvh[e] = h / G; pa_hg[e] = h - pa_kvh[e] * G;
+      const bool ok = i < a.B * K8a;
+      const uint32_t base = (uint32_t)(((pa_b[e] * v.Hkv + pa_kvh[e]) * v.ns) * PS) * 4u;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const bool sok = ok && s2 < v.ns;
+        const uint32_t so = base + (uint32_t)(s2 * PS) * 4u;
+        const auto m = __builtin_amdgcn_raw_buffer_load_b64(prs, sok ? so + (uint32_t)(G * D + 2 * pa_hg[e]) * 4u : OOB, 0, 0);
+        const u32x4 o0 = __builtin_amdgcn_raw_buffer_load_b128(prs, sok ? so + (uint32_t)(pa_hg[e] * D + pa_d0[e]) * 4u : OOB, 0, 0);
+        const u32x4 o1 = __builtin_amdgcn_raw_buffer_load_b128(prs, sok ? so + (uint32_t)(pa_hg[e] * D + pa_d0[e] + 4) * 4u : OOB, 0, 0);
+        pa_ml[e][s2] = make_float2(__uint_as_float(m[0]), __uint_as_float(m[1]));
+        pa_o[e][s2][0] = make_float4(__uint_as_float(o0[0]), __uint_as_float(o0[1]), __uint_as_float(o0[2]), __uint_as_float(o0[3]));
+        pa_o[e][s2][1] = make_float4(__uint_as_float(o1[0]), __uint_as_float(o1[1]), __uint_as_float(o1[2]), __uint_as_float(o1[3]));
+      }
     }
   }
   // all weight loads of the first k-batch go out before the (latency-bound) norm prologue
@@ -223,27 +229,30 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     const AttnPartView& v = a.attn;
     const int nact = *v.pos / v.kb + 1;
     const int G = v.G, D = v.D, PS = G * (D + 2);
-    const int i = threadIdx.x;
-    if (nact > v.po_max) {  // long context: the attention merged its splits into x (bf16 rows)
-      if (i < a.B * K8) {
+#pragma unroll
+    for (int e = 0; e < PA_E; ++e) {
+      const int i = threadIdx.x + e * NW * 64;
+      if (i >= a.B * K8) continue;
+      if (nact > v.po_max) {  // long context: the attention merged its splits into x (bf16 rows)
         const int b = i / K8, c = i - b * K8;
         xs_dyn[i] = reinterpret_cast<const u32x4*>(a.x + (size_t)b * a.ldx)[c];
+        continue;
       }
-    } else if (i < a.B * K8) {
-      const float* pp = v.part + ((size_t)pa_b * v.Hkv + pa_kvh) * v.ns * PS;
+      const float* pp = v.part + ((size_t)pa_b[e] * v.Hkv + pa_kvh[e]) * v.ns * PS;
+      const int hg = pa_hg[e], d0 = pa_d0[e];
       float M = -INFINITY;
-      for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, s2 < 2 ? pa_ml[s2 & 1].x : pp[(size_t)s2 * PS + G * D + 2 * pa_hg]);
+      for (int s2 = 0; s2 < nact; ++s2) M = fmaxf(M, s2 < 2 ? pa_ml[e][s2 & 1].x : pp[(size_t)s2 * PS + G * D + 2 * hg]);
       float L = 0.f, o[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       for (int s2 = 0; s2 < nact; ++s2) {
         float ms, ls;
         float4 o0, o1;
         if (s2 < 2) {
-          ms = pa_ml[s2 & 1].x; ls = pa_ml[s2 & 1].y; o0 = pa_o[s2 & 1][0]; o1 = pa_o[s2 & 1][1];
+          ms = pa_ml[e][s2 & 1].x; ls = pa_ml[e][s2 & 1].y; o0 = pa_o[e][s2 & 1][0]; o1 = pa_o[e][s2 & 1][1];
         } else {
           const float* q = pp + (size_t)s2 * PS;
-          ms = q[G * D + 2 * pa_hg]; ls = q[G * D + 2 * pa_hg + 1];
-          o0 = *reinterpret_cast<const float4*>(q + pa_hg * D + pa_d0);
-          o1 = *reinterpret_cast<const float4*>(q + pa_hg * D + pa_d0 + 4);
+          ms = q[G * D + 2 * hg]; ls = q[G * D + 2 * hg + 1];
+          o0 = *reinterpret_cast<const float4*>(q + hg * D + d0);
+          o1 = *reinterpret_cast<const float4*>(q + hg * D + d0 + 4);
         }
         const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
         L += f * ls;

@@ -11,10 +11,11 @@ enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 // PRO_NORM_PRE: PRO_NORM whose inputs fit one register load per thread ((B+1)*K <= 8192,
 // K <= 4096), loaded before the first weight batch (gemv_body.h)
 // PRO_ATTN_PRE: PRO_ATTN with one merged element per thread (B*Hq*D/8 <= threads) whose first
-// two splits' partials load before the first weight batch
+// two splits' partials load before the first weight batch; PRO_ATTN_PRE2: two per thread
 // PRO_NORM_PREROW: PRO_NORM_PRE for K / 8 == threads (K 4096 at 8 waves): chunk j of a thread
 // is row j (the norm weight after the B rows), one load each, B <= 5
-enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2, PRO_NORM_PRE = 3, PRO_ATTN_PRE = 4, PRO_NORM_PREROW = 5 };
+enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2, PRO_NORM_PRE = 3, PRO_ATTN_PRE = 4, PRO_NORM_PREROW = 5,
+           PRO_ATTN_PRE2 = 6 };
 constexpr int PREROW_MAXB = 5;
 // (B <= 8: the sums of squares of row b load in wave b % NW, two rows per wave at NW = 4)
 inline bool norm_preload_fits(int B, int K) { return B <= 8 && (size_t)(B + 1) * K <= 8192 && K <= 4096; }
