@@ -60,11 +60,12 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
 // ---------------------------------------------------------------------------
 template <int NB, int RT, int EPI, int PRO>
 static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
-  constexpr bool NORM = PRO == PRO_NORM || PRO == PRO_NORM_PRE || PRO == PRO_NORM_PREROW;
+  constexpr bool NORM = PRO == PRO_NORM || PRO == PRO_NORM_PRE || PRO == PRO_NORM_PREROW || PRO == PRO_NORM_DMA;
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
   const int rows = n_tiles * RT * 16;
-  const size_t lds = NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN || PRO == PRO_ATTN_PRE || PRO == PRO_ATTN_PRE2 ? (size_t)a.B * a.K * 2 : 0);
+  const size_t lds = PRO == PRO_NORM_DMA ? norm_dma_lds_bytes(a.B, a.K, a.n_ss)
+                     : NORM ? norm_lds_bytes(a.B, a.K) : (PRO == PRO_ATTN || PRO == PRO_ATTN_PRE || PRO == PRO_ATTN_PRE2 ? (size_t)a.B * a.K * 2 : 0);
   // 17-32 rows (NB = 2): 4 waves of 4-deep batches (in-context B=32 sweep: 5.62 vs 6.03 ms/step)
   int nw = a.force_nw;
   // fused-norm launches stage (B+1)*K*2 bytes of LDS per block: 8 waves keep 2 blocks per CU
@@ -127,11 +128,15 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // batch-1 decode (q|k|v, gate|up at K 4096): the norm prologue's inputs load before the first
   // weight batch (B=1 3.285 -> 3.216 ms/step; MTTS_NO_PRELOAD=1 for A/B)
   static const bool no_pre = getenv("MTTS_NO_PRELOAD") && atoi(getenv("MTTS_NO_PRELOAD"));
+  static const bool no_dma = getenv("MTTS_NO_NORM_DMA") && atoi(getenv("MTTS_NO_NORM_DMA"));  // A/B
   if (two) norm ? launch_nw<2, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<2, RT, EPI, PRO_NONE>(a, n_tiles, s);
   else if (norm && !no_pre && a.B <= PREROW_MAXB && a.K == 4096 && (a.force_nw == 0 || a.force_nw == 8) &&
            norm_lds_bytes(a.B, a.K) <= NORM_LDS_MAX)  // launch_nw gives fused-norm launches 8 waves: K/8 == 512 threads
     launch_nw<1, RT, EPI, PRO_NORM_PREROW>(a, n_tiles, s);
   else if (norm && !no_pre && norm_preload_fits(a.B, a.K)) launch_nw<1, RT, EPI, PRO_NORM_PRE>(a, n_tiles, s);
+  else if (norm && !no_pre && !no_dma && a.ldx == a.K && a.ld_ss == a.n_ss &&
+           norm_dma_lds_bytes(a.B, a.K, a.n_ss) <= NORM_LDS_MAX)  // contiguous rows: LDS-DMA staging
+    launch_nw<1, RT, EPI, PRO_NORM_DMA>(a, n_tiles, s);
   else norm ? launch_nw<1, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<1, RT, EPI, PRO_NONE>(a, n_tiles, s);
 }
 

@@ -23,8 +23,9 @@ template <int NB, int RT, int EPI, int PRO0, int NW, bool PIPE, class Wait, bool
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
   constexpr bool PRER = PRO0 == PRO_NORM_PREROW;  // the same, one row per load (K / 8 == threads)
   constexpr bool PREL = PRO0 == PRO_NORM_PRE || PRER;  // norm prologue inputs loaded before the weights
+  constexpr bool DMAN = PRO0 == PRO_NORM_DMA;  // the same inputs by LDS-DMA (no registers)
   constexpr bool PREA = PRO0 == PRO_ATTN_PRE || PRO0 == PRO_ATTN_PRE2;  // attention partials (2 splits) loaded before the weights
-  constexpr int PRO = PREL ? PRO_NORM : (PREA ? PRO_ATTN : PRO0);
+  constexpr int PRO = (PREL || DMAN) ? PRO_NORM : (PREA ? PRO_ATTN : PRO0);
   // k-tiles per load batch (one batch in flight per wave); the 4-deep variant (PIPE) trades
   // bytes in flight per wave for more resident waves (the default for 17-32 rows)
   constexpr int U = PIPE ? 4 : 8;
@@ -113,6 +114,29 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       }
     }
   }
+  extern __shared__ u32x4 xs_dyn[];
+  if constexpr (DMAN) {
+    // x rows then the norm weight (one contiguous LDS run of (B+1)*K8 chunks), then the B rows'
+    // sums of squares; 64 16-byte chunks per wave-instruction, out-of-range chunks read zero
+    typedef __attribute__((address_space(3))) void lvoid;
+    const int K8d = KT * 4, nx = a.B * K8d, nxs = nx + K8d;
+    const int cx = (nxs + 63) / 64 * 64, ns4 = a.B * a.n_ss / 4;
+    const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0, nx * 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t nrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.nw), 0, K8d * 16, 0x00020000);
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(a.ss_in), 0, ns4 * 16, 0x00020000);
+    for (int c0 = wave * 64; c0 < cx; c0 += NW * 64) {
+      const int i = c0 + lane;
+      if (c0 + 64 <= nx)  // wave-uniform branches: whole instructions from one source
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lvoid*)(xs_dyn + c0), 16, (uint32_t)i * 16u, 0, 0, 0);
+      else if (c0 >= nx)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(nrs, (lvoid*)(xs_dyn + c0), 16, (uint32_t)(i - nx) * 16u, 0, 0, 0);
+      else  // straddles the x / weight boundary: x lanes, then weight lanes (both OOB-zeroed)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(i < nx ? xrs : nrs, (lvoid*)(xs_dyn + c0), 16,
+                                                 (uint32_t)(i < nx ? i : i - nx) * 16u, 0, 0, 0);
+    }
+    for (int c0 = wave * 64; c0 < ns4; c0 += NW * 64)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(srs, (lvoid*)(xs_dyn + cx + c0), 16, (uint32_t)(c0 + lane) * 16u, 0, 0, 0);
+  }
   // PREA: this thread's elements (up to PA_E: threadIdx.x + e * NW * 64) of the attention output
   // -- (m, l) of its head and 8 dims of o -- for splits 0 and 1, loaded now (a third and later
   // split, contexts > 512, load after)
@@ -164,7 +188,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
         wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)min(k + u, kt1 - 1) * 64);
   };
   // the preloads must be ISSUED first: stop the scheduler from hoisting the weight loads above them
-  if constexpr (PREL || PREA) __builtin_amdgcn_sched_barrier(0);
+  if constexpr (PREL || PREA || DMAN) __builtin_amdgcn_sched_barrier(0);
   // unconditional (a wave with an empty K range re-reads its row's last tile, in bounds): a load
   // issue under a branch makes the compiler wait for the preloads with everything else at the
   // join (B=4 also 3.56 -> 3.53 ms/step)
@@ -178,7 +202,6 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   //   PRO_ATTN:  the decode attention output, merged here from its per-split (m, l, o)
   //              partials in split order: x = bf16(sum_s f_s o_s / sum_s f_s l_s),
   //              f_s = exp(m_s - max m) -- the cross-block combine of attn_decode
-  extern __shared__ u32x4 xs_dyn[];
   const int K8 = KT * 4;  // 16-byte chunks per row
   if constexpr (PRO == PRO_NORM) {
     __shared__ float r_s[32];
@@ -201,6 +224,17 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
         const float ss = wave_sum((__uint_as_float(sr[m][0]) + __uint_as_float(sr[m][1])) +
                                   (__uint_as_float(sr[m][2]) + __uint_as_float(sr[m][3])));
         if (b < a.B && lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
+      }
+    } else if constexpr (DMAN) {
+      // the DMA loads were issued before this wave's U*RT weight loads: in-order vmcnt
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U * RT) : "memory");
+      __syncthreads();  // every wave's chunks have landed
+      const float* ssl = reinterpret_cast<const float*>(xs_dyn + (n8x + K8 + 63) / 64 * 64);
+      for (int b = wave; b < a.B; b += NW) {
+        float ss = 0.f;
+        for (int t = lane; t < a.n_ss; t += 64) ss += ssl[b * a.n_ss + t];
+        ss = wave_sum(ss);
+        if (lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
       }
     } else {
     for (int i = threadIdx.x; i < n8x + K8; i += NW * 64) {

@@ -14,8 +14,16 @@ enum Epi { EPI_STORE = 0, EPI_RESADD = 1, EPI_SWIGLU = 2, EPI_LOGITS = 3 };
 // two splits' partials load before the first weight batch; PRO_ATTN_PRE2: two per thread
 // PRO_NORM_PREROW: PRO_NORM_PRE for K / 8 == threads (K 4096 at 8 waves): chunk j of a thread
 // is row j (the norm weight after the B rows), one load each, B <= 5
+// PRO_NORM_DMA: PRO_NORM whose inputs (x rows, norm weight, sums of squares; contiguous rows)
+// go straight to LDS by LDS-DMA before the first weight batch (any B <= 16 whose staging fits)
 enum Pro { PRO_NONE = 0, PRO_NORM = 1, PRO_ATTN = 2, PRO_NORM_PRE = 3, PRO_ATTN_PRE = 4, PRO_NORM_PREROW = 5,
-           PRO_ATTN_PRE2 = 6 };
+           PRO_ATTN_PRE2 = 6, PRO_NORM_DMA = 7 };
+// LDS of the PRO_NORM_DMA prologue: (B+1)*K bf16 + B*n_ss fp32, each region padded to whole
+// 64-chunk (1 KiB) DMA wave-instructions
+inline size_t norm_dma_lds_bytes(int B, int K, int n_ss) {
+  const size_t cx = ((size_t)(B + 1) * K / 8 + 63) / 64 * 64, cs = ((size_t)B * n_ss / 4 + 63) / 64 * 64;
+  return (cx + cs) * 16;
+}
 constexpr int PREROW_MAXB = 5;
 // (B <= 8: the sums of squares of row b load in wave b % NW, two rows per wave at NW = 4)
 inline bool norm_preload_fits(int B, int K) { return B <= 8 && (size_t)(B + 1) * K <= 8192 && K <= 4096; }
