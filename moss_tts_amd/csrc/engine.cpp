@@ -493,7 +493,8 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       return 0;
     }
   }
-  const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn;
+  const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn &&
+                         !st.attn_direct;
   // short contexts: attention + o_proj + residual in one launch (ao.hip); its blocks re-read
   // their KV head from L2 once per o_proj row chunk, so long contexts keep the split form
   const bool use_ao = S == 1 && e->ao && st.ao_part && st.cos_t && st.Cmax <= AO_MAX_CTX &&

@@ -50,6 +50,8 @@ struct Stack {
   int* ao_cnt = nullptr;
   int* qsync = nullptr;     // 16 counter words of the q|k|v + attention launch (qa.hip; zero between launches)
   int rows = 0;             // row capacity of xn / attnb / act (>= 32: 17-32 row decode may use the packed layout)
+  bool attn_direct = false; // the context never spans two attention blocks: the attention writes its
+                            // rows directly and o_proj is a plain GEMV (no split partials to merge)
 };
 
 constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip

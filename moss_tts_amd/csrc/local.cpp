@@ -57,6 +57,10 @@ static Stack local_stack(mtts_engine* e) {
   st.mask = p.mask;
   st.h = p.h; st.xn = p.xn; st.qkvb = p.qkvb; st.qb = nullptr; st.attnb = p.attnb; st.act = p.act;
   st.ss = p.ss; st.part = p.part; st.att_cnt = p.att_cnt; st.fsync = p.fsync;
+  // <= 33 channel positions: one attention block per head, so it writes its rows itself and
+  // the depth o_proj reads them as a plain GEMV (no partial merge in its prologue)
+  static const bool no_direct = getenv("MTTS_LOCAL_ATTN_MERGE") && getenv("MTTS_LOCAL_ATTN_MERGE")[0] == '1';
+  st.attn_direct = !no_direct && LOCAL_CMAX <= attn_decode_keys_per_block();
   return st;
 }
 
