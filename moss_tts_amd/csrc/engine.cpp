@@ -163,6 +163,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
+  if (const char* v = getenv("MTTS_U")) sscanf(v, "%d,%d,%d,%d,%d", &e->nu[0], &e->nu[1], &e->nu[2], &e->nu[3], &e->nu[4]);
   auto bail = [&](int rc) {
     mtts_engine_destroy(e);
     return rc;
@@ -518,7 +519,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     bf16_t* vc = st.vc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     GemvArgs g = gemv_args(w.qkv, st.xn, H, st.qkvb, st.qkv_rows, M, st.qkv_rows, H);
     if (int rc = normed_input(e, st, g, w.in_norm, M, s, ntiles)) return rc;
-    g.force_nw = e->nw[0];
+    g.force_nw = e->nw[0]; g.force_u = e->nu[0];
     DecAttnArgs da{};
     da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
     da.kc = kc; da.vc = vc; da.mask = st.mask + (size_t)b0 * st.Cmax; da.pos = pos_base; da.out = st.attnb;
@@ -574,7 +575,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     }
     if (!(S == 1 && fused_ao) && !use_ao) {
       g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
-      g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1];
+      g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1]; g.force_u = e->nu[1];
       g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
       if (fuse_attn) {
         g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
@@ -585,11 +586,11 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     }
     g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
     if (int rc = normed_input(e, st, g, w.post_norm, M, s, ntiles)) return rc;
-    g.force_nw = e->nw[2];
+    g.force_nw = e->nw[2]; g.force_u = e->nu[2];
     g.y_packed = ntiles ? 1 : 0;
     HIPCHK(proj(e, g, EPI_SWIGLU, s));
     g = gemv_args(w.down, st.act, I, st.h, H, M, H, I);
-    g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3];
+    g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3]; g.force_u = e->nu[3];
     g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
     HIPCHK(proj(e, g, EPI_RESADD, s));
   }
@@ -624,7 +625,7 @@ int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const
                       e->final_norm, e->xn, B, H, eps, s));
   }
   g.pad_start = c.vocab; g.pad_period = e->audio_rows; g.pad_off = e->audio_rows - 1;
-  g.force_nw = e->nw[4];
+  g.force_nw = e->nw[4]; g.force_u = e->nu[4];
   if (text_gate && e->text_tile_lo > 0) {
     // decode: text rows below the special ids only when some row samples text freely.
     // Audio-mode rows see every text logit except gen_slot / delay_slot masked to -inf
@@ -974,11 +975,25 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
   // the kernel instance the decode step launches: q|k|v and gate|up read RMSNorm(h) through
   // the same normed_input choice (fused prologue for small batches), the rest plain
   const Stack st = backbone_stack(e);
+  // 17-32 rows: the decode step's packed-activation instances (xpk_index inputs / SwiGLU output);
+  // the standalone RMSNorm runs once before the timed launches
+  const bool pk = B > 16 && B <= 32 && e->xpack && which != 4;
+  if (pk && (which == 0 || which == 2)) {
+    GemvArgs g0 = gemv_args(W, e->xn, H, y, ldy, B, N, H);
+    if (int rc = normed_input(e, st, g0, which == 0 ? w.in_norm : w.post_norm, B, s, 2)) return rc;
+  }
   auto launch = [&](const bf16_t* Wi) -> int {
+    if (pk) {
+      GemvArgs g = gemv_args(Wi, x, ldx, y, ldy, B, N, K);
+      g.res = res; g.ldres = ldres; g.x_packed = 1; g.y_packed = which == 2 ? 1 : 0;
+      g.force_nw = e->nw[which]; g.force_u = e->nu[which];
+      HIPCHK(gemv_ex(g, epi, s));
+      return 0;
+    }
     if (which == 0 || which == 2) {
       GemvArgs g = gemv_args(Wi, e->xn, H, y, ldy, B, N, H);
       if (int rc = normed_input(e, st, g, which == 0 ? w.in_norm : w.post_norm, B, s)) return rc;
-      g.force_nw = e->nw[which];
+      g.force_nw = e->nw[which]; g.force_u = e->nu[which];
       HIPCHK(gemv_ex(g, epi, s));
       return 0;
     }

@@ -129,6 +129,7 @@ struct mtts_engine {
   bool cap_mode = false;
   bool unfused_norm = false;  // MTTS_UNFUSED_NORM=1: always run the separate RMSNorm kernel (A/B timing)
   int nw[5] = {0, 0, 0, 0, 0};  // waves-per-block overrides (MTTS_NW="qkv,o,gu,down,heads"; 0 = auto)
+  int nu[5] = {0, 0, 0, 0, 0};  // load-batch depth overrides (MTTS_U="qkv,o,gu,down,heads"; 0 = auto, 4 / 8)
   bf16_t* staging = nullptr;
   size_t staging_bytes = 0;
   uint64_t step_weight_bytes = 0;

@@ -75,7 +75,9 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
     nw = a.KT < 64 ? 4 : (NB == 2 ? (a.x_packed ? 8 : 4) : ((rows >= 8192 || a.KT < 128 || NORM) ? 8 : 16));
   // MTTS_GEMV_PIPE bit 0 / bit 1 flips the batch depth (8 <-> 4 k-tiles) for <= 16 / > 16 rows
   static const int pipe = getenv("MTTS_GEMV_PIPE") ? atoi(getenv("MTTS_GEMV_PIPE")) : 0;
-  if ((NB == 1 && (pipe & 1)) || (NB == 2 && !(pipe & 2))) {
+  bool u4 = (NB == 1 && (pipe & 1)) || (NB == 2 && !(pipe & 2));
+  if (a.force_u == 4 || a.force_u == 8) u4 = a.force_u == 4;
+  if (u4) {
     if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
     if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8, true>), dim3(n_tiles), dim3(512), lds, s, a);
     if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16, true>), dim3(n_tiles), dim3(1024), lds, s, a);

@@ -3,6 +3,10 @@
 #pragma once
 #include "kernels.h"
 
+#ifndef GEMV_PROBE
+#define GEMV_PROBE 0
+#endif
+
 namespace mtts {
 
 // bf16(nw * bf16(x * r)) for 8 packed elements (Qwen3RMSNorm rounding points)
@@ -173,6 +177,27 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       }
     }
   }
+  // EPI_RESADD: the residual elements this thread adds in the epilogue, loaded now (issued before
+  // the weights, so the epilogue's wait finds them landed; loaded there, they were one more
+  // dependent L2-miss round trip after the reduction).  Thread t < 256 owns element t of each
+  // output tile (see the epilogue's index map); out-of-range elements read zero.
+  constexpr int OTR = EPI == EPI_RESADD ? RT : 1;
+  constexpr int NBR = EPI == EPI_RESADD ? NB : 1;
+  uint16_t resv[OTR][NBR];
+  if constexpr (EPI == EPI_RESADD) {
+    constexpr uint32_t OOB = 0x7ffffff0u;
+    const int t = threadIdx.x, ln = t >> 2, nl = ((ln >> 4) << 2) + (t & 3);
+    const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16_t*>(a.res), 0, (int)(((size_t)(a.B - 1) * a.ldres + a.N) * 2), 0x00020000);
+#pragma unroll
+    for (int ot = 0; ot < OTR; ++ot)
+#pragma unroll
+      for (int nb = 0; nb < NBR; ++nb) {
+        const int n = (bt * OTR + ot) * 16 + nl, b = (ln & 15) + 16 * nb;
+        const bool ok = t < 256 && b < a.B && n < a.N;
+        resv[ot][nb] = __builtin_amdgcn_raw_buffer_load_b16(rrs, ok ? (uint32_t)(b * a.ldres + n) * 2u : OOB, 0, 0);
+      }
+  }
   // all weight loads of the first k-batch go out before the (latency-bound) norm prologue
   int kt = kt0;
   u32x4 wa[RT][U];
@@ -185,10 +210,14 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int r = 0; r < RT; ++r)
+#if GEMV_PROBE == 2  // timing probe build: no weight loads
+        wa[r][u] = (u32x4){(uint32_t)(k + u), (uint32_t)lane, 0u, 0u};
+#else
         wa[r][u] = __builtin_nontemporal_load(wbase[r] + (size_t)min(k + u, kt1 - 1) * 64);
+#endif
   };
   // the preloads must be ISSUED first: stop the scheduler from hoisting the weight loads above them
-  if constexpr (PREL || PREA || DMAN) __builtin_amdgcn_sched_barrier(0);
+  if constexpr (PREL || PREA || DMAN || EPI == EPI_RESADD) __builtin_amdgcn_sched_barrier(0);
   // unconditional (a wave with an empty K range re-reads its row's last tile, in bounds): a load
   // issue under a branch makes the compiler wait for the preloads with everything else at the
   // join (B=4 also 3.56 -> 3.53 ms/step)
@@ -341,7 +370,11 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
     }
     // unconditional global load: a "load or zero" select would branch and wait on every load
     // (cdna_hip_programming.md trap (c)); token columns >= B read row 0 and are never stored
+#if GEMV_PROBE == 1  // timing probe build: no x loads
+    return (u32x4){(uint32_t)k, (uint32_t)nb, (uint32_t)lane, 0u};
+#else
     return xbase[nb][k * xs];
+#endif
   };
 
   auto compute = [&](u32x4 (&w)[RT][U], int k) {
@@ -409,7 +442,7 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
           if (n >= a.pad_start && ((n - a.pad_start) % a.pad_period) == a.pad_off) out = 0xFF80;  // -inf
         } else if constexpr (EPI == EPI_RESADD) {
           // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
-          if (b < a.B && n < a.N) out = f2bf(bf2f(a.res[(size_t)b * a.ldres + n]) + rbf(vo));
+          if (b < a.B && n < a.N) out = f2bf(bf2f(resv[ot][nb]) + rbf(vo));
           const float ho = bf2f(out);
           sq[ot][nb][bl][nl] = ho * ho;
         } else {  // EPI_SWIGLU: bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)

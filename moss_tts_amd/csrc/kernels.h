@@ -61,6 +61,7 @@ struct GemvArgs {
   float* ss_out;       // [B, ld_ss_out] (nullptr: skip)
   int ld_ss_out;
   int force_nw;        // 0: automatic waves-per-block choice; 4/8/16: forced (tuning)
+  int force_u;         // 0: automatic load-batch depth; 4/8 k-tiles per batch: forced (tuning)
   int tile0;           // first output row tile of this launch (row ranges of one matrix)
   const int* gate;     // device flag: the launch does nothing when *gate == 0 (nullptr: always on)
   int n_row_tiles;     // packed 16-row weight tiles (set by the GEMM launcher)

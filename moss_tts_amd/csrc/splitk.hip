@@ -39,6 +39,15 @@ __global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int
   const int b = lane & 15;
   const bool xok = b < a.B;
   const u32x4* xbase = reinterpret_cast<const u32x4*>(a.x + (size_t)(xok ? b : 0) * a.ldx + (lane >> 4) * 8);
+  // the residual element this thread adds if its workgroup arrives last, loaded before the
+  // weights (in the last arrival's epilogue it was one more dependent round trip)
+  const int ln = t >> 2, nl = ((ln >> 4) << 2) + (t & 3), bl = ln & 15;
+  const int n = bt * 16 + nl;
+  const bool rok = t < 256 && bl < a.B && n < a.N;
+  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16_t*>(a.res), 0, (int)(((size_t)(a.B - 1) * a.ldres + a.N) * 2), 0x00020000);
+  const uint16_t resv = __builtin_amdgcn_raw_buffer_load_b16(rrs, rok ? (uint32_t)(bl * a.ldres + n) * 2u : 0x7ffffff0u, 0, 0);
+  __builtin_amdgcn_sched_barrier(0);
   f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int k = kw0; k < kw1; k += SK_U) {
     u32x4 wv[SK_U], xv[SK_U];
@@ -84,8 +93,6 @@ __global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int
   // ---- the last arrival: sum the S partials in split order, + residual, sums of squares ----
   if (t < 256) {
     // element t: lane = t/4, reg = t%4 -> row n = ((lane>>4)*4 + reg), b = lane & 15
-    const int ln = t >> 2, nl = ((ln >> 4) << 2) + (t & 3), bl = ln & 15;
-    const int n = bt * 16 + nl;
     // sc1 (device-scope) buffer loads (aux 16), all S in flight (atomic loads went one at a time)
     const __amdgpu_buffer_rsrc_t prs =
         __builtin_amdgcn_make_buffer_rsrc(part + (size_t)bt * S * 256, 0, S * 256 * 4, 0x00020000);
@@ -99,9 +106,9 @@ __global__ __launch_bounds__(SK_NW * 64) void gemv_splitk_kernel(GemvArgs a, int
     for (int j = 0; j < SK_MAXS; ++j)
       if (j < S) s += pv[j];
     bf16_t out = 0;
-    if (bl < a.B && n < a.N) {
+    if (rok) {
       // hidden = residual + bf16(o)   (TF/.../modeling_qwen3.py:311,322)
-      out = f2bf(bf2f(a.res[(size_t)bl * a.ldres + n]) + rbf(s));
+      out = f2bf(bf2f(resv) + rbf(s));
       a.y[(size_t)bl * a.ldy + n] = out;
     }
     const float ho = bf2f(out);
