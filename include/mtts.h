@@ -101,6 +101,12 @@ int mtts_heads_ld(const mtts_engine* eng);
  * batches <= 2 rows), 0 when this engine decodes with one launch per stage (MTTS_MEGA=0, or a
  * shape it does not cover). */
 int mtts_mega_workgroups(const mtts_engine* eng);
+/* 1 when batch-1 decode steps run the decoder stack as one persistent launch with run-ahead
+ * weight streaming (MTTS_PSE=1 at creation, MossTTSDelay-8B shape, 256 CUs), else 0 */
+int mtts_pse_active(const mtts_engine* eng);
+/* per-layer event stamps (s_memrealtime, 100 MHz) of the last persistent streaming launch:
+ * [layers][16][256 workgroups] (engine created with MTTS_PSE_TRACE=1; see pse.hip) */
+int mtts_pse_trace(mtts_engine* eng, uint64_t* host, size_t n);
 /* 1 when a decode step of B rows runs attention + o_proj + residual as one launch per layer
  * (ao.hip: B == 1, head_dim 128, KV capacity <= 2048, engine created with MTTS_AO=1), else 0. */
 int mtts_attn_o_active(const mtts_engine* eng, int B);

@@ -70,6 +70,8 @@ _SIGS = {
     "mtts_forward": (I, [P, P, P, I, I, I, P, P]),
     "mtts_heads_ld": (I, [P]),
     "mtts_mega_workgroups": (I, [P]),
+    "mtts_pse_active": (I, [P]),
+    "mtts_pse_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),
     "mtts_attn_o_active": (I, [P, I]),
     "mtts_qkv_attn_active": (I, [P, I]),
     "mtts_mega_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),

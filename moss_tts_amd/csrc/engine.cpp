@@ -114,6 +114,18 @@ static int alloc_capacity(mtts_engine* e) {
         hipMemset(e->mega_sync, 0, nsync * sizeof(uint32_t)) != hipSuccess)
       return fail(MTTS_E_HIP, "mega state");
     e->mega_P = mega_grid(e->device, mega_lds_bytes(MEGA_MAXB, H, Hq * D, I));
+    std::vector<PseLayer> pl(c.layers);
+    for (int l = 0; l < c.layers; ++l) {
+      const LayerW& w = e->L[l];
+      pl[l] = PseLayer{w.qkv, w.o, w.gu, w.down, w.in_norm, w.post_norm, w.q_norm, w.k_norm,
+                       e->kc + l * e->layer_kv, e->vc + l * e->layer_kv};
+    }
+    if ((rc = e->alloc(&e->pse_L, (size_t)c.layers)) || (rc = e->alloc(&e->pse_ws, pse_ws_bytes()))) return rc;
+    if (hipMemcpy(e->pse_L, pl.data(), pl.size() * sizeof(PseLayer), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemset(e->pse_ws, 0, pse_ws_bytes()) != hipSuccess)
+      return fail(MTTS_E_HIP, "pse state");
+    e->pse_ok = pse_supported(e->device, 1, H, Hq, Hkv, D, I, e->qkv_rows, c.max_ctx);
+    if (getenv("MTTS_PSE_TRACE") && (rc = e->alloc(&e->pse_trace, (size_t)c.layers * PSE_TRACE_EV * 256))) return rc;
     if (getenv("MTTS_MEGA_TRACE") && e->mega_P > 0 &&
         (rc = e->alloc(&e->mega_trace, (size_t)c.layers * 5 * e->mega_P * 4)))
       return rc;
@@ -158,6 +170,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
   if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
+  if (const char* v = getenv("MTTS_PSE")) e->pse = v[0] == '1';
   if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
   if (const char* v = getenv("MTTS_QA")) e->qa = v[0] == '1';
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
@@ -237,6 +250,7 @@ extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
   return 0;
 }
 extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
+extern "C" int mtts_pse_active(const mtts_engine* e) { return e && e->pse && e->pse_ok ? 1 : 0; }
 extern "C" int mtts_mega_workgroups(const mtts_engine* e) {
   return e && e->mega && e->c.head_dim == 128 ? e->mega_P : 0;
 }
@@ -251,6 +265,15 @@ extern "C" int mtts_qkv_attn_active(const mtts_engine* e, int B) {
   DecAttnArgs da{};
   da.Hq = e->c.n_heads; da.Hkv = e->c.n_kv; da.D = e->c.head_dim; da.Cmax = e->c.max_ctx;
   return qkv_attn_supported(g, da, B) ? 1 : 0;
+}
+extern "C" int mtts_pse_trace(mtts_engine* e, uint64_t* host, size_t n) {
+  if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
+  if (!e->pse_trace) return fail(MTTS_E_UNSUPPORTED, "engine created without MTTS_PSE_TRACE=1");
+  const size_t have = (size_t)e->c.layers * PSE_TRACE_EV * 256;
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemcpy(host, e->pse_trace, std::min(n, have) * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return 0;
 }
 extern "C" int mtts_mega_trace(mtts_engine* e, uint64_t* host, size_t n) {
   if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
@@ -481,6 +504,18 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   const int M = B * S;
   const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
   const float eps = e->c.rms_eps;
+  if (S == 1 && B == 1 && b0 == 0 && e->pse && e->pse_ok && st.cos_t && st.L == e->L.data()) {
+    // the whole stack as one persistent launch with run-ahead weight streaming (pse.hip)
+    PseArgs pa{};
+    pa.L = e->pse_L; pa.layers = st.layers; pa.h = st.h; pa.ss = st.ss; pa.cos_t = st.cos_t; pa.sin_t = st.sin_t;
+    pa.mask = st.mask; pa.pos = pos_base; pa.Cmax = st.Cmax; pa.eps = e->c.rms_eps;
+    pa.scale = 1.0f / std::sqrt((float)D);
+    pa.trace = e->pse_trace;
+    static const int pse_probe = getenv("MTTS_PSE_PROBE") ? atoi(getenv("MTTS_PSE_PROBE")) : 0;
+    pa.probe = pse_probe;
+    HIPCHK(pse_decode(pa, e->pse_ws, s));
+    return 0;
+  }
   if (S == 1 && B <= MEGA_MAXB && e->mega && e->mega_P > 0 && st.cos_t && st.L == e->L.data() && D == 128) {
     // the whole stack as one persistent launch (mega.hip)
     MegaArgs ma{};
@@ -806,6 +841,15 @@ extern "C" int mtts_generate_poll(mtts_engine* e, int* steps, int* done_step, vo
     if (err) {
       hipMemset(e->mega_sync, 0, mega_sync_words(e->c.layers, e->c.n_kv) * sizeof(uint32_t));
       return fail(MTTS_E_HIP, "persistent decode launch: a stage wait timed out (results invalid)");
+    }
+  }
+  if (e->pse_ws) {  // the persistent streaming launch gave up waiting (pse.hip): the run is invalid
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost));
+    if (err) {
+      hipMemset(e->pse_ws, 0, pse_ws_bytes());
+      return fail(MTTS_E_HIP, "persistent streaming decode: a wait timed out (code " + std::to_string(err) +
+                                  "; results invalid)");
     }
   }
   if (g.topk_overflow)

@@ -113,6 +113,12 @@ struct mtts_engine {
   uint32_t* mega_sync = nullptr; // device, mega_sync_words(layers), zero between launches
   int mega_P = 0;                // workgroups (CUs); 0: unsupported here
   uint64_t* mega_trace = nullptr; // MTTS_MEGA_TRACE=1: per-stage timestamps of the last launch
+  // persistent streaming engine (pse.hip) for the batch-1 decode stack: MTTS_PSE=1 (A/B)
+  bool pse = false;
+  bool pse_ok = false;           // the shape and the device support it
+  PseLayer* pse_L = nullptr;     // device [layers]
+  unsigned char* pse_ws = nullptr;  // pse_ws_bytes(), zero-filled
+  uint64_t* pse_trace = nullptr;    // MTTS_PSE_TRACE=1: per-layer event stamps of the last launch
   // generate state
   GenDev* st = nullptr;
   GenDev hst{};

@@ -298,6 +298,37 @@ int mega_sync_words(int layers, int Hkv);  // zeroed words the launch needs (mul
 int mega_err_word(int layers, int Hkv);    // index of the error word in them
 int mega_grid(int device, size_t lds);  // workgroups per launch (one per CU), 0: unsupported
 hipError_t mega_decode(const MegaArgs& a, int P, hipStream_t s);
+
+// pse.hip: the batch-1 decode stack as one persistent launch with a per-CU LDS-DMA weight ring
+// running ahead of the data-tagged hand-offs (MossTTSDelay-8B shape, 256 CUs)
+struct PseLayer {
+  const bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
+  bf16_t *kc, *vc;  // this layer's caches (row 0)
+};
+struct PseArgs {
+  const PseLayer* L;  // device [layers]
+  int layers;
+  bf16_t* h;          // [H] residual stream: in = the embedding row, out = the stack's output
+  float* ss;          // [H/16] its per-16-column sums of squares (in / out)
+  const bf16_t *cos_t, *sin_t;
+  const uint8_t* mask;  // [Cmax] (row 0)
+  const int* pos;
+  int Cmax;
+  float eps, scale;
+  // workspace (set by pse_decode): granules and words
+  uint64_t *g_qkv, *g_att, *g_h[2], *g_ss[2], *g_act;
+  uint32_t *err, *epoch, *exit_cnt;
+  uint64_t* trace;  // nullptr, or [layers][PSE_TRACE_EV][256] s_memrealtime stamps
+  int probe;        // timing probe (MTTS_PSE_PROBE; results invalid): 1 loader issues no DMA,
+                    // 2 consumers skip the slot reads and MFMAs
+};
+constexpr int PSE_TRACE_EV = 16;
+size_t pse_lds_bytes();
+int pse_grid(int device);
+bool pse_supported(int device, int B, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);
+size_t pse_ws_bytes();  // zero-filled once by the owner
+hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s);
+uint32_t* pse_err_word(void* ws);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);

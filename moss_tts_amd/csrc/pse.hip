@@ -1,0 +1,798 @@
+// Persistent streaming engine (PSE): the batch-1 decode step's decoder stack -- every layer's
+//   input RMSNorm + q|k|v  ->  attention (q/k norm, RoPE, KV append)  ->  o_proj + residual
+//   ->  post-attention RMSNorm + gate|up + SwiGLU  ->  down + residual
+// (TF/models/qwen3/modeling_qwen3.py:294-323, :241-280, :81-83) -- as ONE launch, replacing
+// run_layers' 5 x 36 dependent launches for B = 1 (MossTTSDelay-8B shape).
+//
+// Why: at batch 1 each launch pays a dependent-launch boundary and a grid fill / drain
+// (~1.7 us between streaming kernels, MI355X_MICROARCH.md "boundary"), and the attention chain
+// (~8 us) leaves HBM idle.  Here each CU's weights for the whole step are ONE stream that a
+// loader wave keeps running ahead of every data dependency (MI355X_MICROARCH.md
+// "prefetch-credit", "engine-vs-launches"): while the consumers wait for a hand-off, the ring
+// keeps filling with the next op's weights.
+//
+// Geometry: one 320-thread workgroup per CU (the LDS request keeps it at one; all P = 256
+// resident).  Wave 0 is the LOADER: it streams this CU's weight slices, in op order, into an
+// LDS ring of PSE_NS 16 KiB slots by LDS-DMA (global_load_lds 16 B / lane,
+// non-temporal), and publishes each slot in an LDS FULL counter once its DMA has retired
+// (counted vmcnt).  Waves 1-4 are CONSUMERS: each takes 4 of a slot's 16 packed 1 KiB tiles
+// (v_mfma_f32_16x16x32_bf16, A = the tile from LDS, B = the op's input vector staged in LDS),
+// reports the slot free, and at the end of a row tile the four partial tiles are reduced in LDS
+// in a fixed order (deterministic).
+//
+// Work split per layer (CU c of P = 256): q|k|v = 768 half tiles (row tile, K half), 3 per CU;
+// o_proj and down = row tile c (CU c owns residual columns 16c..16c+15 for the whole step);
+// gate|up = tile pairs 3c..3c+2.  92 slots (1.47 MB) per CU per layer.  The attention of KV
+// head g runs on the consumers of CU pse_att_cu(g) (its loader keeps streaming meanwhile).
+//
+// Hand-offs: data-tagged granules (MI355X_MICROARCH.md "handoff-1to1" / "allgather"): 8 bytes
+// {32-bit payload, 32-bit tag} written by ONE write-through (sc1) store and read with sc1 loads;
+// tag = launch epoch << 8 | layer * 5 + op, so a consumer polls the payload itself (no counters,
+// no fences) and granules of earlier launches / layers never match.  Every spin is bounded: a
+// stuck wait sets the error word, and the launch drains.
+#include "kernels.h"
+
+namespace mtts {
+
+namespace {
+
+constexpr int CW = 4;                   // consumer waves
+constexpr int LW = 2;                   // loader waves (each its own vmcnt: 4 fills = 64 instructions)
+constexpr int THREADS = (LW + CW) * 64;
+#ifndef PSE_NS
+#define PSE_NS 7
+#endif
+#ifndef PSE_FILLS
+#define PSE_FILLS 4
+#endif
+constexpr int NS = PSE_NS;              // ring slots
+constexpr int SLOT_KB = 16;             // 1 KiB tiles per slot
+constexpr int FILLS = PSE_FILLS;        // slot fills the loader keeps in flight (HBM latency under
+                                        // load ~5 us: bytes in flight set the rate)
+constexpr int SPL = 92;                 // slots per layer per CU
+constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
+enum { OP_QKV = 0, OP_ATT = 1, OP_O = 2, OP_GU = 3, OP_DOWN = 4 };
+
+typedef __attribute__((address_space(1))) uint64_t g64;
+typedef __attribute__((address_space(1))) uint32_t g32;
+typedef __attribute__((address_space(3))) void lvoid;
+typedef __attribute__((address_space(1))) void gvoid;
+
+__device__ __forceinline__ void st64(void* p, uint64_t v) {
+  __hip_atomic_store((g64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld32(const void* p) {
+  return __hip_atomic_load((g32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st32(void* p, uint32_t v) {
+  __hip_atomic_store((g32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// trace events (PSE_TRACE_EV per layer): consumers (wave 1) 0 layer start, 1 q|k|v input
+// normed, 2 q|k|v done, 3 attention done (attention CUs), 4 o input, 5 o done, 6 gate|up input
+// normed, 7 gate|up done, 8 down input, 9 down done; loader 10 first q|k|v slot issued, 11 first
+// o slot, 12 first gate|up slot, 13 first down slot, 14 last slot of the layer issued
+#define PSE_STAMP(l, ev)                                                                        \
+  do {                                                                                          \
+    if (a.trace && lane == 0) a.trace[((size_t)(l) * PSE_TRACE_EV + (ev)) * 256 + c] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+// LDS-DMA of 1 KiB (16 B per lane) to the wave-uniform LDS byte address lds_byte, non-temporal.
+// Inline asm so that hipcc does not see an LDS write in flight: for a builtin it drains vmcnt
+// (every fill) before each later LDS access of the loader (cdna_hip_programming.md §5.7); the
+// loader counts its fills itself.
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
+  uint32_t keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds_byte)
+               : "memory");
+}
+__device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
+__device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
+
+// LDS words shared by the loader and the consumers
+struct Ctl {
+  int full[LW];   // per loader wave k: its slots (k, k + LW, ...) whose DMA has retired
+  int freed[CW];  // slots each consumer wave has finished reading
+  int bar;        // consumer-only barrier counter (monotonic)
+  int abort;      // a wait gave up: everyone drains
+  int pad;
+  uint64_t lstamp[2][5];  // loader trace events of the last two layers (copied out by the consumers)
+};
+
+constexpr uint32_t SPIN_LDS = 1u << 22;  // LDS polls (~40 ns each): ~0.2 s
+constexpr uint32_t SPIN_MEM = 1u << 18;  // granule sweeps (~1-2 us each): ~0.3-0.5 s
+
+// LDS layout (bytes)
+constexpr int L_CTL = 0;
+constexpr int L_RING = 256;
+constexpr int L_XS = L_RING + NS * SLOT_KB * 1024;  // op input: 12288 bf16
+constexpr int L_RED = L_XS + I_ * 2;                // [CW][2][256] fp32 partial tiles
+constexpr int L_MISC = L_RED + CW * 2 * 256 * 4;    // [256] gathered sums of squares
+constexpr int PSE_MAXL = 64;                        // layers (weight pointer table in LDS)
+constexpr int L_PTR = L_MISC + 1024;
+constexpr int L_END = L_PTR + PSE_MAXL * 4 * 8;
+// the attention CUs' scratch overlays the op input (q|k|v's input is dead once its slots are
+// consumed; o_proj's gather rewrites it after the attention): gathered q|k|v halves, then
+// q_s [16][D] bf16, k_s / v_s [D], p_s [CW][16][32] bf16, ml_s [CW][G][2], acc_s [CW][G][D]
+constexpr int G_ = HQ_ / HKV_;
+constexpr int L_GRAW = L_XS;
+constexpr int L_ATT = L_GRAW + 1536 * 4;
+static_assert(L_ATT + 16 * D_ * 2 + 2 * D_ * 4 + CW * 16 * 32 * 2 + CW * G_ * 2 * 4 + CW * G_ * D_ * 4 <= L_RED,
+              "attention scratch fits the op input region");
+static_assert(L_END <= 160 * 1024, "LDS");
+
+}  // namespace
+
+size_t pse_lds_bytes() { return (size_t)L_END; }
+// KV head whose attention runs on CU c (one per XCD under round-robin placement), or -1
+__host__ __device__ inline int pse_att_g(int c, int P) {
+  const int d = P - 1 - c;
+  return (d >= 0 && d % 33 == 0 && d / 33 < HKV_) ? d / 33 : -1;
+}
+
+namespace {
+
+// the launch's LDS, visible by name in every helper so that the compiler addresses it as LDS
+// (ds_read / ds_write); an LDS pointer carried through a struct degrades to flat accesses
+extern __shared__ __attribute__((aligned(16))) unsigned char pse_lds[];
+#define PSE_CTL (reinterpret_cast<Ctl*>(pse_lds + L_CTL))
+
+struct Ctx {
+  const PseArgs& a;
+  int c, lane, wave, tid;
+  uint32_t epoch;
+  int bar_gen;
+};
+
+__device__ __forceinline__ bool failed(const Ctx& x) {
+  return __hip_atomic_load(&PSE_CTL->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
+}
+__device__ __forceinline__ void give_up(Ctx& x, uint32_t code) {
+  st32(x.a.err, code);
+  __hip_atomic_store(&PSE_CTL->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// consumer-only barrier (the loader never joins): a monotonic LDS counter
+__device__ __forceinline__ void cbar(Ctx& x) {
+  x.bar_gen += CW;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  if (x.lane == 0) __hip_atomic_fetch_add(&PSE_CTL->bar, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  uint32_t spins = 0;
+  while (__hip_atomic_load(&PSE_CTL->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < x.bar_gen) {
+    if (++spins > SPIN_LDS) {
+      give_up(x, 4);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(0);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Gather n consecutive granules g[0..n) carrying tag t into LDS: the first n0 payloads to
+// dst0, the rest to dst1; all consumer threads cooperate (n <= MAXP * 256) in ONE sweep loop (one
+// round trip per poll); false on timeout / abort.  Branch-free sc1 buffer loads (an out-of-range
+// offset reads zero): a load under a divergent branch would be waited for at once.
+template <int MAXP>
+__device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_t t, uint32_t* dst0, int n0,
+                                       uint32_t* dst1 = nullptr) {
+  constexpr uint32_t OOB = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(g), 0, n * 8, 0x00020000);
+  uint32_t pend = 0;  // bit i: granule tid + i * 256 not seen yet
+#pragma unroll
+  for (int i = 0; i < MAXP; ++i)
+    if (x.tid + i * CW * 64 < n) pend |= 1u << i;
+  bool ok = true;
+  for (uint32_t spins = 0;; ++spins) {
+    uint32_t lo[MAXP], hi[MAXP];
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i) {
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (pend >> i & 1u) ? (uint32_t)(x.tid + i * CW * 64) * 8u : OOB,
+                                                          0, 16 /* sc1 */);
+      lo[i] = v[0];
+      hi[i] = v[1];
+    }
+#pragma unroll
+    for (int i = 0; i < MAXP; ++i)
+      if ((pend >> i & 1u) && hi[i] == t) {
+        const int j = x.tid + i * CW * 64;
+        if (j < n0) dst0[j] = lo[i];
+        else dst1[j - n0] = lo[i];
+        pend &= ~(1u << i);
+      }
+    if (!__any(pend != 0)) break;
+    if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.a.err)))) {
+      give_up(x, 2);
+      ok = false;
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  cbar(x);
+  return ok && !failed(x);
+}
+
+// q|k|v partial granules grouped by KV head: group g = the q tiles of heads G g .. G g + G - 1,
+// then k tile rows of head g, then v (48 tiles x 2 K halves x 16 rows), so the attention of head
+// g gathers one contiguous range.  Row tile t of the q|k|v matrix -> its granule base.
+__device__ __forceinline__ int qkv_gran(int t) {
+  constexpr int TPH = D_ / 16, G = HQ_ / HKV_, GT = (G + 2) * TPH;  // tiles per head, per group
+  int g, o;
+  if (t < HQ_ * TPH) { g = t / (G * TPH); o = t - g * G * TPH; }
+  else if (t < (HQ_ + HKV_) * TPH) { g = (t - HQ_ * TPH) / TPH; o = G * TPH + (t - HQ_ * TPH - g * TPH); }
+  else { g = (t - (HQ_ + HKV_) * TPH) / TPH; o = (G + 1) * TPH + (t - (HQ_ + HKV_) * TPH - g * TPH); }
+  return (g * GT + o) * 32;
+}
+
+// Qwen3RMSNorm of the staged vector in place (TF/.../modeling_qwen3.py:59-64):
+// xs = bf16(w * bf16(h * r)), r = 1 / sqrt(sum(ss) / K + eps), ss = the producers' per-16-column
+// sums of squares (n_ss of them, summed in a fixed order by every wave)
+__device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, const bf16_t* w, int K) {
+  // (as the GEMV's norm prologue sums them: 4 per lane, then across the wave; n_ss <= 256)
+  float s = 0.f;
+  if (4 * x.lane < n_ss) s = (ss[4 * x.lane] + ss[4 * x.lane + 1]) + (ss[4 * x.lane + 2] + ss[4 * x.lane + 3]);
+  s = wave_sum(s);
+  const float r = 1.0f / sqrtf(s / (float)K + x.a.eps);
+  u32x4* xv = reinterpret_cast<u32x4*>(xs);
+  const u32x4* wv = reinterpret_cast<const u32x4*>(w);
+  for (int i = x.tid; i < K / 8; i += CW * 64) {
+    const u32x4 hv = xv[i], nv = wv[i];
+    u32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float h0 = __uint_as_float(hv[q] << 16), h1 = __uint_as_float(hv[q] & 0xffff0000u);
+      const float w0 = __uint_as_float(nv[q] << 16), w1 = __uint_as_float(nv[q] & 0xffff0000u);
+      o[q] = pack2(w0 * rbf(h0 * r), w1 * rbf(h1 * r));
+    }
+    xv[i] = o;
+  }
+  cbar(x);
+}
+
+// This consumer wave's 4 tiles of ring slot `seq`: acc += W_tiles . x over k tiles kt0 + 4w ..
+// (B operand = the staged vector: every MFMA column the same, column 0 is kept)
+__device__ __forceinline__ void consume_slot(Ctx& x, int seq, int kt0, f32x4& acc) {
+  for (uint32_t spins = 0;
+       __hip_atomic_load(&PSE_CTL->full[seq % LW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <= seq / LW;
+       ++spins) {
+    if (spins > SPIN_LDS || failed(x)) {
+      give_up(x, 3);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(0);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (x.a.probe == 2) {
+    if (x.lane == 0) __hip_atomic_store(&PSE_CTL->freed[x.wave - LW], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return;
+  }
+  const u32x4* sl = reinterpret_cast<const u32x4*>(pse_lds + L_RING + (seq % NS) * SLOT_KB * 1024);
+  const u32x4* xv = reinterpret_cast<const u32x4*>(pse_lds + L_XS);
+  const int w = x.wave - LW;
+  u32x4 wt[4], xb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int t = w * 4 + i;
+    wt[i] = sl[t * 64 + x.lane];
+    xb[i] = xv[(kt0 + t) * 4 + (x.lane >> 4)];
+  }
+  // the slot's bytes are in registers: release it to the loader
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (x.lane == 0) __hip_atomic_store(&PSE_CTL->freed[w], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wt[i]), __builtin_bit_cast(bf16x8, xb[i]),
+                                                  acc, 0, 0, 0);
+}
+
+// fixed-order reduction of the CW waves' partial tiles (two tiles r = 0, 1 in flight): put,
+// consumer barrier, then get(r, row) = the tile's output row (MFMA D layout: lane l holds rows
+// 4 (l >> 4) + i of column l & 15; column 0 = lanes 0, 16, 32, 48)
+__device__ __forceinline__ void red_put(Ctx& x, int r, const f32x4& acc) {
+  float* p = reinterpret_cast<float*>(pse_lds + L_RED) + ((x.wave - LW) * 2 + r) * 256 + x.lane * 4;
+  p[0] = acc[0]; p[1] = acc[1]; p[2] = acc[2]; p[3] = acc[3];
+}
+__device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
+  const float* red = reinterpret_cast<const float*>(pse_lds + L_RED);
+  const int off = 64 * (row >> 2) + (row & 3);
+  float s = 0.f;
+#pragma unroll
+  for (int w = 0; w < CW; ++w) s += red[(w * 2 + r) * 256 + off];
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Attention of KV head g for the new token at pos (B = 1), by the CW consumer waves: q / k
+// RMSNorm + RoPE (TF/.../modeling_qwen3.py:252-254, :148-170), K / V appended at pos
+// (TF/cache_utils.py:127-145), softmax(q k^T / sqrt(D)) v over keys 0..pos with the
+// probabilities rounded to bf16 before P.V (the reference's bf16 SDPA), per-wave online softmax
+// over 32-key chunks, the CW partials merged in a fixed order -> G x D outputs as granules.
+// graw: the gathered q|k|v K-half partials, [tile][half][16] fp32 (q tiles, k tiles, v tiles).
+// (false on a failed wait)
+__device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
+  const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
+  constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16;
+  const PseArgs& a = x.a;
+  const PseLayer& Lw = a.L[l];
+  const int pos = *a.pos;
+  const int lane = x.lane, w = x.wave - LW, g4 = lane >> 4, c16 = lane & 15;
+  const int Cmax = a.Cmax;
+  bf16_t* kcache = Lw.kc + (size_t)g * Cmax * D;  // [Cmax][D]
+  bf16_t* vcache = Lw.vc + (size_t)g * D * Cmax;  // [D][Cmax]
+  bf16_t* q_s = reinterpret_cast<bf16_t*>(pse_lds + L_ATT);           // [16][D] (heads >= G zero)
+  float* k_s = reinterpret_cast<float*>(q_s + 16 * D);              // [D]
+  float* v_s = k_s + D;                                             // [D]
+  bf16_t* p_s = reinterpret_cast<bf16_t*>(v_s + D);                 // [CW][16][KW]
+  float* ml_s = reinterpret_cast<float*>(p_s + CW * 16 * KW);       // [CW][G][2]
+  float* acc_s = ml_s + CW * G * 2;                                 // [CW][G][D]
+  constexpr uint32_t OOBA = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(kcache, 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(vcache, 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.mask), 0, Cmax, 0x00020000);
+  const int nchunk = pos / KW + 1;
+  // a wave's 32-key chunk: K tiles (A operands), V^T fragments (B operands), mask words; keys
+  // >= pos read zero (branch-free buffer loads; the new key / value are patched in from LDS)
+  auto load_chunk = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
+    const int k0 = ch * KW;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = k0 + t * 16 + c16;
+#pragma unroll
+      for (int s2 = 0; s2 < QS; ++s2)
+        kt[t][s2] = __builtin_amdgcn_raw_buffer_load_b128(
+            krs, key < pos ? (uint32_t)(key * D + s2 * 32 + 8 * g4) * 2u : OOBA, 0, 0);
+      mk[t] = __builtin_amdgcn_raw_buffer_load_b32(mrs, (k0 + t * 16 <= pos) ? (uint32_t)(k0 + t * 16 + g4 * 4) : OOBA,
+                                                   0, 0);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int kb = k0 + 8 * g4;
+      vt[dt] = __builtin_amdgcn_raw_buffer_load_b128(
+          vrs, kb < pos ? (uint32_t)((dt * 16 + c16) * Cmax + kb) * 2u : OOBA, 0, 0);
+    }
+  };
+  u32x4 ktA[2][QS], vtA[DT];
+  uint32_t mkA[2];
+  constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the head's q|k|v granules
+  if (!gather<NG / (CW * 64)>(x, x.a.g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG))
+    return false;
+  // q|k|v row value: sum of the two K-half partials, rounded to bf16 (the projection output)
+  auto val = [&](int base_tile, int i) {
+    const float* p = graw + (base_tile + i / 16) * 32 + i % 16;
+    return rbf(p[0] + p[16]);
+  };
+  for (int i = x.tid; i < 16 * D; i += CW * 64)
+    if (i / D >= G) q_s[i] = 0;
+  // jobs: j < G q head j, G: k, G + 1: v; wave w takes jobs w, w + CW; a lane holds 2 dims
+  for (int j = w; j < G + 2; j += CW) {
+    const int bt = j < G ? j * (D / 16) : (j == G ? G * (D / 16) : (G + 1) * (D / 16));
+    const float x0 = val(bt, 2 * lane), x1 = val(bt, 2 * lane + 1);
+    if (j == G + 1) {
+      v_s[2 * lane] = x0;
+      v_s[2 * lane + 1] = x1;
+      vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
+      vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
+      continue;
+    }
+    const bf16_t* nw = j < G ? Lw.q_norm : Lw.k_norm;
+    const float ss = wave_sum(x0 * x0 + x1 * x1);
+    const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
+    const float n0 = rbf(bf2f(nw[2 * lane]) * rbf(x0 * r)), n1 = rbf(bf2f(nw[2 * lane + 1]) * rbf(x1 * r));
+    constexpr int q4 = D / 4;
+    const bool lo = 2 * lane < D / 2;
+    const int partner = lo ? lane + q4 : lane - q4;
+    const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
+    const float sg = lo ? -1.f : 1.f;
+    const bf16_t* ct = a.cos_t + (size_t)pos * D;
+    const bf16_t* st = a.sin_t + (size_t)pos * D;
+    const float c0 = bf2f(ct[2 * lane]), c1 = bf2f(ct[2 * lane + 1]);
+    const float s0 = bf2f(st[2 * lane]), s1 = bf2f(st[2 * lane + 1]);
+    const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)), o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+    if (j < G) {
+      q_s[j * D + 2 * lane] = f2bf(o0);
+      q_s[j * D + 2 * lane + 1] = f2bf(o1);
+    } else {
+      k_s[2 * lane] = o0;
+      k_s[2 * lane + 1] = o1;
+      *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
+    }
+  }
+  cbar(x);
+  float m_run = -INFINITY, l_run = 0.f;
+  f32x4 o_run[DT];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt) o_run[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
+    const int k0 = ch * KW;
+    f32x4 sacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      if (k0 + t * 16 + c16 == pos) {  // the new key, from LDS
+#pragma unroll
+        for (int s2 = 0; s2 < QS; ++s2) {
+          const int d0 = s2 * 32 + 8 * g4;
+          u32x4 v;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) v[i] = pack2(k_s[d0 + 2 * i], k_s[d0 + 2 * i + 1]);
+          kt[t][s2] = v;
+        }
+      }
+      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < QS; ++s2)
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][s2]),
+                                                         *reinterpret_cast<const bf16x8*>(&q_s[c16 * D + s2 * 32 + 8 * g4]),
+                                                         sacc[t], 0, 0, 0);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int dim = dt * 16 + c16, kb = k0 + 8 * g4;
+      if (kb + 8 > pos && kb <= pos) {  // the new value patched in, keys past pos zero
+        u32x4 v = vt[dt];
+        const uint32_t nv = (uint32_t)f2bf(v_s[dim]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int kk = kb + 2 * i;
+          const uint32_t lo = kk < pos ? (v[i] & 0xffffu) : (kk == pos ? nv : 0u);
+          const uint32_t hi = kk + 1 < pos ? (v[i] >> 16) : (kk + 1 == pos ? nv : 0u);
+          v[i] = lo | (hi << 16);
+        }
+        vt[dt] = v;
+      }
+    }
+    float sv[2][4], mc = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + t * 16 + g4 * 4 + r;
+        const bool valid = key <= pos && ((mk[t] >> (8 * r)) & 0xffu);
+        sv[t][r] = valid ? sacc[t][r] * a.scale : -INFINITY;
+        mc = fmaxf(mc, sv[t][r]);
+      }
+    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    float lc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float pr4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
+        lc += p;
+        pr4[r] = p;
+      }
+      uint2 pk;
+      pk.x = pack2(pr4[0], pr4[1]);
+      pk.y = pack2(pr4[2], pr4[3]);
+      *reinterpret_cast<uint2*>(&p_s[(w * 16 + c16) * KW + t * 16 + g4 * 4]) = pk;
+    }
+    lc += __shfl_xor(lc, 16, 64);
+    lc += __shfl_xor(lc, 32, 64);
+    const float mn = fmaxf(m_run, mc);
+    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
+    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
+    l_run = l_run * alpha + lc * beta;
+    m_run = mn;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
+    float al[4], be[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      al[r] = __shfl(alpha, g4 * 4 + r, 64);
+      be[r] = __shfl(beta, g4 * 4 + r, 64);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
+                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    };
+  // the wave's chunks w, w + CW, ... (the first one prefetched above)
+  for (int ch = w; ch < nchunk; ch += CW) {
+    load_chunk(ch, ktA, vtA, mkA);
+    compute(ch, ktA, vtA, mkA);
+  }
+  if (lane < G) {
+    ml_s[(w * G + lane) * 2] = m_run;
+    ml_s[(w * G + lane) * 2 + 1] = l_run;
+  }
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int h = g4 * 4 + r;
+      if (h < G) acc_s[(w * G + h) * D + dt * 16 + c16] = o_run[dt][r];
+    }
+  cbar(x);
+  // merge the CW wave partials in a fixed order, 2 output dims per thread -> granules
+  const uint32_t tag = tagof(x.epoch, l, OP_ATT);
+  for (int e2 = x.tid; e2 < G * D / 2; e2 += CW * 64) {
+    const int e = 2 * e2, h = e / D, d = e % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * G + h) * 2]);
+    float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < CW; ++ww) {
+      const float mw = ml_s[(ww * G + h) * 2];
+      const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
+      L += f * ml_s[(ww * G + h) * 2 + 1];
+      o0 += f * acc_s[(ww * G + h) * D + d];
+      o1 += f * acc_s[(ww * G + h) * D + d + 1];
+    }
+    st64(a.g_att + (g * G * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tag));
+  }
+  cbar(x);
+  return true;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
+  unsigned char* const lds = pse_lds;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x, P = gridDim.x;
+  Ctl* ctl = reinterpret_cast<Ctl*>(lds + L_CTL);
+  static_assert(sizeof(Ctl) <= 256, "control words");
+  if (threadIdx.x < 64) reinterpret_cast<int*>(lds + L_CTL)[threadIdx.x] = 0;
+  // the loader's weight pointers, [layer][q|k|v, o, gate|up, down], in LDS: a global load in its
+  // loop would be waited for with vmcnt(0), i.e. with every weight fill in flight
+  const bf16_t** wp = reinterpret_cast<const bf16_t**>(lds + L_PTR);
+  for (int i = threadIdx.x; i < a.layers * 4; i += THREADS) {
+    const PseLayer& q = a.L[i / 4];
+    wp[i] = (i & 3) == 0 ? q.qkv : ((i & 3) == 1 ? q.o : ((i & 3) == 2 ? q.gu : q.down));
+  }
+  __syncthreads();
+  const uint32_t epoch = (ld32(a.epoch) + 1u) & 0xffffffu;
+  const int total = a.layers * SPL;
+
+  if (wave < LW) {
+    // =================== loaders ===================
+    // loader wave k streams slots k, k + LW, ...; m = its own slot count, marked = its slots
+    // published in full[k]
+    const int k = wave;
+    int marked = 0, m = 0;
+    for (int s = k; s < total; s += LW, ++m) {
+      // ring slot s % NS is free once every consumer wave has read slot s - NS
+      if (s >= NS) {
+        for (uint32_t spins = 0;; ++spins) {
+          int mn = 1 << 30;
+#pragma unroll
+          for (int w = 0; w < CW; ++w)
+            mn = min(mn, __hip_atomic_load(&ctl->freed[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          if (mn >= s - NS + 1) break;
+          if (marked < m) {  // stalled: retire every fill in flight so the consumers can drain the ring
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            marked = m;
+            __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          if (spins > SPIN_LDS || __hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            st32(a.err, 1u);
+            s = total;  // drain
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (s >= total) break;
+      }
+      // this slot's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles
+      const int l = s / SPL, r = s - l * SPL;
+      if (a.trace && lane == 0) {  // loader events into LDS (global stores would join its vmcnt count)
+        const int ev = r == 0 ? 0 : (r == 12 ? 1 : (r == 20 ? 2 : (r == 68 ? 3 : (r >= SPL - LW ? 4 : -1))));
+        if (ev >= 0) ctl->lstamp[l & 1][ev] = __builtin_amdgcn_s_memrealtime();
+      }
+      const bf16_t* src;
+      if (r < 12) {  // q|k|v: unit 3c + r / 4 = (row tile, K half), 4 slots each
+        const int u = 3 * c + r / 4, t = u >> 1, half = u & 1;
+        src = wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
+      } else if (r < 20) {  // o_proj row tile c, 8 slots
+        src = wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
+      } else if (r < 68) {  // gate|up pairs 3c .. 3c+2: gate tile (8 slots), then up tile (8)
+        const int q = r - 20, pr = 3 * c + q / 16, rt = 2 * pr + (q % 16) / 8;
+        src = wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
+      } else {  // down row tile c, 24 slots
+        src = wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;
+      }
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)(uintptr_t)(lvoid*)(lds + L_RING + (s % NS) * SLOT_KB * 1024));
+      if (a.probe != 1) {
+#pragma unroll
+        for (int t = 0; t < SLOT_KB; ++t) glds16(reinterpret_cast<const u32x4*>(src) + t * 64 + lane, dst + t * 1024);
+      }
+      // keep FILLS - 1 of this wave's fills in flight behind this one; publish the older ones
+      if (m + 1 - marked >= FILLS) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((FILLS - 1) * SLOT_KB) : "memory");
+        marked = m + 1 - (FILLS - 1);
+        __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&ctl->full[k], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    // =================== consumers ===================
+    Ctx x{a, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
+    uint32_t* xs32 = reinterpret_cast<uint32_t*>(lds + L_XS);
+    bf16_t* xs = reinterpret_cast<bf16_t*>(lds + L_XS);
+    float* ssl = reinterpret_cast<float*>(lds + L_MISC);  // [256] gathered sums of squares
+    constexpr int NT = H_ / 16;
+    const int att_g = pse_att_g(c, P);
+    // residual columns 16c .. 16c+15 owned by this CU: lanes 0..15 of wave 1 (bf16 values)
+    float hres = (wave == LW && lane < 16) ? bf2f(a.h[c * 16 + lane]) : 0.f;
+    float hsq = 0.f;
+    int seq = 0;  // ring slot sequence number
+    // o / d: this lane's output row (wave 1, lanes < 16): hidden = residual + bf16(o)
+    // (TF/.../modeling_qwen3.py:311,322), published with its sum of squares
+    auto emit_h = [&](int which, uint32_t t, float o) {
+      if (wave != LW) return;
+      const float hv = rbf(hres + rbf(o));
+      hres = lane < 16 ? hv : 0.f;
+      const float sq = lane < 16 ? hv * hv : 0.f;
+      // the 16 columns' sum of squares in column order, as the GEMV epilogue forms it
+      float s16 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) s16 += __shfl(sq, i, 64);
+      hsq = s16;
+      const float hn = __shfl_down(hv, 1, 64);
+      if (lane < 16 && (lane & 1) == 0) st64(a.g_h[which] + c * 8 + lane / 2, gran(pack2(hv, hn), t));
+      if (lane == 0) st64(a.g_ss[which] + c, gran(__float_as_uint(s16), t));
+    };
+
+    for (int l = 0; l < a.layers && !failed(x); ++l) {
+      const PseLayer& Lw = a.L[l];
+      if (wave == LW) PSE_STAMP(l, 0);
+      // ---------------- q|k|v (input RMSNorm fused) ----------------
+      if (l == 0) {  // the embedding row and its sums of squares (previous launch)
+        for (int i = x.tid; i < H_ / 2; i += CW * 64) xs32[i] = reinterpret_cast<const uint32_t*>(a.h)[i];
+        for (int i = x.tid; i < NT; i += CW * 64) ssl[i] = a.ss[i];
+        cbar(x);
+      } else {
+        if (!gather<9>(x, a.g_h[1], H_ / 2 + NT, tagof(epoch, l - 1, OP_DOWN), xs32, H_ / 2,
+                       reinterpret_cast<uint32_t*>(ssl)))
+          break;
+      }
+      norm_stage(x, xs, ssl, NT, Lw.in_norm, H_);
+      if (wave == LW) PSE_STAMP(l, 1);
+      const uint32_t tq = tagof(epoch, l, OP_QKV);
+      #pragma unroll 1
+      for (int j = 0; j < 3; ++j) {
+        const int u = 3 * c + j, half = u & 1;
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        #pragma unroll 1
+        for (int k = 0; k < 4; ++k) consume_slot(x, seq++, half * 64 + k * 16, acc);
+        red_put(x, 0, acc);
+        cbar(x);
+        if (wave == LW && lane < 16)
+          st64(a.g_qkv + qkv_gran(u >> 1) + (u & 1) * 16 + lane, gran(__float_as_uint(red_get(x, 0, lane)), tq));
+        cbar(x);
+      }
+      if (wave == LW) PSE_STAMP(l, 2);
+      // ---------------- attention (one CU per KV head) ----------------
+      if (att_g >= 0) {
+        // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
+        if (!attention(x, l, att_g, tq)) break;
+        if (wave == LW) PSE_STAMP(l, 3);
+      }
+      // ---------------- o_proj (+ residual) ----------------
+      if (!gather<8>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2)) break;
+      if (wave == LW) PSE_STAMP(l, 4);
+      {
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        #pragma unroll 1
+        for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, acc);
+        red_put(x, 0, acc);
+        cbar(x);
+        emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f);
+        cbar(x);
+      }
+      if (wave == LW) PSE_STAMP(l, 5);
+      // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
+      if (!gather<9>(x, a.g_h[0], H_ / 2 + NT, tagof(epoch, l, OP_O), xs32, H_ / 2, reinterpret_cast<uint32_t*>(ssl)))
+        break;
+      norm_stage(x, xs, ssl, NT, Lw.post_norm, H_);
+      if (wave == LW) PSE_STAMP(l, 6);
+      const uint32_t tg = tagof(epoch, l, OP_GU);
+      #pragma unroll 1
+      for (int j = 0; j < 3; ++j) {
+        f32x4 ag = (f32x4){0.f, 0.f, 0.f, 0.f}, au = ag;
+        #pragma unroll 1
+        for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, ag);
+        #pragma unroll 1
+        for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, au);
+        red_put(x, 0, ag);
+        red_put(x, 1, au);
+        cbar(x);
+        if (wave == LW) {
+          // bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
+          const float gg = rbf(red_get(x, 0, lane & 15)), uu = rbf(red_get(x, 1, lane & 15));
+          const float o = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
+          const float on = __shfl_down(o, 1, 64);
+          if (lane < 16 && (lane & 1) == 0) st64(a.g_act + (3 * c + j) * 8 + lane / 2, gran(pack2(o, on), tg));
+        }
+        cbar(x);
+      }
+      if (wave == LW) PSE_STAMP(l, 7);
+      // ---------------- down (+ residual) ----------------
+      if (!gather<24>(x, a.g_act, I_ / 2, tg, xs32, I_ / 2)) break;
+      if (wave == LW) PSE_STAMP(l, 8);
+      {
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        #pragma unroll 1
+        for (int k = 0; k < 24; ++k) consume_slot(x, seq++, k * 16, acc);
+        red_put(x, 0, acc);
+        cbar(x);
+        emit_h(1, tagof(epoch, l, OP_DOWN), lane < 16 ? red_get(x, 0, lane) : 0.f);
+        cbar(x);
+      }
+      if (wave == LW) PSE_STAMP(l, 9);
+      if (a.trace && wave == LW && lane < 5)
+        a.trace[((size_t)l * PSE_TRACE_EV + 10 + lane) * 256 + c] = ctl->lstamp[l & 1][lane];
+    }
+    // the final residual and its sums of squares for the heads (plain stores: the next launch)
+    if (wave == LW && lane < 16) a.h[c * 16 + lane] = f2bf(hres);
+    if (wave == LW && lane == 0) a.ss[c] = hsq;
+  }
+  // exit: the last workgroup out advances the epoch for the next launch
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t t = __hip_atomic_fetch_add((g32*)a.exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == (uint32_t)P - 1) {
+      st32(a.exit_cnt, 0u);
+      st32(a.epoch, epoch);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+bool pse_supported(int device, int B, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax) {
+  if (B != 1 || H != H_ || Hq != HQ_ || Hkv != HKV_ || D != D_ || I != I_ || qkv_rows != QKVR_ || Cmax % 64) return false;
+  return pse_grid(device) == 256;
+}
+
+int pse_grid(int device) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, device) != hipSuccess) return 0;
+  if (hipFuncSetAttribute((const void*)pse_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pse_lds_bytes()) !=
+      hipSuccess)
+    return 0;
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pse_kernel, THREADS, pse_lds_bytes()) !=
+      hipSuccess || per_cu < 1)
+    return 0;
+  return p.multiProcessorCount;
+}
+
+size_t pse_ws_bytes() {
+  // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
+  // act (6144); words: error, epoch, exit count
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 + 64;
+}
+
+hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
+  if (a0.layers < 1 || a0.layers > PSE_MAXL || a0.Cmax % 64) return hipErrorInvalidValue;
+  PseArgs a = a0;
+  uint64_t* g = reinterpret_cast<uint64_t*>(ws);
+  a.g_qkv = g; g += 768 * 16;
+  a.g_att = g; g += HQ_ * D_ / 2;
+  // h granules of an op immediately followed by its sums of squares: one gather range
+  a.g_h[0] = g; g += H_ / 2;
+  a.g_ss[0] = g; g += H_ / 16;
+  a.g_h[1] = g; g += H_ / 2;
+  a.g_ss[1] = g; g += H_ / 16;
+  a.g_act = g; g += I_ / 2;
+  uint32_t* w = reinterpret_cast<uint32_t*>(g);
+  a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
+  hipLaunchKernelGGL(pse_kernel, dim3(256), dim3(THREADS), pse_lds_bytes(), s, a);
+  return hipGetLastError();
+}
+
+uint32_t* pse_err_word(void* ws) {
+  return reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse_ws_bytes() - 64);
+}
+
+}  // namespace mtts

@@ -135,6 +135,10 @@ class Engine:
         """Workgroups of the persistent decode launch (0: one launch per stage)."""
         return int(N.load().mtts_mega_workgroups(self._h))
 
+    def pse_active(self) -> bool:
+        """Whether batch-1 decode steps run the decoder stack as one persistent launch (pse.hip)."""
+        return bool(N.load().mtts_pse_active(self._h))
+
     def attn_o_active(self, batch: int) -> bool:
         """Whether a decode step of `batch` rows runs attention + o_proj as one launch (ao.hip)."""
         return bool(N.load().mtts_attn_o_active(self._h, batch))

@@ -1,0 +1,75 @@
+"""Per-layer event timeline of the persistent streaming decode launch (csrc/pse.hip), 8B shape, B=1.
+
+Builds a random-weight engine with MTTS_PSE=1 MTTS_PSE_TRACE=1, prefills a synthetic prompt,
+runs teacher-forced decode forwards, and prints, for a few layers, each event's time (us from the
+launch's first stamp; median / max over the 256 workgroups) -- consumer events 0-9, loader
+events 10-14 (see pse.hip) -- and the decode forward wall time with and without PSE."""
+import ctypes
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from moss_tts_amd import _native as N  # noqa: E402
+
+NAMES = ["layer", "qkv in", "qkv done", "att done", "o in", "o done", "gu in", "gu done", "down in", "down done",
+         "L qkv", "L o", "L gu", "L down", "L end"]
+
+
+def build(pse, layers):
+    from moss_tts_amd.engine import Engine, EngineConfig
+    os.environ["MTTS_PSE"] = "1" if pse else "0"
+    if os.environ.get("PSE_NO_TRACE") != "1":
+        os.environ["MTTS_PSE_TRACE"] = "1"
+    e = Engine(EngineConfig(layers=layers, max_batch=1, max_ctx=512, max_prefill_tokens=512), 0)
+    e.init_random(seed=0)
+    return e
+
+
+def run(e, T, steps):
+    rng = np.random.default_rng(0)
+    ids = torch.from_numpy(rng.integers(0, 1024, (1, T + steps, 33))).cuda()
+    mask = torch.ones(1, T + steps, dtype=torch.uint8, device="cuda")
+    e.forward(ids[:, :T], mask[:, :T], 0)
+    torch.cuda.synchronize()
+    ts = []
+    for s in range(steps):
+        p = T + s
+        t0 = time.perf_counter()
+        e.forward(ids[:, p:p + 1], mask[:, :p + 1], p)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts[2:])) * 1e3
+
+
+layers = int(sys.argv[1]) if len(sys.argv) > 1 else 8
+T = 181
+eb = build(False, layers)
+print(f"per-op launches: decode forward {run(eb, T, 8):.3f} ms ({layers} layers)")
+eb.close()
+e = build(True, layers)
+print(f"pse: decode forward {run(e, T, 8):.3f} ms ({layers} layers)")
+if os.environ.get("PSE_NO_TRACE") == "1":
+    sys.exit(0)
+n = layers * 16 * 256
+buf = (ctypes.c_uint64 * n)()
+N.check(N.load().mtts_pse_trace(e._h, buf, n), "trace")
+tr = np.frombuffer(buf, np.uint64).reshape(layers, 16, 256).astype(np.float64)
+t0 = tr[0, 10][tr[0, 10] > 0].min()
+for l in list(range(min(layers, 4))) + [layers - 1]:
+    row = []
+    for ev in range(15):
+        v = tr[l, ev]
+        v = v[v > 0]
+        if v.size:
+            row.append(f"{NAMES[ev]} {np.median((v - t0) / 100):.1f}/{np.max((v - t0) / 100):.1f}")
+    print(f"L{l}: " + " | ".join(row))
+lay = []
+for l in range(1, layers):
+    a0, a1 = tr[l - 1, 9], tr[l, 9]
+    lay.append(np.median(a1 - a0) / 100)
+print("median layer period (down done -> down done) us:", np.round(lay, 1))
+e.close()
