@@ -316,13 +316,13 @@ struct PseArgs {
   int Cmax;
   float eps, scale;
   // workspace (set by pse_decode): granules and words
-  uint64_t *g_qkv, *g_att, *g_h[2], *g_ss[2], *g_act;
+  uint64_t *g_qkv, *g_att, *g_attp, *g_h[2], *g_ss[2], *g_act;
   uint32_t *err, *epoch, *exit_cnt;
   uint64_t* trace;  // nullptr, or [layers][PSE_TRACE_EV][256] s_memrealtime stamps
   int probe;        // timing probe (MTTS_PSE_PROBE; results invalid): 1 loader issues no DMA,
                     // 2 consumers skip the slot reads and MFMAs
 };
-constexpr int PSE_TRACE_EV = 16;
+constexpr int PSE_TRACE_EV = 20;
 size_t pse_lds_bytes();
 int pse_grid(int device);
 bool pse_supported(int device, int B, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);

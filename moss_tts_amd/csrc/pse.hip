@@ -37,13 +37,16 @@ namespace mtts {
 namespace {
 
 constexpr int CW = 4;                   // consumer waves
-constexpr int LW = 2;                   // loader waves (each its own vmcnt: 4 fills = 64 instructions)
+#ifndef PSE_LW
+#define PSE_LW 1
+#endif
+constexpr int LW = PSE_LW;              // loader waves (each its own vmcnt: 4 fills = 64 instructions)
 constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_NS
 #define PSE_NS 7
 #endif
 #ifndef PSE_FILLS
-#define PSE_FILLS 4
+#define PSE_FILLS 3
 #endif
 constexpr int NS = PSE_NS;              // ring slots
 constexpr int SLOT_KB = 16;             // 1 KiB tiles per slot
@@ -70,7 +73,8 @@ __device__ __forceinline__ void st32(void* p, uint32_t v) {
 // trace events (PSE_TRACE_EV per layer): consumers (wave 1) 0 layer start, 1 q|k|v input
 // normed, 2 q|k|v done, 3 attention done (attention CUs), 4 o input, 5 o done, 6 gate|up input
 // normed, 7 gate|up done, 8 down input, 9 down done; loader 10 first q|k|v slot issued, 11 first
-// o slot, 12 first gate|up slot, 13 first down slot, 14 last slot of the layer issued
+// o slot, 12 first gate|up slot, 13 first down slot, 14 last slot of the layer issued;
+// attention CUs 15 q|k|v gathered, 16 chunks start, 17 chunks done, 18 other units' partials in
 #define PSE_STAMP(l, ev)                                                                        \
   do {                                                                                          \
     if (a.trace && lane == 0) a.trace[((size_t)(l) * PSE_TRACE_EV + (ev)) * 256 + c] = __builtin_amdgcn_s_memrealtime(); \
@@ -124,10 +128,15 @@ static_assert(L_END <= 160 * 1024, "LDS");
 }  // namespace
 
 size_t pse_lds_bytes() { return (size_t)L_END; }
-// KV head whose attention runs on CU c (one per XCD under round-robin placement), or -1
-__host__ __device__ inline int pse_att_g(int c, int P) {
+// Attention units: PSE_AU per KV head, each a quarter of the 32-key chunks (round-robin), so a
+// wave holds one chunk up to 32 PSE_AU CW keys of context.  Unit index u = g * PSE_AU + k runs on
+// CU P - 1 - 7 u (spread over the XCDs under round-robin placement); -1: no attention unit.
+#ifndef PSE_AU
+#define PSE_AU 2
+#endif
+__host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
-  return (d >= 0 && d % 33 == 0 && d / 33 < HKV_) ? d / 33 : -1;
+  return (d >= 0 && d % 7 == 0 && d / 7 < HKV_ * PSE_AU) ? d / 7 : -1;
 }
 
 namespace {
@@ -308,7 +317,8 @@ __device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
 // over 32-key chunks, the CW partials merged in a fixed order -> G x D outputs as granules.
 // graw: the gathered q|k|v K-half partials, [tile][half][16] fp32 (q tiles, k tiles, v tiles).
 // (false on a failed wait)
-__device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
+__device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) {
+  const int g = unit / PSE_AU, ku = unit % PSE_AU;
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16;
   const PseArgs& a = x.a;
@@ -352,9 +362,27 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
   };
   u32x4 ktA[2][QS], vtA[DT];
   uint32_t mkA[2];
+  // this wave's chunks: ku CW + w, then every PSE_AU CW; the first one goes out before the
+  // q|k|v gather (the cached keys do not depend on it)
+  const int ch0 = ku * CW + w;
+  constexpr int CSTEP = PSE_AU * CW;
+  load_chunk(ch0, ktA, vtA, mkA);
+  // and the prologue's other inputs: this wave's jobs' norm weights and the RoPE row at pos
+  // (2 dims per lane), also before the gather
+  constexpr int JW = (G + 2 + CW - 1) / CW;  // jobs per wave
+  uint32_t pnw[JW], pcs = 0, psn = 0;
+#pragma unroll
+  for (int jj = 0; jj < JW; ++jj) {
+    const int j = w + jj * CW;
+    pnw[jj] = j <= G ? reinterpret_cast<const uint32_t*>(j < G ? Lw.q_norm : Lw.k_norm)[lane] : 0u;
+  }
+  pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
+  psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
   constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the head's q|k|v granules
   if (!gather<NG / (CW * 64)>(x, x.a.g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG))
     return false;
+  const int c = x.c;
+  if (w == 0) PSE_STAMP(l, 15);
   // q|k|v row value: sum of the two K-half partials, rounded to bf16 (the projection output)
   auto val = [&](int base_tile, int i) {
     const float* p = graw + (base_tile + i / 16) * 32 + i % 16;
@@ -363,29 +391,32 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
   for (int i = x.tid; i < 16 * D; i += CW * 64)
     if (i / D >= G) q_s[i] = 0;
   // jobs: j < G q head j, G: k, G + 1: v; wave w takes jobs w, w + CW; a lane holds 2 dims
-  for (int j = w; j < G + 2; j += CW) {
+#pragma unroll
+  for (int jj = 0; jj < JW; ++jj) {
+    const int j = w + jj * CW;
+    if (j >= G + 2) continue;
     const int bt = j < G ? j * (D / 16) : (j == G ? G * (D / 16) : (G + 1) * (D / 16));
     const float x0 = val(bt, 2 * lane), x1 = val(bt, 2 * lane + 1);
     if (j == G + 1) {
       v_s[2 * lane] = x0;
       v_s[2 * lane + 1] = x1;
-      vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
-      vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
+      if (ku == 0) {  // one unit appends the new token to the cache
+        vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
+        vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
+      }
       continue;
     }
-    const bf16_t* nw = j < G ? Lw.q_norm : Lw.k_norm;
     const float ss = wave_sum(x0 * x0 + x1 * x1);
     const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
-    const float n0 = rbf(bf2f(nw[2 * lane]) * rbf(x0 * r)), n1 = rbf(bf2f(nw[2 * lane + 1]) * rbf(x1 * r));
+    const float n0 = rbf(__uint_as_float(pnw[jj] << 16) * rbf(x0 * r)),
+                n1 = rbf(__uint_as_float(pnw[jj] & 0xffff0000u) * rbf(x1 * r));
     constexpr int q4 = D / 4;
     const bool lo = 2 * lane < D / 2;
     const int partner = lo ? lane + q4 : lane - q4;
     const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
     const float sg = lo ? -1.f : 1.f;
-    const bf16_t* ct = a.cos_t + (size_t)pos * D;
-    const bf16_t* st = a.sin_t + (size_t)pos * D;
-    const float c0 = bf2f(ct[2 * lane]), c1 = bf2f(ct[2 * lane + 1]);
-    const float s0 = bf2f(st[2 * lane]), s1 = bf2f(st[2 * lane + 1]);
+    const float c0 = __uint_as_float(pcs << 16), c1 = __uint_as_float(pcs & 0xffff0000u);
+    const float s0 = __uint_as_float(psn << 16), s1 = __uint_as_float(psn & 0xffff0000u);
     const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)), o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
     if (j < G) {
       q_s[j * D + 2 * lane] = f2bf(o0);
@@ -393,7 +424,7 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
     } else {
       k_s[2 * lane] = o0;
       k_s[2 * lane + 1] = o1;
-      *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
+      if (ku == 0) *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
     }
   }
   cbar(x);
@@ -492,11 +523,12 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
-  // the wave's chunks w, w + CW, ... (the first one prefetched above)
-  for (int ch = w; ch < nchunk; ch += CW) {
-    load_chunk(ch, ktA, vtA, mkA);
+  if (w == 0) PSE_STAMP(l, 16);
+  for (int ch = ch0; ch < nchunk; ch += CSTEP) {
+    if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
     compute(ch, ktA, vtA, mkA);
   }
+  if (w == 0) PSE_STAMP(l, 17);
   if (lane < G) {
     ml_s[(w * G + lane) * 2] = m_run;
     ml_s[(w * G + lane) * 2 + 1] = l_run;
@@ -509,23 +541,59 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int g, uint32_t tq) {
       if (h < G) acc_s[(w * G + h) * D + dt * 16 + c16] = o_run[dt][r];
     }
   cbar(x);
-  // merge the CW wave partials in a fixed order, 2 output dims per thread -> granules
-  const uint32_t tag = tagof(x.epoch, l, OP_ATT);
-  for (int e2 = x.tid; e2 < G * D / 2; e2 += CW * 64) {
-    const int e = 2 * e2, h = e / D, d = e % D;
-    float M = -INFINITY;
+  // merge the CW wave partials in a fixed order: thread e2 holds 2 output dims of head h,
+  // unnormalised (M, L, O) of this unit
+  const int e = 2 * x.tid, h = e / D, d = e % D;  // G * D / 2 == CW * 64 threads
+  float M = -INFINITY;
 #pragma unroll
-    for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * G + h) * 2]);
-    float L = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * G + h) * 2]);
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < CW; ++ww) {
-      const float mw = ml_s[(ww * G + h) * 2];
-      const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
-      L += f * ml_s[(ww * G + h) * 2 + 1];
-      o0 += f * acc_s[(ww * G + h) * D + d];
-      o1 += f * acc_s[(ww * G + h) * D + d + 1];
+  for (int ww = 0; ww < CW; ++ww) {
+    const float mw = ml_s[(ww * G + h) * 2];
+    const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
+    L += f * ml_s[(ww * G + h) * 2 + 1];
+    o0 += f * acc_s[(ww * G + h) * D + d];
+    o1 += f * acc_s[(ww * G + h) * D + d + 1];
+  }
+  constexpr int PW = G * D + 2 * G;  // partial granules of one unit: O [G][D], M [G], L [G]
+  if constexpr (PSE_AU == 1) {
+    st64(a.g_att + (g * G * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+  } else {
+  if (ku != 0) {
+    // units 1..: publish the partial for unit 0 of the head
+    const uint32_t tp = tagof(x.epoch, l, OP_ATT) | 0x80000000u;
+    uint64_t* pp = a.g_attp + (size_t)unit * PW;
+    st64(pp + e, gran(__float_as_uint(o0), tp));
+    st64(pp + e + 1, gran(__float_as_uint(o1), tp));
+    if (d == 0) {
+      st64(pp + G * D + h, gran(__float_as_uint(M), tp));
+      st64(pp + G * D + G + h, gran(__float_as_uint(L), tp));
     }
-    st64(a.g_att + (g * G * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tag));
+    cbar(x);
+    return true;
+  }
+  // unit 0: the other units' partials (contiguous), merged in unit order -> the output granules
+  float* pg = reinterpret_cast<float*>(pse_lds + L_GRAW);  // (q|k|v partials and q_s are dead)
+  if (!gather<((PSE_AU - 1) * PW + CW * 64 - 1) / (CW * 64)>(x, a.g_attp + (size_t)(unit + 1) * PW, (PSE_AU - 1) * PW,
+                                                            tagof(x.epoch, l, OP_ATT) | 0x80000000u,
+                                                            reinterpret_cast<uint32_t*>(pg), (PSE_AU - 1) * PW))
+    return false;
+  if (w == 0) PSE_STAMP(l, 18);
+  float MM = M;
+#pragma unroll
+  for (int k2 = 1; k2 < PSE_AU; ++k2) MM = fmaxf(MM, pg[(k2 - 1) * PW + G * D + h]);
+  float LL = 0.f, O0 = 0.f, O1 = 0.f;
+#pragma unroll
+  for (int k2 = 0; k2 < PSE_AU; ++k2) {
+    const float* q = pg + (k2 - 1) * PW;
+    const float mk = k2 == 0 ? M : q[G * D + h];
+    const float f = (mk == -INFINITY) ? 0.f : expf(mk - MM);
+    LL += f * (k2 == 0 ? L : q[G * D + G + h]);
+    O0 += f * (k2 == 0 ? o0 : q[e]);
+    O1 += f * (k2 == 0 ? o1 : q[e + 1]);
+  }
+  st64(a.g_att + (g * G * D + e) / 2, gran(LL > 0.f ? pack2(O0 / LL, O1 / LL) : 0u, tagof(x.epoch, l, OP_ATT)));
   }
   cbar(x);
   return true;
@@ -621,7 +689,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     bf16_t* xs = reinterpret_cast<bf16_t*>(lds + L_XS);
     float* ssl = reinterpret_cast<float*>(lds + L_MISC);  // [256] gathered sums of squares
     constexpr int NT = H_ / 16;
-    const int att_g = pse_att_g(c, P);
+    const int att_u = pse_att_unit(c, P);
     // residual columns 16c .. 16c+15 owned by this CU: lanes 0..15 of wave 1 (bf16 values)
     float hres = (wave == LW && lane < 16) ? bf2f(a.h[c * 16 + lane]) : 0.f;
     float hsq = 0.f;
@@ -673,9 +741,9 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       }
       if (wave == LW) PSE_STAMP(l, 2);
       // ---------------- attention (one CU per KV head) ----------------
-      if (att_g >= 0) {
+      if (att_u >= 0) {
         // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
-        if (!attention(x, l, att_g, tq)) break;
+        if (!attention(x, l, att_u, tq)) break;
         if (wave == LW) PSE_STAMP(l, 3);
       }
       // ---------------- o_proj (+ residual) ----------------
@@ -770,7 +838,8 @@ int pse_grid(int device) {
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 + 64;
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + HKV_ * PSE_AU * (HQ_ / HKV_ * (D_ + 2)) + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 +
+         64;
 }
 
 hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
@@ -779,6 +848,7 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
   uint64_t* g = reinterpret_cast<uint64_t*>(ws);
   a.g_qkv = g; g += 768 * 16;
   a.g_att = g; g += HQ_ * D_ / 2;
+  a.g_attp = g; g += HKV_ * PSE_AU * (HQ_ / HKV_ * (D_ + 2));
   // h granules of an op immediately followed by its sums of squares: one gather range
   a.g_h[0] = g; g += H_ / 2;
   a.g_ss[0] = g; g += H_ / 16;

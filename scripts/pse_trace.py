@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from moss_tts_amd import _native as N  # noqa: E402
 
 NAMES = ["layer", "qkv in", "qkv done", "att done", "o in", "o done", "gu in", "gu done", "down in", "down done",
-         "L qkv", "L o", "L gu", "L down", "L end"]
+         "L qkv", "L o", "L gu", "L down", "L end", "A qkv in", "A chunks", "A chunks done", "A parts in"]
 
 
 def build(pse, layers):
@@ -46,7 +46,7 @@ def run(e, T, steps):
 
 
 layers = int(sys.argv[1]) if len(sys.argv) > 1 else 8
-T = 181
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 181
 eb = build(False, layers)
 print(f"per-op launches: decode forward {run(eb, T, 8):.3f} ms ({layers} layers)")
 eb.close()
@@ -54,14 +54,15 @@ e = build(True, layers)
 print(f"pse: decode forward {run(e, T, 8):.3f} ms ({layers} layers)")
 if os.environ.get("PSE_NO_TRACE") == "1":
     sys.exit(0)
-n = layers * 16 * 256
+EV = 20
+n = layers * EV * 256
 buf = (ctypes.c_uint64 * n)()
 N.check(N.load().mtts_pse_trace(e._h, buf, n), "trace")
-tr = np.frombuffer(buf, np.uint64).reshape(layers, 16, 256).astype(np.float64)
+tr = np.frombuffer(buf, np.uint64).reshape(layers, EV, 256).astype(np.float64)
 t0 = tr[0, 10][tr[0, 10] > 0].min()
 for l in list(range(min(layers, 4))) + [layers - 1]:
     row = []
-    for ev in range(15):
+    for ev in range(19):
         v = tr[l, ev]
         v = v[v > 0]
         if v.size:
