@@ -975,7 +975,8 @@ extern "C" int mtts_k_fill_uniform(uint16_t* dst, size_t n, uint64_t seed, uint6
 
 // ---------------------------------------------------------------------------
 // roofline probe: time one weight-streaming GEMV of the loaded model on the engine
-// stream with HIP events (which: 0 q|k|v, 1 o_proj, 2 gate|up (SwiGLU), 3 down, 4 heads)
+// stream with HIP events (which: 0 q|k|v, 1 o_proj, 2 gate|up (SwiGLU), 3 down, 4 heads,
+// 5 the persistent streaming decode stack of every layer, batch 1)
 extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B, int iters, float* avg_ms,
                                      uint64_t* alg_bytes) {
   if (!e || !avg_ms || !alg_bytes || iters <= 0) return fail(MTTS_E_INVALID, "null argument");
@@ -983,6 +984,43 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
   if (layer < 0 || layer >= c.layers || B <= 0 || B > c.max_batch) return fail(MTTS_E_INVALID, "bad layer/B");
   hipSetDevice(e->device);
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, I = c.inter;
+  if (which == 5) {
+    // the persistent streaming decode stack (pse.hip): ONE launch streams every layer, at the
+    // engine's current decode position `layer` ignored; the cached keys up to pos are read
+    if (e->lp || !(e->pse && e->pse_ok) || B != 1) return fail(MTTS_E_UNSUPPORTED, "persistent streaming decode inactive");
+    hipStream_t s = e->stream;
+    const Stack st = backbone_stack(e);
+    int pos = 0;
+    HIPCHK(hipMemcpy(&pos, &e->st->fwd_pos, sizeof(int), hipMemcpyDeviceToHost));
+    pos = std::min(std::max(pos, 0), c.max_ctx - 1);
+    HIPCHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(e->d_pos), pos, 1, s));
+    const int n_split = (c.max_ctx + CH_DECODE - 1) / CH_DECODE;
+    hipEvent_t a, b;
+    HIPCHK(hipEventCreate(&a));
+    HIPCHK(hipEventCreate(&b));
+    if (int rc = run_layers(e, st, 0, 1, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
+    HIPCHK(hipEventRecord(a, s));
+    for (int i = 0; i < iters; ++i)
+      if (int rc = run_layers(e, st, 0, 1, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
+    HIPCHK(hipEventRecord(b, s));
+    HIPCHK(hipEventSynchronize(b));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, a, b));
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    uint32_t err = 0;
+    HIPCHK(hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost));
+    if (err) {
+      hipMemset(pse_err_word(e->pse_ws), 0, 4);
+      return fail(MTTS_E_HIP, "persistent streaming decode: a wait timed out (timing invalid)");
+    }
+    *avg_ms = ms / iters;
+    // every layer's weights once + its K / V rows 0..pos read and row pos written
+    const uint64_t wl = 2ull * ((uint64_t)e->qkv_rows * H + (uint64_t)H * Hq * D + 3ull * I * H);
+    const uint64_t kv = 2ull * 2 * c.n_kv * D * (uint64_t)(pos + 1);
+    *alg_bytes = (uint64_t)st.layers * (wl + kv);
+    return 0;
+  }
   const LayerW& w = e->L[layer];
   hipStream_t s = e->stream;
   const bf16_t* W = nullptr;

@@ -114,7 +114,7 @@ struct mtts_engine {
   int mega_P = 0;                // workgroups (CUs); 0: unsupported here
   uint64_t* mega_trace = nullptr; // MTTS_MEGA_TRACE=1: per-stage timestamps of the last launch
   // persistent streaming engine (pse.hip) for the batch-1 decode stack: MTTS_PSE=1 (A/B)
-  bool pse = false;
+  bool pse = true;               // MTTS_PSE=0: per-op launches for batch-1 decode too
   bool pse_ok = false;           // the shape and the device support it
   PseLayer* pse_L = nullptr;     // device [layers]
   unsigned char* pse_ws = nullptr;  // pse_ws_bytes(), zero-filled

@@ -42,8 +42,16 @@ constexpr int CW = 4;                   // consumer waves
 #endif
 constexpr int LW = PSE_LW;              // loader waves (each its own vmcnt: 4 fills = 64 instructions)
 constexpr int THREADS = (LW + CW) * 64;
+// PSE_PF: slots the stalled loader touches ahead (L2 / Infinity Cache); PSE_THIN: one fill in
+// flight while the consumers gather (both measured slower, off)
+#ifndef PSE_PF
+#define PSE_PF 0
+#endif
+#ifndef PSE_THIN
+#define PSE_THIN 0
+#endif
 #ifndef PSE_NS
-#define PSE_NS 7
+#define PSE_NS 8
 #endif
 #ifndef PSE_FILLS
 #define PSE_FILLS 3
@@ -90,6 +98,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
                : "v"(gsrc), "s"(lds_byte)
                : "memory");
 }
+// LDS-DMA of one dword per lane (default cache policy) into the 256 B sink: brings the lane's
+// 64-B line into L2 / the Infinity Cache ahead of its fill
+__device__ __forceinline__ void touch4(const void* gsrc, uint32_t lds_byte) {
+  uint32_t save;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(save)
+               : "v"(gsrc), "s"(lds_byte)
+               : "memory");
+}
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
@@ -99,7 +116,7 @@ struct Ctl {
   int freed[CW];  // slots each consumer wave has finished reading
   int bar;        // consumer-only barrier counter (monotonic)
   int abort;      // a wait gave up: everyone drains
-  int pad;
+  int gath;       // the consumers are gathering: the loader keeps one fill in flight
   uint64_t lstamp[2][5];  // loader trace events of the last two layers (copied out by the consumers)
 };
 
@@ -110,11 +127,12 @@ constexpr uint32_t SPIN_MEM = 1u << 18;  // granule sweeps (~1-2 us each): ~0.3-
 constexpr int L_CTL = 0;
 constexpr int L_RING = 256;
 constexpr int L_XS = L_RING + NS * SLOT_KB * 1024;  // op input: 12288 bf16
-constexpr int L_RED = L_XS + I_ * 2;                // [CW][2][256] fp32 partial tiles
-constexpr int L_MISC = L_RED + CW * 2 * 256 * 4;    // [256] gathered sums of squares
+constexpr int L_RED = L_XS + I_ * 2;                // [CW][2][16] fp32: column 0 of the partial tiles
+constexpr int L_MISC = L_RED + CW * 2 * 16 * 4;     // [256] gathered sums of squares
 constexpr int PSE_MAXL = 64;                        // layers (weight pointer table in LDS)
 constexpr int L_PTR = L_MISC + 1024;
-constexpr int L_END = L_PTR + PSE_MAXL * 4 * 8;
+constexpr int L_PF = L_PTR + PSE_MAXL * 4 * 8;  // 256 B sink of the loader's prefetch touches
+constexpr int L_END = L_PF + (PSE_PF > 0 ? 256 : 0);
 // the attention CUs' scratch overlays the op input (q|k|v's input is dead once its slots are
 // consumed; o_proj's gather rewrites it after the attention): gathered q|k|v halves, then
 // q_s [16][D] bf16, k_s / v_s [D], p_s [CW][16][32] bf16, ml_s [CW][G][2], acc_s [CW][G][D]
@@ -181,15 +199,21 @@ __device__ __forceinline__ void cbar(Ctx& x) {
 // dst0, the rest to dst1; all consumer threads cooperate (n <= MAXP * 256) in ONE sweep loop (one
 // round trip per poll); false on timeout / abort.  Branch-free sc1 buffer loads (an out-of-range
 // offset reads zero): a load under a divergent branch would be waited for at once.
-template <int MAXP>
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <int MAXP, typename Hook = NoHook>
 __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_t t, uint32_t* dst0, int n0,
-                                       uint32_t* dst1 = nullptr) {
+                                       uint32_t* dst1 = nullptr, const Hook& after_first_issue = Hook()) {
   constexpr uint32_t OOB = 0x7ffffff0u;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(g), 0, n * 8, 0x00020000);
   uint32_t pend = 0;  // bit i: granule tid + i * 256 not seen yet
 #pragma unroll
   for (int i = 0; i < MAXP; ++i)
     if (x.tid + i * CW * 64 < n) pend |= 1u << i;
+  // the first sweep, then the caller's own loads (independent of the granules: they queue
+  // behind the sweep instead of delaying it, and the sweep's results are waited for alone)
+  if (PSE_THIN && x.tid == 0) __hip_atomic_store(&PSE_CTL->gath, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   bool ok = true;
   for (uint32_t spins = 0;; ++spins) {
     uint32_t lo[MAXP], hi[MAXP];
@@ -200,6 +224,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
       lo[i] = v[0];
       hi[i] = v[1];
     }
+    if (spins == 0) after_first_issue();
 #pragma unroll
     for (int i = 0; i < MAXP; ++i)
       if ((pend >> i & 1u) && hi[i] == t) {
@@ -217,6 +242,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     __builtin_amdgcn_s_sleep(1);
   }
   cbar(x);
+  if (PSE_THIN && x.tid == 0) __hip_atomic_store(&PSE_CTL->gath, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return ok && !failed(x);
 }
 
@@ -297,15 +323,15 @@ __device__ __forceinline__ void consume_slot(Ctx& x, int seq, int kt0, f32x4& ac
 // consumer barrier, then get(r, row) = the tile's output row (MFMA D layout: lane l holds rows
 // 4 (l >> 4) + i of column l & 15; column 0 = lanes 0, 16, 32, 48)
 __device__ __forceinline__ void red_put(Ctx& x, int r, const f32x4& acc) {
-  float* p = reinterpret_cast<float*>(pse_lds + L_RED) + ((x.wave - LW) * 2 + r) * 256 + x.lane * 4;
+  if (x.lane & 15) return;
+  float* p = reinterpret_cast<float*>(pse_lds + L_RED) + ((x.wave - LW) * 2 + r) * 16 + (x.lane >> 4) * 4;
   p[0] = acc[0]; p[1] = acc[1]; p[2] = acc[2]; p[3] = acc[3];
 }
 __device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
   const float* red = reinterpret_cast<const float*>(pse_lds + L_RED);
-  const int off = 64 * (row >> 2) + (row & 3);
   float s = 0.f;
 #pragma unroll
-  for (int w = 0; w < CW; ++w) s += red[(w * 2 + r) * 256 + off];
+  for (int w = 0; w < CW; ++w) s += red[(w * 2 + r) * 16 + row];
   return s;
 }
 
@@ -362,24 +388,27 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
   };
   u32x4 ktA[2][QS], vtA[DT];
   uint32_t mkA[2];
-  // this wave's chunks: ku CW + w, then every PSE_AU CW; the first one goes out before the
-  // q|k|v gather (the cached keys do not depend on it)
+  // this wave's chunks: ku CW + w, then every PSE_AU CW
   const int ch0 = ku * CW + w;
   constexpr int CSTEP = PSE_AU * CW;
-  load_chunk(ch0, ktA, vtA, mkA);
-  // and the prologue's other inputs: this wave's jobs' norm weights and the RoPE row at pos
-  // (2 dims per lane), also before the gather
+  // this wave's jobs' norm weights and the RoPE row at pos (2 dims per lane)
   constexpr int JW = (G + 2 + CW - 1) / CW;  // jobs per wave
   uint32_t pnw[JW], pcs = 0, psn = 0;
-#pragma unroll
-  for (int jj = 0; jj < JW; ++jj) {
-    const int j = w + jj * CW;
-    pnw[jj] = j <= G ? reinterpret_cast<const uint32_t*>(j < G ? Lw.q_norm : Lw.k_norm)[lane] : 0u;
-  }
-  pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
-  psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
+  // the first chunk and the prologue's inputs go out right behind the q|k|v gather's first
+  // sweep (the cached keys do not depend on it)
   constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the head's q|k|v granules
-  if (!gather<NG / (CW * 64)>(x, x.a.g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG))
+  auto prefetch = [&]() {
+    load_chunk(ch0, ktA, vtA, mkA);
+#pragma unroll
+    for (int jj = 0; jj < JW; ++jj) {
+      const int j = w + jj * CW;
+      pnw[jj] = j <= G ? reinterpret_cast<const uint32_t*>(j < G ? Lw.q_norm : Lw.k_norm)[lane] : 0u;
+    }
+    pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
+    psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
+  };
+  if (!gather<NG / (CW * 64)>(x, x.a.g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
+                              nullptr, prefetch))
     return false;
   const int c = x.c;
   if (w == 0) PSE_STAMP(l, 15);
@@ -626,6 +655,22 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     // published in full[k]
     const int k = wave;
     int marked = 0, m = 0;
+    // slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles
+    auto slot_src = [&](int s) -> const bf16_t* {
+      const int l = s / SPL, r = s - l * SPL;
+      if (r < 12) {  // q|k|v: unit 3c + r / 4 = (row tile, K half), 4 slots each
+        const int u = 3 * c + r / 4, t = u >> 1, half = u & 1;
+        return wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
+      } else if (r < 20) {  // o_proj row tile c, 8 slots
+        return wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
+      } else if (r < 68) {  // gate|up pairs 3c .. 3c+2: gate tile (8 slots), then up tile (8)
+        const int q = r - 20, pr = 3 * c + q / 16, rt = 2 * pr + (q % 16) / 8;
+        return wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
+      }
+      return wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;  // down row tile c, 24 slots
+    };
+    int pf = 0;  // next slot to touch ahead of its fill while the ring is full
+    const uint32_t sink = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid*)(lds + L_PF));
     for (int s = k; s < total; s += LW, ++m) {
       // ring slot s % NS is free once every consumer wave has read slot s - NS
       if (s >= NS) {
@@ -645,36 +690,42 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
             s = total;  // drain
             break;
           }
+          // the stream is idle: pull the next slots into L2 / the Infinity Cache (up to PSE_PF
+          // ahead of the one waiting for its ring slot), one slot per check
+          if (PSE_PF > 0) {
+            pf = max(pf, s);
+            if (pf < s + PSE_PF && pf < total) {
+              const char* p = reinterpret_cast<const char*>(slot_src(pf)) + lane * 64;
+#pragma unroll
+              for (int t = 0; t < SLOT_KB / 4; ++t) touch4(p + t * 4096, sink);
+              ++pf;
+              continue;
+            }
+          }
           __builtin_amdgcn_s_sleep(1);
         }
         if (s >= total) break;
       }
-      // this slot's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles
       const int l = s / SPL, r = s - l * SPL;
       if (a.trace && lane == 0) {  // loader events into LDS (global stores would join its vmcnt count)
         const int ev = r == 0 ? 0 : (r == 12 ? 1 : (r == 20 ? 2 : (r == 68 ? 3 : (r >= SPL - LW ? 4 : -1))));
         if (ev >= 0) ctl->lstamp[l & 1][ev] = __builtin_amdgcn_s_memrealtime();
       }
-      const bf16_t* src;
-      if (r < 12) {  // q|k|v: unit 3c + r / 4 = (row tile, K half), 4 slots each
-        const int u = 3 * c + r / 4, t = u >> 1, half = u & 1;
-        src = wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
-      } else if (r < 20) {  // o_proj row tile c, 8 slots
-        src = wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
-      } else if (r < 68) {  // gate|up pairs 3c .. 3c+2: gate tile (8 slots), then up tile (8)
-        const int q = r - 20, pr = 3 * c + q / 16, rt = 2 * pr + (q % 16) / 8;
-        src = wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
-      } else {  // down row tile c, 24 slots
-        src = wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;
-      }
+      const bf16_t* src = slot_src(s);
       const uint32_t dst = __builtin_amdgcn_readfirstlane(
           (uint32_t)(uintptr_t)(lvoid*)(lds + L_RING + (s % NS) * SLOT_KB * 1024));
       if (a.probe != 1) {
 #pragma unroll
         for (int t = 0; t < SLOT_KB; ++t) glds16(reinterpret_cast<const u32x4*>(src) + t * 64 + lane, dst + t * 1024);
       }
-      // keep FILLS - 1 of this wave's fills in flight behind this one; publish the older ones
-      if (m + 1 - marked >= FILLS) {
+      // keep FILLS - 1 of this wave's fills in flight behind this one (none while the consumers
+      // gather: their sweeps would queue behind the fills); publish the older ones
+      if (PSE_THIN && marked < m &&
+          __hip_atomic_load(&ctl->gath, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SLOT_KB) : "memory");
+        marked = m;
+        __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else if (m + 1 - marked >= FILLS) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((FILLS - 1) * SLOT_KB) : "memory");
         marked = m + 1 - (FILLS - 1);
         __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

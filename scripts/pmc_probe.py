@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Launch the bench's dominant kernel on its own (the decode step's gate|up GEMV instance, via
 mtts_engine_time_gemv: layers rotated, so no launch re-reads a matrix the previous one left in
-the 256 MB MALL) for rocprofv3 PMC passes:
+the 256 MB MALL; --config pse: the batch-1 persistent streaming decode launch, every layer) for
+rocprofv3 PMC passes:
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D -o f --output-format csv -- python3 scripts/pmc_probe.py --config clone
     rocprofv3 --pmc WRITE_SIZE --kernel-trace -d D -o w --output-format csv -- python3 scripts/pmc_probe.py --config clone
@@ -35,8 +36,13 @@ def run(cfg_name, iters):
         B = 1
     eng = Engine(cfg, 0)
     eng.init_random(0)
+    which = 2
+    if cfg_name == "pse":  # the batch-1 decode stack as one persistent launch (pse.hip)
+        if not eng.pse_active():
+            raise SystemExit("persistent streaming decode inactive")
+        which = 5
     ms, nb = ctypes.c_float(), ctypes.c_uint64()
-    N.check(N.load().mtts_engine_time_gemv(eng._h, 2, 0, B, iters, ctypes.byref(ms), ctypes.byref(nb)), "time_gemv")
+    N.check(N.load().mtts_engine_time_gemv(eng._h, which, 0, B, iters, ctypes.byref(ms), ctypes.byref(nb)), "time_gemv")
     torch.cuda.synchronize()
     print(json.dumps({"avg_launch_us": ms.value * 1e3, "alg_bytes": nb.value, "B": B}))
     eng.close()
@@ -46,7 +52,7 @@ def summarize(d, cfg_name):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "gemv_kernel" not in r["Kernel_Name"]:
+            if ("pse_kernel" if cfg_name == "pse" else "gemv_kernel") not in r["Kernel_Name"]:
                 continue
             vals.setdefault(r["Counter_Name"], {}).setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     out = {"config": cfg_name, "unit_raw": "KiB (rocprofv3 FETCH_SIZE / WRITE_SIZE)"}
@@ -64,7 +70,7 @@ def summarize(d, cfg_name):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["clone", "local"], default="clone")
+    ap.add_argument("--config", choices=["clone", "local", "pse"], default="clone")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--summarize", default=None)
     a = ap.parse_args()

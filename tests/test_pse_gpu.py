@@ -16,11 +16,11 @@ torch = pytest.importorskip("torch")
 LAYERS = 3
 
 
-def make(pse, max_ctx=768):
+def make(pse, max_ctx=768, max_prefill=1024):
     from moss_tts_amd.engine import Engine, EngineConfig
     os.environ["MTTS_PSE"] = "1" if pse else "0"
     try:
-        e = Engine(EngineConfig(layers=LAYERS, max_batch=1, max_ctx=max_ctx, max_prefill_tokens=1024), 0)
+        e = Engine(EngineConfig(layers=LAYERS, max_batch=1, max_ctx=max_ctx, max_prefill_tokens=max_prefill), 0)
     finally:
         os.environ.pop("MTTS_PSE")
     e.init_random(seed=3)
@@ -58,12 +58,7 @@ def decode_logits(eng, ids, mask, T, steps):
     return out
 
 
-@pytest.mark.parametrize("T,steps", [(150, 12), (611, 20)])
-def test_pse_decode_logits_match_launches(engines, T, steps):
-    ref, pse = engines
-    ids, mask = prompt(T, steps, T)
-    want = decode_logits(ref, ids, mask, T, steps)
-    got = decode_logits(pse, ids, mask, T, steps)
+def check_logits(ref, want, got):
     V, A = ref.cfg.vocab, 1025
     for s, (w, g) in enumerate(zip(want, got)):
         for j in range(33):
@@ -74,6 +69,30 @@ def test_pse_decode_logits_match_launches(engines, T, steps):
             scale = np.abs(wr[fin]).max()
             err = np.abs(gr[fin] - wr[fin]).max()
             assert err <= 8 * ulp_bf16(scale), (s, j, float(err), float(scale))
+
+
+@pytest.mark.parametrize("T,steps,pad", [(150, 12, 0), (611, 20, 0), (300, 8, 37)])
+def test_pse_decode_logits_match_launches(engines, T, steps, pad):
+    """pad: left-padded prompt (mask 0 on the first pad positions; the keys must be masked out)"""
+    ref, pse = engines
+    ids, mask = prompt(T, steps, T)
+    mask[0, :pad] = 0
+    check_logits(ref, decode_logits(ref, ids, mask, T, steps), decode_logits(pse, ids, mask, T, steps))
+
+
+def test_pse_long_context():
+    """Thousands of cached keys: every attention wave runs several 32-key chunks"""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    ref, pse = make(False, 4096, 4096), make(True, 4096, 4096)
+    try:
+        if not pse.pse_active():
+            pytest.skip("persistent streaming decode unsupported on this device")
+        ids, mask = prompt(3500, 3, 5)
+        check_logits(ref, decode_logits(ref, ids, mask, 3500, 3), decode_logits(pse, ids, mask, 3500, 3))
+    finally:
+        ref.close()
+        pse.close()
 
 
 def test_pse_deterministic(engines):
