@@ -104,10 +104,13 @@ int mtts_heads_ld(const mtts_engine* eng);
  * shape it does not cover). */
 int mtts_mega_workgroups(const mtts_engine* eng);
 /* 1 when batch-1 decode steps run the decoder stack as one persistent launch with run-ahead
- * weight streaming (MTTS_PSE=1 at creation, MossTTSDelay-8B shape, 256 CUs), else 0 */
+ * weight streaming (default; MTTS_PSE=0 at creation turns it off; MossTTSDelay-8B shape,
+ * 256 CUs), else 0.  It is taken by a generation whose prompt + max_new tokens, or a
+ * teacher-forced forward whose past + S, stays within mtts_pse_ctx_max (MTTS_PSE_CTX). */
 int mtts_pse_active(const mtts_engine* eng);
+int mtts_pse_ctx_max(const mtts_engine* eng);
 /* per-layer event stamps (s_memrealtime, 100 MHz) of the last persistent streaming launch:
- * [layers][16][256 workgroups] (engine created with MTTS_PSE_TRACE=1; see pse.hip) */
+ * [layers][20][256 workgroups] (engine created with MTTS_PSE_TRACE=1; see pse.hip) */
 int mtts_pse_trace(mtts_engine* eng, uint64_t* host, size_t n);
 /* 1 when a decode step of B rows runs attention + o_proj + residual as one launch per layer
  * (ao.hip: B == 1, head_dim 128, KV capacity <= 2048, engine created with MTTS_AO=1), else 0. */

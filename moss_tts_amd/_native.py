@@ -71,6 +71,7 @@ _SIGS = {
     "mtts_heads_ld": (I, [P]),
     "mtts_mega_workgroups": (I, [P]),
     "mtts_pse_active": (I, [P]),
+    "mtts_pse_ctx_max": (I, [P]),
     "mtts_pse_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),
     "mtts_attn_o_active": (I, [P, I]),
     "mtts_qkv_attn_active": (I, [P, I]),

@@ -171,6 +171,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
   if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE")) e->pse = v[0] == '1';
+  if (const char* v = getenv("MTTS_PSE_CTX")) e->pse_ctx_max = atoi(v);
   if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
   if (const char* v = getenv("MTTS_QA")) e->qa = v[0] == '1';
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
@@ -251,6 +252,7 @@ extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
 }
 extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
 extern "C" int mtts_pse_active(const mtts_engine* e) { return e && e->pse && e->pse_ok ? 1 : 0; }
+extern "C" int mtts_pse_ctx_max(const mtts_engine* e) { return e && e->pse && e->pse_ok ? e->pse_ctx_max : 0; }
 extern "C" int mtts_mega_workgroups(const mtts_engine* e) {
   return e && e->mega && e->c.head_dim == 128 ? e->mega_P : 0;
 }
@@ -504,7 +506,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   const int M = B * S;
   const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
   const float eps = e->c.rms_eps;
-  if (S == 1 && B == 1 && b0 == 0 && e->pse && e->pse_ok && st.cos_t && st.L == e->L.data()) {
+  if (S == 1 && B == 1 && b0 == 0 && e->pse && e->pse_ok && e->pse_now && st.cos_t && st.L == e->L.data()) {
     // the whole stack as one persistent launch with run-ahead weight streaming (pse.hip)
     PseArgs pa{};
     pa.L = e->pse_L; pa.layers = st.layers; pa.h = st.h; pa.ss = st.ss; pa.cos_t = st.cos_t; pa.sin_t = st.sin_t;
@@ -736,6 +738,7 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   if (B <= 0 || B > c.max_batch || S <= 0 || past < 0 || past + S > c.max_ctx) return fail(MTTS_E_INVALID, "bad B/S/past");
   hipStream_t s = enter(e, stream);
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
+  e->pse_choose(past + S);
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
   leave(e, stream);
   return rc;
@@ -787,6 +790,7 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(e->seen, 0, 2 * e->audio_rows, s));
   HIPCHK(gen_init(e->bufs(), ids, mask, s));
+  e->pse_choose(T + max_new);
   int rc = forward_chunked(e, ids, B, T, 0, e->logits, s);
   if (rc) return rc;
   HIPCHK(sample_step(e->bufs(), B, c.n_vq, TEXT_PARTS, s));
@@ -804,7 +808,9 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   // every step-dependent value is read from device state, so one graph serves all steps
   auto it = e->graphs.find(e->gen_B);
   hipGraphExec_t exec = nullptr;
-  if (it != e->graphs.end() && it->second.forced == e->forced) {
+  // the PSE path is baked into the graph: taken when the whole generation fits its context range
+  e->pse_choose(e->gen_T + e->gen_max_new);
+  if (it != e->graphs.end() && it->second.forced == e->forced && it->second.pse == e->pse_now) {
     exec = it->second.exec;
   } else {
     if (it != e->graphs.end()) {
@@ -819,7 +825,7 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
     if (ce != hipSuccess) return fail(MTTS_E_HIP, std::string("capture: ") + hipGetErrorString(ce));
     HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
     hipGraphDestroy(graph);
-    e->graphs[e->gen_B] = mtts_engine::Graph{exec, e->forced};
+    e->graphs[e->gen_B] = mtts_engine::Graph{exec, e->forced, e->pse_now};
   }
   for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
     HIPCHK(hipGraphLaunch(exec, s));
@@ -998,6 +1004,7 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
+    e->pse_now = true;
     if (int rc = run_layers(e, st, 0, 1, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
     HIPCHK(hipEventRecord(a, s));
     for (int i = 0; i < iters; ++i)

@@ -115,6 +115,11 @@ struct mtts_engine {
   uint64_t* mega_trace = nullptr; // MTTS_MEGA_TRACE=1: per-stage timestamps of the last launch
   // persistent streaming engine (pse.hip) for the batch-1 decode stack: MTTS_PSE=1 (A/B)
   bool pse = true;               // MTTS_PSE=0: per-op launches for batch-1 decode too
+  int pse_ctx_max = 448;         // PSE only while the context stays within this (MTTS_PSE_CTX):
+                                 // its attention (2 CUs per KV head) loses to the per-op
+                                 // split-K attention beyond ~500 cached keys
+  bool pse_now = false;          // this forward / captured decode step may take the PSE path
+  void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
   bool pse_ok = false;           // the shape and the device support it
   PseLayer* pse_L = nullptr;     // device [layers]
   unsigned char* pse_ws = nullptr;  // pse_ws_bytes(), zero-filled
@@ -128,7 +133,7 @@ struct mtts_engine {
   float* part_val = nullptr;
   const int* forced = nullptr;
   int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
-  struct Graph { hipGraphExec_t exec; const int* forced; };
+  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };
   std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
   std::vector<void*> allocs;      // weights
   std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)

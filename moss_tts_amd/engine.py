@@ -139,6 +139,10 @@ class Engine:
         """Whether batch-1 decode steps run the decoder stack as one persistent launch (pse.hip)."""
         return bool(N.load().mtts_pse_active(self._h))
 
+    def pse_ctx_max(self) -> int:
+        """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
+        return int(N.load().mtts_pse_ctx_max(self._h))
+
     def attn_o_active(self, batch: int) -> bool:
         """Whether a decode step of `batch` rows runs attention + o_proj as one launch (ao.hip)."""
         return bool(N.load().mtts_attn_o_active(self._h, batch))

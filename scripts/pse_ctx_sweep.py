@@ -13,6 +13,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def build(pse, max_ctx):
     from moss_tts_amd.engine import Engine, EngineConfig
     os.environ["MTTS_PSE"] = "1" if pse else "0"
+    os.environ.setdefault("MTTS_PSE_CTX", "1000000")  # the kernel at every length (no gate)
     e = Engine(EngineConfig(max_batch=1, max_ctx=max_ctx, max_prefill_tokens=2048), 0)
     e.init_random(seed=0)
     return e

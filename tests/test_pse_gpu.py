@@ -16,13 +16,17 @@ torch = pytest.importorskip("torch")
 LAYERS = 3
 
 
-def make(pse, max_ctx=768, max_prefill=1024):
+def make(pse, max_ctx=768, max_prefill=1024, ctx_limit=1 << 20):
+    """ctx_limit: the PSE context range (MTTS_PSE_CTX; unlimited here to test the kernel itself)"""
     from moss_tts_amd.engine import Engine, EngineConfig
     os.environ["MTTS_PSE"] = "1" if pse else "0"
+    if ctx_limit is not None:
+        os.environ["MTTS_PSE_CTX"] = str(ctx_limit)
     try:
         e = Engine(EngineConfig(layers=LAYERS, max_batch=1, max_ctx=max_ctx, max_prefill_tokens=max_prefill), 0)
     finally:
         os.environ.pop("MTTS_PSE")
+        os.environ.pop("MTTS_PSE_CTX", None)
     e.init_random(seed=3)
     return e
 
@@ -133,3 +137,21 @@ def test_pse_generate_matches_launches(engines):
         row = lg[:V] if j == 0 else lg[V + (j - 1) * A: V + j * A - 1]
         top = np.sort(row[np.isfinite(row)])[-2:]
         assert top[1] - top[0] <= 8 * ulp_bf16(np.abs(top[1])), (r, int(j), top)
+
+
+def test_pse_context_gate(engines):
+    """The default engine takes the PSE path only within its context range: beyond it a decode
+    forward is the per-op launches' (bit-identical), within it the PSE one (within the band)"""
+    ref, _ = engines
+    dflt = make(True, ctx_limit=None)
+    try:
+        lim = dflt.pse_ctx_max()
+        assert 0 < lim < 700
+        ids, mask = prompt(lim + 20, 2, 9)
+        want = decode_logits(ref, ids, mask, lim + 20, 2)
+        got = decode_logits(dflt, ids, mask, lim + 20, 2)
+        assert all(np.array_equal(w, g) for w, g in zip(want, got))
+        ids, mask = prompt(lim - 40, 2, 9)
+        check_logits(ref, decode_logits(ref, ids, mask, lim - 40, 2), decode_logits(dflt, ids, mask, lim - 40, 2))
+    finally:
+        dflt.close()
