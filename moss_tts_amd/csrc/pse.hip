@@ -47,6 +47,9 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_PF
 #define PSE_PF 0
 #endif
+#ifndef PSE_APAUSE
+#define PSE_APAUSE 2
+#endif
 #ifndef PSE_THIN
 #define PSE_THIN 0
 #endif
@@ -117,6 +120,7 @@ struct Ctl {
   int bar;        // consumer-only barrier counter (monotonic)
   int abort;      // a wait gave up: everyone drains
   int gath;       // the consumers are gathering: the loader keeps one fill in flight
+  int apause;     // attention gathering its inputs: the loader issues nothing
   uint64_t lstamp[2][5];  // loader trace events of the last two layers (copied out by the consumers)
 };
 
@@ -407,6 +411,7 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
     pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
     psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
   };
+  if (PSE_APAUSE && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (!gather<NG / (CW * 64)>(x, x.a.g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
                               nullptr, prefetch))
     return false;
@@ -552,6 +557,7 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
+  if (PSE_APAUSE == 1 && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (w == 0) PSE_STAMP(l, 16);
   for (int ch = ch0; ch < nchunk; ch += CSTEP) {
     if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
@@ -706,6 +712,18 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         }
         if (s >= total) break;
       }
+      // this CU's attention is gathering its inputs: no new fills (its sweeps and chunk loads
+      // would queue behind them); retire the ones in flight
+      if (PSE_APAUSE && __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        marked = m;
+        __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (uint32_t spins = 0; __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                                 !__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                                 spins < SPIN_LDS;
+             ++spins)
+          __builtin_amdgcn_s_sleep(1);
+      }
       const int l = s / SPL, r = s - l * SPL;
       if (a.trace && lane == 0) {  // loader events into LDS (global stores would join its vmcnt count)
         const int ev = r == 0 ? 0 : (r == 12 ? 1 : (r == 20 ? 2 : (r == 68 ? 3 : (r >= SPL - LW ? 4 : -1))));
@@ -794,7 +812,10 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       // ---------------- attention (one CU per KV head) ----------------
       if (att_u >= 0) {
         // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
-        if (!attention(x, l, att_u, tq)) break;
+        const bool att_ok = attention(x, l, att_u, tq);
+        if (PSE_APAUSE == 2 && x.tid == 0)  // (PSE_APAUSE 2: the loader waits out the whole attention)
+          __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (!att_ok) break;
         if (wave == LW) PSE_STAMP(l, 3);
       }
       // ---------------- o_proj (+ residual) ----------------
