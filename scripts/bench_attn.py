@@ -11,7 +11,7 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from moss_tts_amd import _native as N
     L = N.load()
-    B, Hq, Hkv, D, Cmax = int(sys.argv[3]), 32, 8, 128, 4096
+    B, Hq, Hkv, D, Cmax = int(sys.argv[3]), 32, 8, 128, int(os.environ.get("CMAX", "4096"))
     pos = int(sys.argv[2])
     P = lambda t: ctypes.c_void_p(t.data_ptr())
     qkv = torch.randn(B, (Hq + 2 * Hkv) * D, device="cuda").bfloat16()
@@ -38,9 +38,9 @@ if len(sys.argv) > 1 and sys.argv[1] == "--child":
     sys.exit(0)
 
 for pos in [int(x) for x in sys.argv[1:]] or [100, 389, 1000, 3000]:
-  for nwv in ("4", "8", "16"):
-    for B in (1, 4):
-        for probe in ("3", "0"):
+  for nwv in os.environ.get("NWVS", "4,8,16").split(","):
+    for B in [int(b) for b in os.environ.get("BS", "1,4").split(",")]:
+        for probe in os.environ.get("PROBES", "3,0").split(","):
             env = dict(os.environ, MTTS_ATTN_PROBE=probe, MTTS_ATTN_NWV=nwv)
             r = subprocess.run([sys.executable, __file__, "--child", str(pos), str(B)], env=env, capture_output=True,
                                text=True, timeout=300)
