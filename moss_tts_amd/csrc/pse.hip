@@ -42,16 +42,8 @@ constexpr int CW = 4;                   // consumer waves
 #endif
 constexpr int LW = PSE_LW;              // loader waves (each its own vmcnt: 4 fills = 64 instructions)
 constexpr int THREADS = (LW + CW) * 64;
-// PSE_PF: slots the stalled loader touches ahead (L2 / Infinity Cache); PSE_THIN: one fill in
-// flight while the consumers gather (both measured slower, off)
-#ifndef PSE_PF
-#define PSE_PF 0
-#endif
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
-#endif
-#ifndef PSE_THIN
-#define PSE_THIN 0
 #endif
 #ifndef PSE_NS
 #define PSE_NS 8
@@ -101,15 +93,6 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
                : "v"(gsrc), "s"(lds_byte)
                : "memory");
 }
-// LDS-DMA of one dword per lane (default cache policy) into the 256 B sink: brings the lane's
-// 64-B line into L2 / the Infinity Cache ahead of its fill
-__device__ __forceinline__ void touch4(const void* gsrc, uint32_t lds_byte) {
-  uint32_t save;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(save)
-               : "v"(gsrc), "s"(lds_byte)
-               : "memory");
-}
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
@@ -119,7 +102,6 @@ struct Ctl {
   int freed[CW];  // slots each consumer wave has finished reading
   int bar;        // consumer-only barrier counter (monotonic)
   int abort;      // a wait gave up: everyone drains
-  int gath;       // the consumers are gathering: the loader keeps one fill in flight
   int apause;     // attention gathering its inputs: the loader issues nothing
   uint64_t lstamp[2][5];  // loader trace events of the last two layers (copied out by the consumers)
 };
@@ -135,8 +117,7 @@ constexpr int L_RED = L_XS + I_ * 2;                // [CW][2][16] fp32: column 
 constexpr int L_MISC = L_RED + CW * 2 * 16 * 4;     // [256] gathered sums of squares
 constexpr int PSE_MAXL = 64;                        // layers (weight pointer table in LDS)
 constexpr int L_PTR = L_MISC + 1024;
-constexpr int L_PF = L_PTR + PSE_MAXL * 4 * 8;  // 256 B sink of the loader's prefetch touches
-constexpr int L_END = L_PF + (PSE_PF > 0 ? 256 : 0);
+constexpr int L_END = L_PTR + PSE_MAXL * 4 * 8;
 // the attention CUs' scratch overlays the op input (q|k|v's input is dead once its slots are
 // consumed; o_proj's gather rewrites it after the attention): gathered q|k|v halves, then
 // q_s [16][D] bf16, k_s / v_s [D], p_s [CW][16][32] bf16, ml_s [CW][G][2], acc_s [CW][G][D]
@@ -217,7 +198,6 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     if (x.tid + i * CW * 64 < n) pend |= 1u << i;
   // the first sweep, then the caller's own loads (independent of the granules: they queue
   // behind the sweep instead of delaying it, and the sweep's results are waited for alone)
-  if (PSE_THIN && x.tid == 0) __hip_atomic_store(&PSE_CTL->gath, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   bool ok = true;
   for (uint32_t spins = 0;; ++spins) {
     uint32_t lo[MAXP], hi[MAXP];
@@ -246,7 +226,6 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     __builtin_amdgcn_s_sleep(1);
   }
   cbar(x);
-  if (PSE_THIN && x.tid == 0) __hip_atomic_store(&PSE_CTL->gath, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   return ok && !failed(x);
 }
 
@@ -675,8 +654,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       }
       return wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;  // down row tile c, 24 slots
     };
-    int pf = 0;  // next slot to touch ahead of its fill while the ring is full
-    const uint32_t sink = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lvoid*)(lds + L_PF));
     for (int s = k; s < total; s += LW, ++m) {
       // ring slot s % NS is free once every consumer wave has read slot s - NS
       if (s >= NS) {
@@ -695,18 +672,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
             st32(a.err, 1u);
             s = total;  // drain
             break;
-          }
-          // the stream is idle: pull the next slots into L2 / the Infinity Cache (up to PSE_PF
-          // ahead of the one waiting for its ring slot), one slot per check
-          if (PSE_PF > 0) {
-            pf = max(pf, s);
-            if (pf < s + PSE_PF && pf < total) {
-              const char* p = reinterpret_cast<const char*>(slot_src(pf)) + lane * 64;
-#pragma unroll
-              for (int t = 0; t < SLOT_KB / 4; ++t) touch4(p + t * 4096, sink);
-              ++pf;
-              continue;
-            }
           }
           __builtin_amdgcn_s_sleep(1);
         }
@@ -736,14 +701,8 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
 #pragma unroll
         for (int t = 0; t < SLOT_KB; ++t) glds16(reinterpret_cast<const u32x4*>(src) + t * 64 + lane, dst + t * 1024);
       }
-      // keep FILLS - 1 of this wave's fills in flight behind this one (none while the consumers
-      // gather: their sweeps would queue behind the fills); publish the older ones
-      if (PSE_THIN && marked < m &&
-          __hip_atomic_load(&ctl->gath, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SLOT_KB) : "memory");
-        marked = m;
-        __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      } else if (m + 1 - marked >= FILLS) {
+      // keep FILLS - 1 of this wave's fills in flight behind this one; publish the older ones
+      if (m + 1 - marked >= FILLS) {
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"((FILLS - 1) * SLOT_KB) : "memory");
         marked = m + 1 - (FILLS - 1);
         __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
