@@ -76,6 +76,10 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   // MTTS_GEMV_PIPE bit 0 / bit 1 flips the batch depth (8 <-> 4 k-tiles) for <= 16 / > 16 rows
   static const int pipe = getenv("MTTS_GEMV_PIPE") ? atoi(getenv("MTTS_GEMV_PIPE")) : 0;
   bool u4 = (NB == 1 && (pipe & 1)) || (NB == 2 && !(pipe & 2));
+  // gate|up at K <= 2048 (the MossTTSLocal backbone, depth stack and adapters): 4-deep batches,
+  // i.e. more resident waves per CU (its roofline GEMV 12.9 -> 11.4 us, frame 9.11 -> 8.66 ms);
+  // at K 4096 (MossTTSDelay) the 8-deep batches stay faster (B=4 3.32 vs 3.47 ms/step)
+  if (EPI == EPI_SWIGLU && NB == 1 && a.KT <= 64 && !(pipe & 1)) u4 = true;
   if (a.force_u == 4 || a.force_u == 8) u4 = a.force_u == 4;
   if (u4) {
     if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
