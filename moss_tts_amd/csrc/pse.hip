@@ -42,6 +42,9 @@ constexpr int CW = 4;                   // consumer waves
 #endif
 constexpr int LW = PSE_LW;              // loader waves (each its own vmcnt: 4 fills = 64 instructions)
 constexpr int THREADS = (LW + CW) * 64;
+#ifndef PSE_POLL_SLEEP
+#define PSE_POLL_SLEEP 1  // s_sleep count between a gather's sweeps (x 64 cycles)
+#endif
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
@@ -223,7 +226,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
       ok = false;
       break;
     }
-    __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_s_sleep(PSE_POLL_SLEEP);
   }
   cbar(x);
   return ok && !failed(x);
