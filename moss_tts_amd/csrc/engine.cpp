@@ -495,6 +495,16 @@ hipError_t proj(mtts_engine* e, const GemvArgs& g, int epi, hipStream_t s) {
     if (S > 1 && tiles <= SK_TILES && gemv_splitk_ws_floats(tiles, S) <= SK_PART_FLOATS)
       return gemv_splitk(g, S, e->sk_part, e->sk_cnt, s);
   }
+  // 17-32 packed rows (B = 32 decode o_proj / down_proj): row tiles share the x fragments,
+  // K split to keep the grid full (splitk.hip)
+  if (epi == EPI_RESADD && e->splitk && e->sk_part && g.res && !g.ss_in && !g.attn.part && !g.gate && !g.tile0 &&
+      g.x_packed) {
+    const int tiles = (g.N + 15) / 16;
+    int RT = 0, S = 0;
+    if (gemv_splitk2_pick(tiles, g.K / 32, g.B, &RT, &S) && tiles / RT <= SK_TILES &&
+        gemv_splitk2_ws_floats(tiles, S) <= SK_PART_FLOATS)
+      return gemv_splitk2(g, RT, S, e->sk_part, e->sk_cnt, s);
+  }
   return gemv_ex(g, epi, s);
 }
 

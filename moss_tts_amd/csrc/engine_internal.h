@@ -56,7 +56,7 @@ struct Stack {
 
 constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip
 constexpr int SK_TILES = 256;                   // split-K GEMV: most output tiles, and
-constexpr size_t SK_PART_FLOATS = 1024 * 256;   // its partial workspace (tiles x splits x 256)
+constexpr size_t SK_PART_FLOATS = 4096 * 256;   // its partial workspace (tiles x splits x 256; x 2 rows halves)
 constexpr size_t GK_WS_FLOATS = 8u << 20;       // prefill GEMM split-K partials (32 MB)
 
 inline size_t packed_bytes(int rows, int K) { return (size_t)((rows + 15) / 16) * 16 * K * sizeof(bf16_t); }

@@ -256,6 +256,11 @@ hipError_t attn_o(const AOArgs& a, hipStream_t s);
 int gemv_splitk_splits(int n_tiles, int KT, int B);
 size_t gemv_splitk_ws_floats(int n_tiles, int S);
 hipError_t gemv_splitk(const GemvArgs& a, int S, float* part, int* cnt, hipStream_t s);
+// 17-32 packed rows: RT row tiles per workgroup, K split S ways (o_proj / down_proj at B = 32);
+// part: gemv_splitk2_ws_floats(n_tiles, S), cnt: n_tiles / RT zeroed ints
+bool gemv_splitk2_pick(int n_tiles, int KT, int B, int* RT, int* S);
+size_t gemv_splitk2_ws_floats(int n_tiles, int S);
+hipError_t gemv_splitk2(const GemvArgs& a, int RT, int S, float* part, int* cnt, hipStream_t s);
 
 // qa.hip: the q|k|v GEMV (fused input RMSNorm) and the decode attention as one launch (block
 // attention units prefetch K / V, then wait for the projection); sync = 16 zeroed ints owned
