@@ -23,7 +23,9 @@
 // Work split per layer (CU c of P = 256): q|k|v = 768 half tiles (row tile, K half), 3 per CU;
 // o_proj and down = row tile c (CU c owns residual columns 16c..16c+15 for the whole step);
 // gate|up = tile pairs 3c..3c+2.  92 slots (1.47 MB) per CU per layer.  The attention of KV
-// head g runs on the consumers of CU pse_att_cu(g) (its loader keeps streaming meanwhile).
+// head g runs on the consumers of PSE_AU CUs (pse_att_unit: unit k takes every PSE_AU-th group
+// of chunks, unit 0 merges), whose loaders pause while it runs (PSE_APAUSE).  The engine takes
+// this launch only for contexts up to its PSE range (engine.cpp pse_choose).
 //
 // Hand-offs: data-tagged granules (MI355X_MICROARCH.md "handoff-1to1" / "allgather"): 8 bytes
 // {32-bit payload, 32-bit tag} written by ONE write-through (sc1) store and read with sc1 loads;
