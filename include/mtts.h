@@ -105,8 +105,9 @@ int mtts_heads_ld(const mtts_engine* eng);
 int mtts_mega_workgroups(const mtts_engine* eng);
 /* 1 when batch-1 decode steps run the decoder stack as one persistent launch with run-ahead
  * weight streaming (default; MTTS_PSE=0 at creation turns it off; MossTTSDelay-8B shape,
- * 256 CUs), else 0.  It is taken by a generation whose prompt + max_new tokens, or a
- * teacher-forced forward whose past + S, stays within mtts_pse_ctx_max (MTTS_PSE_CTX). */
+ * 256 CUs), else 0.  It is taken by the decode steps of a generation (and teacher-forced
+ * forwards) whose context stays within mtts_pse_ctx_max (MTTS_PSE_CTX); later steps of the
+ * same generation take the per-op launches. */
 int mtts_pse_active(const mtts_engine* eng);
 int mtts_pse_ctx_max(const mtts_engine* eng);
 /* per-layer event stamps (s_memrealtime, 100 MHz) of the last persistent streaming launch:

@@ -800,7 +800,7 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(e->seen, 0, 2 * e->audio_rows, s));
   HIPCHK(gen_init(e->bufs(), ids, mask, s));
-  e->pse_choose(T + max_new);
+  e->pse_choose(T);  // (a prefill takes the launch only as a one-token prompt)
   int rc = forward_chunked(e, ids, B, T, 0, e->logits, s);
   if (rc) return rc;
   HIPCHK(sample_step(e->bufs(), B, c.n_vq, TEXT_PARTS, s));
@@ -815,29 +815,37 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   if (e->gen_B <= 0) return fail(MTTS_E_INVALID, "generate_begin not called");
   hipStream_t s = enter(e, stream);
   // the graph bakes the kernel arguments (buffers, B, the forced-schedule pointer);
-  // every step-dependent value is read from device state, so one graph serves all steps
-  auto it = e->graphs.find(e->gen_B);
-  hipGraphExec_t exec = nullptr;
-  // the PSE path is baked into the graph: taken when the whole generation fits its context range
-  e->pse_choose(e->gen_T + e->gen_max_new);
-  if (it != e->graphs.end() && it->second.forced == e->forced && it->second.pse == e->pse_now) {
-    exec = it->second.exec;
-  } else {
+  // every step-dependent value is read from device state, so one graph serves all steps --
+  // one per path: the persistent streaming launch (pse.hip) while the context stays in its
+  // range, the per-op launches beyond (the choice is per step, from the host's step count)
+  auto graph_for = [&](bool pse, hipGraphExec_t* exec) -> int {
+    const int key = e->gen_B * 2 + (pse ? 1 : 0);
+    auto it = e->graphs.find(key);
+    if (it != e->graphs.end() && it->second.forced == e->forced) {
+      *exec = it->second.exec;
+      return 0;
+    }
     if (it != e->graphs.end()) {
       hipGraphExecDestroy(it->second.exec);
       e->graphs.erase(it);
     }
+    e->pse_now = pse;
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = decode_step_launch(e, s);
     hipError_t ce = hipStreamEndCapture(s, &graph);
     if (rc) return rc;
     if (ce != hipSuccess) return fail(MTTS_E_HIP, std::string("capture: ") + hipGetErrorString(ce));
-    HIPCHK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    HIPCHK(hipGraphInstantiate(exec, graph, nullptr, nullptr, 0));
     hipGraphDestroy(graph);
-    e->graphs[e->gen_B] = mtts_engine::Graph{exec, e->forced, e->pse_now};
-  }
+    e->graphs[key] = mtts_engine::Graph{*exec, e->forced, pse};
+    return 0;
+  };
   for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
+    // context of this step <= prompt + steps so far + 1
+    const bool pse = e->pse && e->pse_ok && e->gen_B == 1 && e->gen_T + e->steps_issued + 1 <= e->pse_ctx_max;
+    hipGraphExec_t exec = nullptr;
+    if (int rc = graph_for(pse, &exec)) return rc;
     HIPCHK(hipGraphLaunch(exec, s));
     ++e->steps_issued;
   }

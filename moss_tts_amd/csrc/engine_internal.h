@@ -133,7 +133,7 @@ struct mtts_engine {
   float* part_val = nullptr;
   const int* forced = nullptr;
   int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
-  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };
+  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };  // key: 2 B + pse
   std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
   std::vector<void*> allocs;      // weights
   std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)

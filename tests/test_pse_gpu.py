@@ -155,3 +155,38 @@ def test_pse_context_gate(engines):
         check_logits(ref, decode_logits(ref, ids, mask, lim - 40, 2), decode_logits(dflt, ids, mask, lim - 40, 2))
     finally:
         dflt.close()
+
+
+def test_pse_generation_crosses_the_context_range(engines):
+    """A generation longer than the PSE range switches to the per-op launches mid-way (per
+    decode step); its ids must match the per-op engine's (or diverge first at a bf16 near-tie)"""
+    from moss_tts_amd.engine import sampling_params
+    ref, _ = engines
+    part = make(True, ctx_limit=150)
+    try:
+        assert part.pse_ctx_max() == 150
+        ids, mask = prompt(120, 0, 13)
+        ids[0, -1, 0] = 151652
+        sp = sampling_params(text_temperature=0, audio_temperature=0)
+        forced = torch.full((60,), 151656, dtype=torch.int32)
+        outs = [e.generate_ids(torch.from_numpy(ids), torch.from_numpy(mask.astype(bool)), 60, sp,
+                               forced_text=forced).cpu().numpy() for e in (ref, part)]
+    finally:
+        part.close()
+    assert outs[0].shape == outs[1].shape
+    diff = np.nonzero((outs[0] != outs[1]).any(-1)[0])[0]
+    if diff.size == 0:
+        return
+    r = int(diff[0])
+    T = ids.shape[1]
+    assert r > T
+    traj = outs[0]
+    lg = ref.forward(torch.from_numpy(traj[:, :T].copy()), torch.ones(1, T, dtype=torch.uint8), 0)
+    for p in range(T, r):
+        lg = ref.forward(torch.from_numpy(traj[:, p:p + 1].copy()), torch.ones(1, p + 1, dtype=torch.uint8), p)
+    lg = lg.float().cpu().numpy()[0]
+    V, A = ref.cfg.vocab, 1025
+    for j in np.nonzero(outs[0][0, r] != outs[1][0, r])[0]:
+        row = lg[:V] if j == 0 else lg[V + (j - 1) * A: V + j * A - 1]
+        top = np.sort(row[np.isfinite(row)])[-2:]
+        assert top[1] - top[0] <= 8 * ulp_bf16(np.abs(top[1])), (r, int(j), top)
