@@ -115,9 +115,9 @@ struct mtts_engine {
   uint64_t* mega_trace = nullptr; // MTTS_MEGA_TRACE=1: per-stage timestamps of the last launch
   // persistent streaming engine (pse.hip) for the batch-1 decode stack: MTTS_PSE=1 (A/B)
   bool pse = true;               // MTTS_PSE=0: per-op launches for batch-1 decode too
-  int pse_ctx_max = 448;         // PSE only while the context stays within this (MTTS_PSE_CTX):
+  int pse_ctx_max = 576;         // PSE only while the context stays within this (MTTS_PSE_CTX):
                                  // its attention (2 CUs per KV head) loses to the per-op
-                                 // split-K attention beyond ~500 cached keys
+                                 // split-K attention beyond ~600 cached keys
   bool pse_now = false;          // this forward / captured decode step may take the PSE path
   void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
   bool pse_ok = false;           // the shape and the device support it
