@@ -751,6 +751,18 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   e->pse_choose(past + S);
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
   leave(e, stream);
+  if (!rc && S == 1 && B == 1 && e->pse && e->pse_ok && e->pse_now && e->pse_ws) {
+    // a persistent streaming launch that gave up waiting leaves invalid logits: say so here
+    // (generation checks the same word in mtts_generate_poll)
+    uint32_t err = 0;
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost));
+    if (err) {
+      hipMemset(e->pse_ws, 0, pse_ws_bytes());
+      return fail(MTTS_E_HIP, "persistent streaming decode: a wait timed out (code " + std::to_string(err) +
+                                  "; logits invalid)");
+    }
+  }
   return rc;
 }
 
