@@ -579,6 +579,9 @@ def main():
                        "layers": args.layers, "parallelism": f"dp{world}", "sampling": "greedy, forced text schedule"},
             "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
             "audio_frames_per_utt": frames0,
+            "decode_path": (f"batch 1: the 36-layer stack as one persistent streaming launch (csrc/pse.hip) for steps "
+                            f"with context <= {eng.pse_ctx_max()}, per-op hipGraph launches beyond"
+                            if eng.pse_active() and args.batch == 1 else "per-op hipGraph launches"),
             "p50_first_chunk_ms": round(p50, 2),
             "first_chunk_def": f"prefill + {13 + n_vq + 1} decode steps (first 1 s of audio codes complete), codec excluded",
             "decode_weight_bytes": wb,
