@@ -47,6 +47,12 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_POLL_SLEEP
 #define PSE_POLL_SLEEP 1  // s_sleep count between a gather's sweeps (x 64 cycles)
 #endif
+#ifndef PSE_GPRIO
+#define PSE_GPRIO 1  // consumer waves raise their issue priority while gathering
+#endif
+#ifndef PSE_LPRIO
+#define PSE_LPRIO 0
+#endif
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
@@ -203,6 +209,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     if (x.tid + i * CW * 64 < n) pend |= 1u << i;
   // the first sweep, then the caller's own loads (independent of the granules: they queue
   // behind the sweep instead of delaying it, and the sweep's results are waited for alone)
+  if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);  // sweeps issue ahead of the loader's fills
   bool ok = true;
   for (uint32_t spins = 0;; ++spins) {
     uint32_t lo[MAXP], hi[MAXP];
@@ -230,6 +237,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     }
     __builtin_amdgcn_s_sleep(PSE_POLL_SLEEP);
   }
+  if (PSE_GPRIO) __builtin_amdgcn_s_setprio(PSE_GPRIO == 2 ? 2 : 0);
   cbar(x);
   return ok && !failed(x);
 }
@@ -641,6 +649,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
 
   if (wave < LW) {
     // =================== loaders ===================
+    if (PSE_LPRIO) __builtin_amdgcn_s_setprio(PSE_LPRIO);  // (A/B: the loader ahead of spinning consumers)
     // loader wave k streams slots k, k + LW, ...; m = its own slot count, marked = its slots
     // published in full[k]
     const int k = wave;
@@ -718,6 +727,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
   } else {
     // =================== consumers ===================
     Ctx x{a, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
+    if (PSE_GPRIO == 2) __builtin_amdgcn_s_setprio(2);  // (A/B: consumers ahead of the loader always)
     uint32_t* xs32 = reinterpret_cast<uint32_t*>(lds + L_XS);
     bf16_t* xs = reinterpret_cast<bf16_t*>(lds + L_XS);
     float* ssl = reinterpret_cast<float*>(lds + L_MISC);  // [256] gathered sums of squares
