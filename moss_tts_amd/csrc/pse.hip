@@ -53,6 +53,11 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_LPRIO
 #define PSE_LPRIO 0
 #endif
+#ifndef PSE_PPRIO
+#define PSE_PPRIO 1  // consumer waves raise their issue priority over each op's publish
+#endif
+#define PSE_PRIO_UP() do { if (PSE_PPRIO) __builtin_amdgcn_s_setprio(3); } while (0)
+#define PSE_PRIO_DOWN() do { if (PSE_PPRIO) __builtin_amdgcn_s_setprio(0); } while (0)
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
@@ -776,11 +781,13 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         #pragma unroll 1
         for (int k = 0; k < 4; ++k) consume_slot(x, seq++, half * 64 + k * 16, acc);
+        PSE_PRIO_UP();
         red_put(x, 0, acc);
         cbar(x);
         if (wave == LW && lane < 16)
           st64(a.g_qkv + qkv_gran(u >> 1) + (u & 1) * 16 + lane, gran(__float_as_uint(red_get(x, 0, lane)), tq));
         cbar(x);
+        PSE_PRIO_DOWN();
       }
       if (wave == LW) PSE_STAMP(l, 2);
       // ---------------- attention (one CU per KV head) ----------------
@@ -799,10 +806,12 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         #pragma unroll 1
         for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, acc);
+        PSE_PRIO_UP();
         red_put(x, 0, acc);
         cbar(x);
         emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f);
         cbar(x);
+        PSE_PRIO_DOWN();
       }
       if (wave == LW) PSE_STAMP(l, 5);
       // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
@@ -818,6 +827,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, ag);
         #pragma unroll 1
         for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, au);
+        PSE_PRIO_UP();
         red_put(x, 0, ag);
         red_put(x, 1, au);
         cbar(x);
@@ -829,6 +839,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
           if (lane < 16 && (lane & 1) == 0) st64(a.g_act + (3 * c + j) * 8 + lane / 2, gran(pack2(o, on), tg));
         }
         cbar(x);
+        PSE_PRIO_DOWN();
       }
       if (wave == LW) PSE_STAMP(l, 7);
       // ---------------- down (+ residual) ----------------
@@ -838,10 +849,12 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         #pragma unroll 1
         for (int k = 0; k < 24; ++k) consume_slot(x, seq++, k * 16, acc);
+        PSE_PRIO_UP();
         red_put(x, 0, acc);
         cbar(x);
         emit_h(1, tagof(epoch, l, OP_DOWN), lane < 16 ? red_get(x, 0, lane) : 0.f);
         cbar(x);
+        PSE_PRIO_DOWN();
       }
       if (wave == LW) PSE_STAMP(l, 9);
       if (a.trace && wave == LW && lane < 5)
