@@ -58,6 +58,9 @@ constexpr int THREADS = (LW + CW) * 64;
 #endif
 #define PSE_PRIO_UP() do { if (PSE_PPRIO) __builtin_amdgcn_s_setprio(3); } while (0)
 #define PSE_PRIO_DOWN() do { if (PSE_PPRIO) __builtin_amdgcn_s_setprio(0); } while (0)
+#ifndef PSE_CSLEEP
+#define PSE_CSLEEP 0  // s_sleep of a consumer waiting for a ring slot
+#endif
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
@@ -294,7 +297,7 @@ __device__ __forceinline__ void consume_slot(Ctx& x, int seq, int kt0, f32x4& ac
       give_up(x, 3);
       return;
     }
-    __builtin_amdgcn_s_sleep(0);
+    __builtin_amdgcn_s_sleep(PSE_CSLEEP);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
   if (x.a.probe == 2) {
