@@ -156,9 +156,11 @@ hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   if (a0.attn.part && (epi != EPI_RESADD || a0.B > 16 || (size_t)a0.B * a0.K * 2 > NORM_LDS_MAX || a0.attn.D % 8 ||
                        a0.K != a0.attn.Hkv * a0.attn.G * a0.attn.D))
     return hipErrorInvalidValue;
+  // the row gather is read by the plain (no-prologue, <= 16 row) body only
+  if (a0.xtok && (a0.x_packed || a0.ss_in || a0.attn.part || a0.B > 16 || a0.ld_xtok <= 0)) return hipErrorInvalidValue;
   for (int b0 = 0; b0 < a0.B; b0 += 32) {
     GemvArgs a = a0;
-    a.x = a0.x + (size_t)b0 * a0.ldx;
+    a.x = a0.xtok ? a0.x : a0.x + (size_t)b0 * a0.ldx;
     a.y = a0.y + (size_t)b0 * a0.ldy;
     a.res = a0.res ? a0.res + (size_t)b0 * a0.ldres : nullptr;
     a.ss_in = a0.ss_in ? a0.ss_in + (size_t)b0 * a0.ld_ss : nullptr;

@@ -60,8 +60,9 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
   for (int nb = 0; nb < NB; ++nb) {
     const int b = (lane & 15) + 16 * nb;
     xok[nb] = b < a.B;
+    const size_t row = a.xtok ? (size_t)a.xtok[(size_t)(xok[nb] ? b : 0) * a.ld_xtok] : (size_t)(xok[nb] ? b : 0);
     xbase[nb] = a.x_packed ? reinterpret_cast<const u32x4*>(a.x) + nb * 64 + lane
-                           : reinterpret_cast<const u32x4*>(a.x + (size_t)(xok[nb] ? b : 0) * a.ldx + (lane >> 4) * 8);
+                           : reinterpret_cast<const u32x4*>(a.x + row * a.ldx + (lane >> 4) * 8);
   }
   // Small norm prologues (B = 1 at K 4096, the batch-1 decode step's q|k|v and gate|up) load
   // their inputs -- x rows, the norm weight, the sums of squares -- into registers BEFORE the

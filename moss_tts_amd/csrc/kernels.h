@@ -71,6 +71,11 @@ struct GemvArgs {
   // 17-32 row decode (NB = 2): x / y in the fragment-packed layout (xpk_index) instead of [B, ld]
   int x_packed, y_packed;
   int pk_tiles;        // prefill GEMM (gemm2): token tiles T of the packed x / y (0: decode form, T = 2)
+  // row gather (<= 16 rows, no prologue): x is an embedding table [rows, ldx] and row b of the
+  // input is x + xtok[b * ld_xtok] * ldx -- the MossTTSLocal channel embedding read by the
+  // next adapter's gate|up directly (no separate embed launch); nullptr: x rows are contiguous
+  const int64_t* xtok;
+  int ld_xtok;
 };
 
 // Fragment-packed activations of the 17-32 row decode GEMVs: the MFMA B-operand order of

@@ -291,16 +291,25 @@ int local_init_random(mtts_engine* e, uint64_t seed) {
 
 // ---------------------------------------------------------------------------
 // speech_embedding_to_local_mlp(x) -> the depth stack's residual stream (+ its per-16-column
-// sums of squares for the first layer's input norm); x [B, H]
-static int mlp_in(mtts_engine* e, const Stack& st, const bf16_t* x, int B, hipStream_t s) {
+// sums of squares for the first layer's input norm); x [B, H], or with tok != nullptr the
+// embedding rows x + tok[b * ld_tok] * H gathered by the gate|up GEMV itself
+static int mlp_in(mtts_engine* e, const Stack& st, const bf16_t* x, int B, hipStream_t s,
+                  const int64_t* tok = nullptr, int ld_tok = 0) {
   LocalParts& p = *e->lp;
   const int H = e->c.hidden, LH = p.LH, F = p.F;
   GemvArgs g = gemv_args(p.mi_gu, x, H, p.actF, F, B, F, H);
+  g.xtok = tok; g.ld_xtok = ld_tok;
   HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
   g = gemv_args(p.mi_down, p.actF, F, st.h, LH, B, LH, F);
   g.res = p.zero; g.ldres = LH; g.ss_out = st.ss; g.ld_ss_out = LH / 16;  // bf16(0 + y) == y
   HIPCHK(gemv_ex(g, EPI_RESADD, s));
   return 0;
+}
+
+// MTTS_LOCAL_SEP_EMBED=1: the channel embedding as its own launch (the A/B side of the gather)
+static bool local_sep_embed() {
+  static const bool v = getenv("MTTS_LOCAL_SEP_EMBED") && getenv("MTTS_LOCAL_SEP_EMBED")[0] == '1';
+  return v;
 }
 
 // The depth loop of one frame from the backbone state p.hid [B, H].  Greedy tokens go to
@@ -333,8 +342,13 @@ static int local_depth(mtts_engine* e, int B, int n_ch, const int64_t* forced, i
     if (i + 1 < n_ch) {
       const int64_t* tok = forced ? forced + i : p.next + i;
       const bf16_t* table = i == 0 ? e->emb_text : e->emb_audio + (size_t)(i - 1) * e->audio_rows * H;
-      HIPCHK(embed(tok, 1, table, nullptr, e->audio_rows, H, p.eb, B, s, nullptr, 0, forced ? ld_forced : C));
-      if (int rc = mlp_in(e, st, p.eb, B, s)) return rc;
+      const int ld_tok = forced ? ld_forced : C;
+      if (B <= 16 && !local_sep_embed()) {  // the adapter's gate|up gathers the rows itself
+        if (int rc = mlp_in(e, st, table, B, s, tok, ld_tok)) return rc;
+      } else {
+        HIPCHK(embed(tok, 1, table, nullptr, e->audio_rows, H, p.eb, B, s, nullptr, 0, ld_tok));
+        if (int rc = mlp_in(e, st, p.eb, B, s)) return rc;
+      }
     }
   }
   return 0;
