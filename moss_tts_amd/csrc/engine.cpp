@@ -575,6 +575,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     da.publish_only = fuse_attn ? 1 : 0;
     da.po_max = attn_publish_max_splits();
     da.out_packed = xpk ? 1 : 0;
+    da.nwv_force = st.attn_nwv;
     da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
     // decode, small batch: q|k|v projection + attention in one launch (qa.hip)
     const bool use_qa = S == 1 && fuse_attn && e->qa && st.qsync && !use_ao && !e->fused_ao && B <= QA_MAXB &&

@@ -52,6 +52,7 @@ struct Stack {
   int rows = 0;             // row capacity of xn / attnb / act (>= 32: 17-32 row decode may use the packed layout)
   bool attn_direct = false; // the context never spans two attention blocks: the attention writes its
                             // rows directly and o_proj is a plain GEMV (no split partials to merge)
+  int attn_nwv = 0;         // decode attention waves per block for this stack (0: the engine default)
 };
 
 constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip

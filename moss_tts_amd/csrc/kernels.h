@@ -144,6 +144,7 @@ struct DecAttnArgs {
   int Hq, Hkv, D, Cmax;
   int ns;               // splits per head (set by attn_decode)
   int nwv;              // waves per block (32 keys each; set by attn_decode)
+  int nwv_force;        // 4 / 8 / 16: waves per block for this call (a self-combining form; 0: automatic)
   float eps, scale;
   int publish_only;     // 1: every block writes its (m, l, o) partial; the o_proj GEMV merges them
   int po_max;           // publish_only applies up to po_max blocks per head; longer contexts merge here

@@ -61,6 +61,10 @@ static Stack local_stack(mtts_engine* e) {
   // the depth o_proj reads them as a plain GEMV (no partial merge in its prologue)
   static const bool no_direct = getenv("MTTS_LOCAL_ATTN_MERGE") && getenv("MTTS_LOCAL_ATTN_MERGE")[0] == '1';
   st.attn_direct = !no_direct && LOCAL_CMAX <= attn_decode_keys_per_block();
+  // the direct form's block: 4 waves (128 keys) hold the <= 33 positions, a 4-wave merge instead
+  // of 8 (frame 8.57 -> 8.53 ms in two same-box pairs; MTTS_LOCAL_ATTN_NWV=8 for A/B)
+  static const int nwv = getenv("MTTS_LOCAL_ATTN_NWV") ? atoi(getenv("MTTS_LOCAL_ATTN_NWV")) : 4;
+  if (st.attn_direct && (nwv == 4 || nwv == 8) && LOCAL_CMAX <= 32 * nwv) st.attn_nwv = nwv;
   return st;
 }
 
