@@ -109,3 +109,31 @@ def test_device_pick_greedy_and_top1():
     N.check(N.load().mtts_k_local_pick(P(logits), 1025, 1025, 2, P(seen), P(out), C, R, A, 1.0, 1, 1.0, 1.0, 1, 0,
                                        None), "pick")
     assert np.isin(out[:, 2].cpu().numpy(), [100, 200]).all()  # TopKLogitsWarper keeps ties
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("V,ld", [(1025, 1032), (151936, 151936), (1025, 1025)])
+def test_device_pick_greedy_vector_rows(V, ld):
+    """greedy pick over 16-byte row loads (ld % 8 == 0) and the scalar form: torch.argmax's
+    first index, with the maximum tied across two loads and, in row 1, alone in the V % 8 tail"""
+    import ctypes
+    from moss_tts_amd import _native as N
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    R, C, A = 3, 4, 1025
+    g = torch.Generator().manual_seed(V)
+    x = torch.randn(R, ld, generator=g).to(torch.bfloat16)
+    x[:, V:] = 100.0  # padding columns beyond V never win
+    top = x[:, :V].float().max() + 4
+    x[0, 13] = x[0, V - 9] = top  # a tie in two different 8-column loads: first index wins
+    x[1, V - 1] = top            # the tail element past the last full load
+    logits = x.contiguous().cuda()
+    seen = torch.zeros(R, C, A, dtype=torch.uint8, device="cuda")
+    out = torch.full((R, C), -1, dtype=torch.int64, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    ch = 0 if V > A else 1
+    N.check(N.load().mtts_k_local_pick(P(logits), ld, V, ch, P(seen), P(out), C, R, A, 0.0, 50, 1.0, 1.0, 1, 0,
+                                       None), "pick")
+    want = torch.argmax(x[:, :V].float(), dim=1)
+    assert out[:, ch].cpu().tolist() == want.tolist()
+    assert want[0].item() == 13 and want[1].item() == V - 1
