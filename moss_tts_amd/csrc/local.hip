@@ -16,6 +16,49 @@ __global__ __launch_bounds__(256) void moss_rmsnorm_kernel(const bf16_t* __restr
   const int m = blockIdx.x, t = threadIdx.x;
   const bf16_t* xr = x + (size_t)m * H;
   float s = 0.f;
+  if (H <= 2 * 256 * 8) {
+    // H <= 4096: the row's chunks and the weight load together, once, and stay in registers
+    // (the general form below re-reads x and the weight after the reduction)
+    uint4 xv[2], wv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = t + u * 256;
+      if (c < (H >> 3)) {
+        xv[u] = *reinterpret_cast<const uint4*>(xr + c * 8);
+        wv[u] = *reinterpret_cast<const uint4*>(w + c * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      if (t + u * 256 < (H >> 3)) {
+        float v[8];
+        unpack8(xv[u], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) s += rbf(v[i] * v[i]);
+      }
+    }
+    s = wave_sum(s);
+    if ((t & 63) == 0) red[t >> 6] = s;
+    __syncthreads();
+    const float tot = (red[0] + red[1]) + (red[2] + red[3]);
+    const float norm = rbf(tot / (float)H);
+    const float r = rbf(1.0f / sqrtf(rbf(norm + eps)));
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c = t + u * 256;
+      if (c < (H >> 3)) {
+        float v[8], g[8], q[8];
+        unpack8(xv[u], v);
+        unpack8(wv[u], g);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) q[i] = rbf(v[i] * r) * g[i];
+        uint4 o;
+        o.x = pack2(q[0], q[1]); o.y = pack2(q[2], q[3]); o.z = pack2(q[4], q[5]); o.w = pack2(q[6], q[7]);
+        *reinterpret_cast<uint4*>(y + (size_t)m * H + c * 8) = o;
+      }
+    }
+    return;
+  }
   for (int c = t; c < (H >> 3); c += 256) {
     float v[8];
     unpack8(*reinterpret_cast<const uint4*>(xr + c * 8), v);

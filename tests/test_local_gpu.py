@@ -174,7 +174,7 @@ def test_moss_rmsnorm_kernel(gpu):
     from moss_tts_amd import _native as N
     from oracle.moss_delay import _Ctx
     rng = np.random.default_rng(5)
-    for M, H in [(1, 64), (3, 2048), (5, 520)]:
+    for M, H in [(1, 64), (3, 2048), (5, 520), (2, 4096), (2, 6000)]:  # register-cached form up to 4096, then the general one
         x = (rng.standard_normal((M, H)) * rng.uniform(0.1, 30)).astype(np.float32)
         w = rng.uniform(0.5, 1.5, H).astype(np.float32)
         xt = torch.from_numpy(x).to(torch.bfloat16)
