@@ -28,6 +28,9 @@ extern "C" {
 #define MTTS_E_OOM -2
 #define MTTS_E_HIP -3         /* HIP runtime error */
 #define MTTS_E_UNSUPPORTED -4 /* config the kernels do not cover */
+#define MTTS_E_PSE_TIMEOUT -5 /* the batch-1 persistent decode launch timed out (device shared): results of
+                                 the current generation are invalid; the engine has switched to the per-op
+                                 launches, so restarting the generation succeeds (mtts_generate does) */
 
 typedef struct mtts_engine mtts_engine;
 
@@ -99,10 +102,6 @@ int mtts_engine_time_gemv(mtts_engine* eng, int which, int layer, int B, int ite
 int mtts_forward(mtts_engine* eng, const int64_t* ids_dev, const uint8_t* mask_dev, int B, int S, int past,
                  uint16_t* logits_dev, void* stream);
 int mtts_heads_ld(const mtts_engine* eng);
-/* Workgroups of the persistent decode launch (one decode step's decoder stack as one kernel,
- * batches <= 2 rows), 0 when this engine decodes with one launch per stage (MTTS_MEGA=0, or a
- * shape it does not cover). */
-int mtts_mega_workgroups(const mtts_engine* eng);
 /* 1 when batch-1 decode steps run the decoder stack as one persistent launch with run-ahead
  * weight streaming (default; MTTS_PSE=0 at creation turns it off; MossTTSDelay-8B shape,
  * 256 CUs), else 0.  It is taken by the decode steps of a generation (and teacher-forced
@@ -110,19 +109,13 @@ int mtts_mega_workgroups(const mtts_engine* eng);
  * same generation take the per-op launches. */
 int mtts_pse_active(const mtts_engine* eng);
 int mtts_pse_ctx_max(const mtts_engine* eng);
+/* Fault injection (tests): mark the persistent launch's error word as if a wait had timed out.
+ * The next check (a teacher-forced batch-1 forward, or mtts_generate_poll) takes the fallback:
+ * the launch is turned off for this engine and the work re-runs on the per-op launches. */
+int mtts_pse_inject_timeout(mtts_engine* eng);
 /* per-layer event stamps (s_memrealtime, 100 MHz) of the last persistent streaming launch:
  * [layers][20][256 workgroups] (engine created with MTTS_PSE_TRACE=1; see pse.hip) */
 int mtts_pse_trace(mtts_engine* eng, uint64_t* host, size_t n);
-/* 1 when a decode step of B rows runs attention + o_proj + residual as one launch per layer
- * (ao.hip: B == 1, head_dim 128, KV capacity <= 2048, engine created with MTTS_AO=1), else 0. */
-int mtts_attn_o_active(const mtts_engine* eng, int B);
-/* 1 when a decode step of B rows runs the q|k|v projection and the attention as one launch per
- * layer (qa.hip: B <= 8 with the fused input RMSNorm, engine created with MTTS_QA=1), else 0. */
-int mtts_qkv_attn_active(const mtts_engine* eng, int B);
-/* Diagnostics (engine created with MTTS_MEGA_TRACE=1): the last persistent launch's
- * s_memrealtime stamps (100 MHz), [layers][stage q|k|v, attention, o, gate|up, down]
- * [workgroup][wait start, input ready, staged, done]; n = elements of host. */
-int mtts_mega_trace(mtts_engine* eng, uint64_t* host, size_t n);
 
 /* ---- generate (MossTTSDelayModel.generate, modeling_moss_tts.py:392-525) ----
  * begin: state init + prefill + the step-0 sampling.  decode: n more steps (hipGraph).

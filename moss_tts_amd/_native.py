@@ -15,6 +15,7 @@ MTTS_E_INVALID = -1
 MTTS_E_OOM = -2
 MTTS_E_HIP = -3
 MTTS_E_UNSUPPORTED = -4
+MTTS_E_PSE_TIMEOUT = -5
 
 
 class MttsConfig(ctypes.Structure):
@@ -69,13 +70,10 @@ _SIGS = {
     "mtts_engine_time_gemv": (I, [P, I, I, I, I, ctypes.POINTER(F), ctypes.POINTER(U64)]),
     "mtts_forward": (I, [P, P, P, I, I, I, P, P]),
     "mtts_heads_ld": (I, [P]),
-    "mtts_mega_workgroups": (I, [P]),
     "mtts_pse_active": (I, [P]),
     "mtts_pse_ctx_max": (I, [P]),
+    "mtts_pse_inject_timeout": (I, [P]),
     "mtts_pse_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),
-    "mtts_attn_o_active": (I, [P, I]),
-    "mtts_qkv_attn_active": (I, [P, I]),
-    "mtts_mega_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),
     "mtts_generate_begin": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, P]),
     "mtts_generate_decode": (I, [P, I, P]),
     "mtts_generate_stats": (I, [P, P]),

@@ -23,19 +23,8 @@ namespace mtts {
 constexpr int DEC_KW = 32;      // keys per wave
 constexpr int DEC_MAXS = 256;  // splits per head
 
-struct NoWait {
-  __device__ void operator()() const {}
-};
-
-// SC1 (mega.hip): partials and outputs are stored write-through (sc1) for consumers inside the
-// same launch; the arrival tickets are per layer and reset by the launch's last workgroup.
-// Wait (qa.hip): the block's K / V^T / mask loads, which do not depend on the q|k|v GEMV, go
-// out first; wait() then blocks until the q|k|v rows are published, and only then does the
-// prologue read them.
-template <int G, int D, int NWV, bool SC1 = false, class Wait = NoWait>
-__device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int sp, const int kvh, const int b,
-                                                 const Wait& wait = Wait{}) {
-  constexpr bool PF = !__is_same(Wait, NoWait);
+template <int G, int D, int NWV>
+__device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int sp, const int kvh, const int b) {
   constexpr int KW = DEC_KW, KB = KW * NWV;
   constexpr int QS = (D + 31) / 32;  // 32-dim MFMA steps of q.k
   constexpr int DT = (D + 15) / 16;  // 16-dim output tiles of p.v
@@ -100,10 +89,6 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
     }
   };
   const int kbeg = sp * KB + wave * KW;
-  if constexpr (PF) {
-    load_keys(kbeg);  // waves past the new token: every offset out of range, no traffic
-    wait();
-  }
 
   // ---- prologue loads: job j < G: q head j; G: k; G+1: v (k, v only in the owner);
   // wave w takes jobs w, w + NWV, ... ----
@@ -136,7 +121,7 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       ps[jj] = __builtin_amdgcn_raw_buffer_load_b32(srs, nw && rope ? lo : OOBA, 0, 0);
     }
   }
-  if constexpr (!PF) load_keys(kbeg);  // waves past the new token: every offset out of range
+  load_keys(kbeg);  // waves past the new token: every offset out of range
 
   // ---- prologue math ----
 #pragma unroll
@@ -323,14 +308,9 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
     }
     if (single) {
       bf16_t* op = a.out + (a.out_packed ? xpk_index(b, kvh * G * D + e) : (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e);
-      if constexpr (SC1) {
-        typedef __attribute__((address_space(1))) uint16_t g16;
-        __hip_atomic_store((g16*)op, f2bf(L > 0.f ? o / L : 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        *op = f2bf(L > 0.f ? o / L : 0.f);
-      }
-    } else if (SC1 || !po) {
-      // consumed inside this launch (the last arriver below, or mega.hip): write-through (sc1)
+      *op = f2bf(L > 0.f ? o / L : 0.f);
+    } else if (!po) {
+      // consumed inside this launch (the last arriver below): write-through (sc1)
       // stores, drained before the ticket -- no release fence (cdna_hip_programming.md G16 R1)
       typedef __attribute__((address_space(1))) uint32_t g32;
       __hip_atomic_store((g32*)(part + e), __float_as_uint(o), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -387,15 +367,10 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
       o += f * ld1(p0 + (size_t)s2 * PS + e);
     }
     bf16_t* op = a.out + (a.out_packed ? xpk_index(b, kvh * G * D + e) : (size_t)b * a.Hq * D + (size_t)(kvh * G) * D + e);
-    if constexpr (SC1) {
-      typedef __attribute__((address_space(1))) uint16_t g16;
-      __hip_atomic_store((g16*)op, f2bf(L > 0.f ? o / L : 0.f), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      *op = f2bf(L > 0.f ? o / L : 0.f);
-    }
+    *op = f2bf(L > 0.f ? o / L : 0.f);
   }
-  // ready for the next launch (graph replay); SC1 (mega.hip): per-layer tickets, reset at exit
-  if (!SC1 && t == 0) *cnt = 0;
+  // ready for the next launch (graph replay)
+  if (t == 0) *cnt = 0;
 }
 
 }  // namespace mtts

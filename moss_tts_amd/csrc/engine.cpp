@@ -89,31 +89,13 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->part, e->part_floats))) return rc;
   if ((rc = e->alloc(&e->logits, (size_t)c.max_batch * e->heads_ld))) return rc;
   if ((rc = e->alloc(&e->d_pos, 4))) return rc;
-  if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv)) || (rc = e->alloc(&e->fsync, 4))) return rc;
+  if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv))) return rc;
   if (hipMemset(e->att_cnt, 0, (size_t)c.max_batch * Hkv * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
-  if (hipMemset(e->fsync, 0, 4 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
-  if ((rc = e->alloc(&e->ao_part, attn_o_ws_floats(H, Hkv))) || (rc = e->alloc(&e->ao_cnt, (size_t)attn_o_chunks(H))))
-    return rc;
-  if (hipMemset(e->ao_cnt, 0, attn_o_chunks(H) * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if ((rc = e->alloc(&e->sk_part, SK_PART_FLOATS)) || (rc = e->alloc(&e->sk_cnt, (size_t)SK_TILES))) return rc;
   if ((rc = e->alloc(&e->gk_ws, GK_WS_FLOATS))) return rc;
   if (hipMemset(e->sk_cnt, 0, SK_TILES * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
-  if ((rc = e->alloc(&e->qsync, 16))) return rc;
-  if (hipMemset(e->qsync, 0, 16 * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   // persistent decode launch: per-layer pointers (the caches move with the capacity) + counters
   {
-    std::vector<MegaLayer> ml(c.layers);
-    for (int l = 0; l < c.layers; ++l) {
-      const LayerW& w = e->L[l];
-      ml[l] = MegaLayer{w.qkv, w.o, w.gu, w.down, w.in_norm, w.post_norm, w.q_norm, w.k_norm,
-                        e->kc + l * e->layer_kv, e->vc + l * e->layer_kv};
-    }
-    const int nsync = mega_sync_words(c.layers, Hkv);
-    if ((rc = e->alloc(&e->mega_L, (size_t)c.layers)) || (rc = e->alloc(&e->mega_sync, (size_t)nsync))) return rc;
-    if (hipMemcpy(e->mega_L, ml.data(), ml.size() * sizeof(MegaLayer), hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemset(e->mega_sync, 0, nsync * sizeof(uint32_t)) != hipSuccess)
-      return fail(MTTS_E_HIP, "mega state");
-    e->mega_P = mega_grid(e->device, mega_lds_bytes(MEGA_MAXB, H, Hq * D, I));
     std::vector<PseLayer> pl(c.layers);
     for (int l = 0; l < c.layers; ++l) {
       const LayerW& w = e->L[l];
@@ -124,11 +106,8 @@ static int alloc_capacity(mtts_engine* e) {
     if (hipMemcpy(e->pse_L, pl.data(), pl.size() * sizeof(PseLayer), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(e->pse_ws, 0, pse_ws_bytes()) != hipSuccess)
       return fail(MTTS_E_HIP, "pse state");
-    e->pse_ok = pse_supported(e->device, 1, H, Hq, Hkv, D, I, e->qkv_rows, c.max_ctx);
+    e->pse_ok = pse_supported(e->device, 1, c.layers, H, Hq, Hkv, D, I, e->qkv_rows, c.max_ctx);
     if (getenv("MTTS_PSE_TRACE") && (rc = e->alloc(&e->pse_trace, (size_t)c.layers * PSE_TRACE_EV * 256))) return rc;
-    if (getenv("MTTS_MEGA_TRACE") && e->mega_P > 0 &&
-        (rc = e->alloc(&e->mega_trace, (size_t)c.layers * 5 * e->mega_P * 4)))
-      return rc;
   }
   // generate state
   const int B = c.max_batch;
@@ -136,7 +115,8 @@ static int alloc_capacity(mtts_engine* e) {
       (rc = e->alloc(&e->text_cand, B)) || (rc = e->alloc(&e->audio_cand, (size_t)B * c.n_vq)) ||
       (rc = e->alloc(&e->part_idx, (size_t)B * TEXT_PARTS)) || (rc = e->alloc(&e->part_val, (size_t)B * TEXT_PARTS)) ||
       (rc = e->alloc(&e->audio_len, B)) || (rc = e->alloc(&e->delayed, B)) || (rc = e->alloc(&e->cur_ids, (size_t)B * (c.n_vq + 1))) ||
-      (rc = e->alloc(&e->gen_ids, (size_t)B * c.max_ctx * (c.n_vq + 1))) || (rc = e->alloc(&e->seen, 2 * e->audio_rows)))
+      (rc = e->alloc(&e->gen_ids, (size_t)B * c.max_ctx * (c.n_vq + 1))) || (rc = e->alloc(&e->seen, 2 * e->audio_rows)) ||
+      (rc = e->alloc(&e->wide_hist, (size_t)B * 65536)))
     return rc;
   e->cap_mode = false;
   return 0;
@@ -168,12 +148,8 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_GEMV_PREFILL")) e->gemv_prefill = v[0] == '1';
   if (const char* v = getenv("MTTS_UNFUSED_ATTN")) e->unfused_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
-  if (const char* v = getenv("MTTS_FUSED_AO")) e->fused_ao = v[0] == '1';
-  if (const char* v = getenv("MTTS_MEGA")) e->mega = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE")) e->pse = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE_CTX")) e->pse_ctx_max = atoi(v);
-  if (const char* v = getenv("MTTS_AO")) e->ao = v[0] == '1';
-  if (const char* v = getenv("MTTS_QA")) e->qa = v[0] == '1';
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
@@ -252,22 +228,15 @@ extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
 }
 extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
 extern "C" int mtts_pse_active(const mtts_engine* e) { return e && e->pse && e->pse_ok ? 1 : 0; }
+extern "C" int mtts_pse_inject_timeout(mtts_engine* e) {
+  if (!e || !e->pse_ws) return fail(MTTS_E_INVALID, "no persistent launch state");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const uint32_t code = 0x7e57u;
+  HIPCHK(hipMemcpy(pse_err_word(e->pse_ws), &code, 4, hipMemcpyHostToDevice));
+  return 0;
+}
 extern "C" int mtts_pse_ctx_max(const mtts_engine* e) { return e && e->pse && e->pse_ok ? e->pse_ctx_max : 0; }
-extern "C" int mtts_mega_workgroups(const mtts_engine* e) {
-  return e && e->mega && e->c.head_dim == 128 ? e->mega_P : 0;
-}
-extern "C" int mtts_attn_o_active(const mtts_engine* e, int B) {
-  return e && e->ao && e->c.max_ctx <= AO_MAX_CTX &&
-         attn_o_supported(B, e->c.n_heads, e->c.n_kv, e->c.head_dim, e->c.hidden) ? 1 : 0;
-}
-extern "C" int mtts_qkv_attn_active(const mtts_engine* e, int B) {
-  if (!e || !e->qa || e->ao || e->fused_ao || e->unfused_attn || B > QA_MAXB || B <= 0) return 0;
-  GemvArgs g = gemv_args(e->L[0].qkv, e->h, e->c.hidden, e->qkvb, e->qkv_rows, B, e->qkv_rows, e->c.hidden);
-  g.ss_in = norm_lds_bytes(B, e->c.hidden) <= NORM_LDS_MAX && !e->unfused_norm ? e->ss : nullptr;
-  DecAttnArgs da{};
-  da.Hq = e->c.n_heads; da.Hkv = e->c.n_kv; da.D = e->c.head_dim; da.Cmax = e->c.max_ctx;
-  return qkv_attn_supported(g, da, B) ? 1 : 0;
-}
 extern "C" int mtts_pse_trace(mtts_engine* e, uint64_t* host, size_t n) {
   if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
   if (!e->pse_trace) return fail(MTTS_E_UNSUPPORTED, "engine created without MTTS_PSE_TRACE=1");
@@ -275,15 +244,6 @@ extern "C" int mtts_pse_trace(mtts_engine* e, uint64_t* host, size_t n) {
   hipSetDevice(e->device);
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(host, e->pse_trace, std::min(n, have) * sizeof(uint64_t), hipMemcpyDeviceToHost));
-  return 0;
-}
-extern "C" int mtts_mega_trace(mtts_engine* e, uint64_t* host, size_t n) {
-  if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
-  if (!e->mega_trace) return fail(MTTS_E_UNSUPPORTED, "engine created without MTTS_MEGA_TRACE=1");
-  const size_t have = (size_t)e->c.layers * 5 * e->mega_P * 4;
-  hipSetDevice(e->device);
-  HIPCHK(hipStreamSynchronize(e->stream));
-  HIPCHK(hipMemcpy(host, e->mega_trace, std::min(n, have) * sizeof(uint64_t), hipMemcpyDeviceToHost));
   return 0;
 }
 
@@ -462,8 +422,7 @@ Stack backbone_stack(mtts_engine* e) {
   st.cos_t = e->cos_t; st.sin_t = e->sin_t; st.mask = e->mask;
   st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
   st.rows = e->Mmax;
-  st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt; st.fsync = e->fsync;
-  st.ao_part = e->ao_part; st.ao_cnt = e->ao_cnt; st.qsync = e->qsync;
+  st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt;
   return st;
 }
 
@@ -528,29 +487,12 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     HIPCHK(pse_decode(pa, e->pse_ws, s));
     return 0;
   }
-  if (S == 1 && B <= MEGA_MAXB && e->mega && e->mega_P > 0 && st.cos_t && st.L == e->L.data() && D == 128) {
-    // the whole stack as one persistent launch (mega.hip)
-    MegaArgs ma{};
-    ma.L = e->mega_L; ma.layers = st.layers; ma.h = st.h; ma.ss = st.ss; ma.qkvb = st.qkvb; ma.act = st.act;
-    ma.part = st.part; ma.cos_t = st.cos_t; ma.sin_t = st.sin_t; ma.mask = st.mask + (size_t)b0 * st.Cmax;
-    ma.pos = pos_base; ma.B = B; ma.H = H; ma.Hq = Hq; ma.Hkv = Hkv; ma.D = D; ma.I = I; ma.qkv_rows = st.qkv_rows;
-    ma.Cmax = st.Cmax; ma.eps = e->c.rms_eps; ma.scale = 1.0f / std::sqrt((float)D); ma.sync = e->mega_sync;
-    ma.attnb = st.attnb; ma.w_err = mega_err_word(st.layers, Hkv); ma.trace = e->mega_trace;
-    if (b0 == 0) {
-      HIPCHK(mega_decode(ma, e->mega_P, s));
-      return 0;
-    }
-  }
   const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn &&
                          !st.attn_direct;
-  // short contexts: attention + o_proj + residual in one launch (ao.hip); its blocks re-read
-  // their KV head from L2 once per o_proj row chunk, so long contexts keep the split form
-  const bool use_ao = S == 1 && e->ao && st.ao_part && st.cos_t && st.Cmax <= AO_MAX_CTX &&
-                      attn_o_supported(B, Hq, Hkv, D, H);
   // 17-32 row decode: the GEMV inputs (xn, the attention output, the SwiGLU output) travel in
   // the fragment-packed layout, so each x fragment is one 1 KiB load (B=32 per layer: x loads
   // cost ~22 of 129 us row-major)
-  const bool xpk = S == 1 && M > 16 && M <= 32 && st.rows >= 32 && e->xpack && !use_ao && !e->fused_ao;
+  const bool xpk = S == 1 && M > 16 && M <= 32 && st.rows >= 32 && e->xpack;
   // long prefills (the 32-utterance batch): the same for the 128 x 128 GEMM, T = M / 16 token
   // tiles (its x loads were 81 of 191 ms row-major)
   // prefills of >= 128 token rows (the 128 x 128 GEMM's range): packed GEMM inputs.  B=1 clone
@@ -577,34 +519,9 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     da.out_packed = xpk ? 1 : 0;
     da.nwv_force = st.attn_nwv;
     da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
-    // decode, small batch: q|k|v projection + attention in one launch (qa.hip)
-    const bool use_qa = S == 1 && fuse_attn && e->qa && st.qsync && !use_ao && !e->fused_ao && B <= QA_MAXB &&
-                        qkv_attn_supported(g, da, B);
-    if (use_qa) HIPCHK(qkv_attn(g, da, st.qsync, B, s));
-    else HIPCHK(proj(e, g, EPI_STORE, s));
-    // decode, small batch: attention + o_proj in one launch (fused.hip)
-    const bool fused_ao = fuse_attn && e->fused_ao && st.fsync &&
-                          fused_attn_splits(st.Cmax) * Hkv * B <= 1024;
-    if (use_ao) {
-      AOArgs aa{};
-      aa.qkv = st.qkvb; aa.qn_w = w.q_norm; aa.kn_w = w.k_norm; aa.cos_t = st.cos_t; aa.sin_t = st.sin_t;
-      aa.kc = kc; aa.vc = vc; aa.mask = st.mask + (size_t)b0 * st.Cmax; aa.pos = pos_base; aa.wo = w.o;
-      aa.h = st.h; aa.ldh = H; aa.ss_out = st.ss; aa.ld_ss = NT; aa.part = st.ao_part; aa.cnt = st.ao_cnt;
-      aa.B = B; aa.H = H; aa.NRT = H / 16; aa.KT = Hq * D / 32; aa.Hq = Hq; aa.Hkv = Hkv; aa.D = D; aa.Cmax = st.Cmax;
-      aa.eps = eps; aa.scale = 1.0f / std::sqrt((float)D);
-      static const int ao_probe = getenv("MTTS_AO_PROBE") ? atoi(getenv("MTTS_AO_PROBE")) : 0;
-      aa.probe = ao_probe;
-      HIPCHK(attn_o(aa, s));
-    } else if (use_qa) {
-      // attention ran with the projection
-    } else if (S == 1) {
-      if (fused_ao) {
-        GemvArgs go = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
-        go.res = st.h; go.ldres = H; go.ss_out = st.ss; go.ld_ss_out = NT;
-        HIPCHK(attn_oproj(da, go, st.fsync, B, s));
-      } else {
-        HIPCHK(attn_decode(da, B, s));
-      }
+    HIPCHK(proj(e, g, EPI_STORE, s));
+    if (S == 1) {
+      HIPCHK(attn_decode(da, B, s));
     } else {
       if (!st.cos_t) return fail(MTTS_E_UNSUPPORTED, "multi-token forward of a stack without positions");
       QKRopeArgs qa;
@@ -621,17 +538,15 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       if (e->old_prefill_attn) HIPCHK(attention(aa, s));
       else HIPCHK(attention_prefill(aa, s));
     }
-    if (!(S == 1 && fused_ao) && !use_ao) {
-      g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
-      g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1]; g.force_u = e->nu[1];
-      g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
-      if (fuse_attn) {
-        g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
-        g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
-        g.attn.po_max = use_qa ? ATTN_PO_ALL : attn_publish_max_splits();  // qa.hip publishes every split
-      }
-      HIPCHK(proj(e, g, EPI_RESADD, s));
+    g = gemv_args(w.o, st.attnb, Hq * D, st.h, H, M, H, Hq * D);
+    g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[1]; g.force_u = e->nu[1];
+    g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
+    if (fuse_attn) {
+      g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
+      g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
+      g.attn.po_max = attn_publish_max_splits();
     }
+    HIPCHK(proj(e, g, EPI_RESADD, s));
     g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
     if (int rc = normed_input(e, st, g, w.post_norm, M, s, ntiles)) return rc;
     g.force_nw = e->nw[2]; g.force_u = e->nu[2];
@@ -741,6 +656,23 @@ void leave(mtts_engine* e, void* user) {
   hipStreamWaitEvent((hipStream_t)user, e->ev_out, 0);
 }
 
+// The persistent streaming launch's error word (pse.hip: a bounded wait timed out).  When set:
+// clear it, turn the launch off for this engine (every later step takes the per-op launches)
+// and report true; synchronises the engine stream.
+bool pse_tripped(mtts_engine* e, hipStream_t s) {
+  if (!e->pse_ws) return false;
+  uint32_t err = 0;
+  if (hipStreamSynchronize(s) != hipSuccess ||
+      hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost) != hipSuccess || !err)
+    return false;
+  hipMemset(e->pse_ws, 0, pse_ws_bytes());
+  e->pse = false;
+  e->pse_timeouts += 1;
+  fprintf(stderr, "libmtts: persistent streaming decode timed out (code %u; device shared with other work?); "
+                  "this engine continues on the per-op launches\n", err);
+  return true;
+}
+
 extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
                             uint16_t* logits, void* stream) {
   if (!e || !ids || !mask || !logits) return fail(MTTS_E_INVALID, "null argument");
@@ -751,19 +683,21 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
   e->pse_choose(past + S);
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
-  leave(e, stream);
   if (!rc && S == 1 && B == 1 && e->pse && e->pse_ok && e->pse_now && e->pse_ws) {
-    // a persistent streaming launch that gave up waiting leaves invalid logits: say so here
-    // (generation checks the same word in mtts_generate_poll)
-    uint32_t err = 0;
-    HIPCHK(hipStreamSynchronize(s));
-    HIPCHK(hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost));
-    if (err) {
-      hipMemset(e->pse_ws, 0, pse_ws_bytes());
-      return fail(MTTS_E_HIP, "persistent streaming decode: a wait timed out (code " + std::to_string(err) +
-                                  "; logits invalid)");
+    // A persistent streaming launch that gave up waiting (its workgroups were not all resident:
+    // other work on the device) leaves invalid logits.  Outside a stream capture the step is
+    // checked here and, on a timeout, re-run on the per-op launches, which every later step of
+    // this engine then takes (the forward is idempotent: it rewrites the KV rows at past..).
+    // Inside a caller's capture nothing may synchronise: the check is left to the caller
+    // (mtts_generate_poll reads the same word).
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cs));
+    if (cs == hipStreamCaptureStatusNone && pse_tripped(e, s)) {
+      e->pse_now = false;
+      rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
     }
   }
+  leave(e, stream);
   return rc;
 }
 
@@ -804,10 +738,9 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   g.ids.audio_start = c.audio_start_token_id; g.ids.audio_end = c.audio_end_token_id;
   g.ids.user_slot = c.audio_user_slot_token_id; g.ids.gen_slot = c.audio_assistant_gen_slot_token_id;
   g.ids.delay_slot = c.audio_assistant_delay_slot_token_id; g.ids.audio_pad = c.audio_pad_code;
-  // sampled text keeps at most TOPK_CAP candidates (top_k <= 0 would be the whole 151,936-id
-  // vocab); audio rows have 1,025 codes, so any audio top_k (<= 0: no filter) fits
-  if (g.text_sample && (sp->text_top_k <= 0 || sp->text_top_k > TOPK_CAP))
-    return fail(MTTS_E_UNSUPPORTED, "sampled text needs 1 <= text_top_k <= 2048");
+  // sampled text: top_k 1..TOPK_CAP sorts its candidates; <= 0 (no filter, inference_utils.py:136)
+  // or larger runs the key-bin sampler over the whole row (topk.h block_wide_draw); audio rows
+  // have 1,025 codes, so any audio top_k (<= 0: no filter) fits the sorted form
   if (e->audio_rows > TOPK_CAP) return fail(MTTS_E_UNSUPPORTED, "audio vocab above 2048");
   e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = forced;
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
@@ -872,23 +805,9 @@ extern "C" int mtts_generate_poll(mtts_engine* e, int* steps, int* done_step, vo
   HIPCHK(hipStreamSynchronize(e->stream));
   GenDev g;
   HIPCHK(hipMemcpy(&g, e->st, sizeof(g), hipMemcpyDeviceToHost));
-  if (e->mega_sync) {  // a persistent decode launch that gave up waiting (mega.hip) poisons the run
-    uint32_t err = 0;
-    HIPCHK(hipMemcpy(&err, e->mega_sync + mega_err_word(e->c.layers, e->c.n_kv), 4, hipMemcpyDeviceToHost));
-    if (err) {
-      hipMemset(e->mega_sync, 0, mega_sync_words(e->c.layers, e->c.n_kv) * sizeof(uint32_t));
-      return fail(MTTS_E_HIP, "persistent decode launch: a stage wait timed out (results invalid)");
-    }
-  }
-  if (e->pse_ws) {  // the persistent streaming launch gave up waiting (pse.hip): the run is invalid
-    uint32_t err = 0;
-    HIPCHK(hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost));
-    if (err) {
-      hipMemset(e->pse_ws, 0, pse_ws_bytes());
-      return fail(MTTS_E_HIP, "persistent streaming decode: a wait timed out (code " + std::to_string(err) +
-                                  "; results invalid)");
-    }
-  }
+  if (pse_tripped(e, e->stream))  // the persistent streaming launch gave up waiting: the run is invalid
+    return fail(MTTS_E_PSE_TIMEOUT, "persistent streaming decode: a wait timed out (results invalid; the engine "
+                                    "now runs the per-op launches: restart the generation)");
   if (g.topk_overflow)
     return fail(MTTS_E_UNSUPPORTED, "top-k: ties at the k-th score exceed 2048 candidates (lower top_k)");
   if (steps) *steps = g.step;
@@ -909,19 +828,25 @@ extern "C" int mtts_generate_stats(mtts_engine* e, int* text_head_steps) {
 
 extern "C" int mtts_generate(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T, int max_new,
                              const mtts_sampling* sp, const int32_t* forced, int chunk, int* n_rows, void* stream) {
-  int rc = mtts_generate_begin(e, ids, mask, B, T, max_new, sp, forced, stream);
-  if (rc) return rc;
   if (chunk <= 0) chunk = 16;
-  int steps = 1, done = -1;
-  while (true) {
-    rc = mtts_generate_poll(e, &steps, &done, stream);
+  // a persistent-launch timeout (MTTS_E_PSE_TIMEOUT) turned that launch off: the generation
+  // restarts once from the prompt on the per-op launches (the inputs are the caller's)
+  for (int attempt = 0;; ++attempt) {
+    int rc = mtts_generate_begin(e, ids, mask, B, T, max_new, sp, forced, stream);
     if (rc) return rc;
-    if (done >= 0 || steps >= max_new) break;
-    rc = mtts_generate_decode(e, std::min(chunk, max_new - steps), stream);
+    int steps = 1, done = -1;
+    while (true) {
+      rc = mtts_generate_poll(e, &steps, &done, stream);
+      if (rc) break;
+      if (done >= 0 || steps >= max_new) break;
+      rc = mtts_generate_decode(e, std::min(chunk, max_new - steps), stream);
+      if (rc) break;
+    }
+    if (rc == MTTS_E_PSE_TIMEOUT && attempt == 0) continue;
     if (rc) return rc;
+    if (n_rows) *n_rows = done >= 0 ? done + 1 : steps;
+    return 0;
   }
-  if (n_rows) *n_rows = done >= 0 ? done + 1 : steps;
-  return 0;
 }
 
 extern "C" int mtts_generate_fetch(mtts_engine* e, int64_t* out, int n_rows, void* stream) {

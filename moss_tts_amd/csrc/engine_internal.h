@@ -45,17 +45,12 @@ struct Stack {
   float* ss = nullptr;      // per-16-column sums of squares of h
   float* part = nullptr;
   int* att_cnt = nullptr;
-  int* fsync = nullptr;     // 4 ticket words of the fused attention + o_proj launch (zero between launches)
-  float* ao_part = nullptr; // attention + o_proj launch (ao.hip): split-K partials and row-chunk tickets
-  int* ao_cnt = nullptr;
-  int* qsync = nullptr;     // 16 counter words of the q|k|v + attention launch (qa.hip; zero between launches)
   int rows = 0;             // row capacity of xn / attnb / act (>= 32: 17-32 row decode may use the packed layout)
   bool attn_direct = false; // the context never spans two attention blocks: the attention writes its
                             // rows directly and o_proj is a plain GEMV (no split partials to merge)
   int attn_nwv = 0;         // decode attention waves per block for this stack (0: the engine default)
 };
 
-constexpr int AO_MAX_CTX = 2048;                // largest KV capacity that decodes through ao.hip
 constexpr int SK_TILES = 256;                   // split-K GEMV: most output tiles, and
 constexpr size_t SK_PART_FLOATS = 4096 * 256;   // its partial workspace (tiles x splits x 256; x 2 rows halves)
 constexpr size_t GK_WS_FLOATS = 8u << 20;       // prefill GEMM split-K partials (32 MB)
@@ -91,29 +86,13 @@ struct mtts_engine {
   bool gemv_prefill = false;      // MTTS_GEMV_PREFILL=1: prefill through the decode GEMV (A/B)
   bool unfused_attn = false;      // MTTS_UNFUSED_ATTN=1: decode attention combines in its own kernel (A/B)
   bool old_prefill_attn = false;  // MTTS_OLD_PREFILL_ATTN=1: per-token split-K prefill attention (A/B)
-  bool fused_ao = false;          // MTTS_FUSED_AO=1: decode attention + o_proj as one launch (fused.hip; A/B, slower)
-  int* fsync = nullptr;
-  // decode attention + o_proj + residual as one launch (ao.hip); MTTS_AO=1 turns it on (A/B;
-  // off until it beats attn_decode + the o_proj GEMV)
-  bool ao = false;
-  float* ao_part = nullptr;
-  int* ao_cnt = nullptr;
   // split-K residual GEMV for few-tile projections (splitk.hip); MTTS_SPLITK=0 turns it off (A/B)
   bool splitk = true;
   float* gk_ws = nullptr;    // prefill GEMM split-K partials (GK_WS_FLOATS; gemm.hip)
   float* sk_part = nullptr;  // SK_PART_FLOATS
   int* sk_cnt = nullptr;     // SK_TILES tickets, zero between launches
-  // q|k|v GEMV + decode attention as one launch (qa.hip); MTTS_QA=1 turns it on (A/B; off: slower)
-  bool qa = false;
   // 17-32 row decode: xn / attnb / act in the fragment-packed layout (xpk_index; MTTS_XPACK=0: row-major)
   bool xpack = true;
-  int* qsync = nullptr;
-  // persistent decode launch (mega.hip): MTTS_MEGA=1 turns it on (A/B; off until it wins)
-  bool mega = false;
-  MegaLayer* mega_L = nullptr;   // device [layers]
-  uint32_t* mega_sync = nullptr; // device, mega_sync_words(layers), zero between launches
-  int mega_P = 0;                // workgroups (CUs); 0: unsupported here
-  uint64_t* mega_trace = nullptr; // MTTS_MEGA_TRACE=1: per-stage timestamps of the last launch
   // persistent streaming engine (pse.hip) for the batch-1 decode stack: MTTS_PSE=1 (A/B)
   bool pse = true;               // MTTS_PSE=0: per-op launches for batch-1 decode too
   int pse_ctx_max = 576;         // PSE only while the context stays within this (MTTS_PSE_CTX):
@@ -122,6 +101,7 @@ struct mtts_engine {
   bool pse_now = false;          // this forward / captured decode step may take the PSE path
   void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
   bool pse_ok = false;           // the shape and the device support it
+  int pse_timeouts = 0;          // launches that gave up waiting (each turns `pse` off)
   PseLayer* pse_L = nullptr;     // device [layers]
   unsigned char* pse_ws = nullptr;  // pse_ws_bytes(), zero-filled
   uint64_t* pse_trace = nullptr;    // MTTS_PSE_TRACE=1: per-layer event stamps of the last launch
@@ -131,6 +111,7 @@ struct mtts_engine {
   int *is_stopping = nullptr, *is_audio = nullptr, *text_cand = nullptr, *audio_cand = nullptr, *part_idx = nullptr;
   int64_t *audio_len = nullptr, *delayed = nullptr, *cur_ids = nullptr, *gen_ids = nullptr;
   uint8_t* seen = nullptr;
+  int* wide_hist = nullptr;  // [max_batch][65536] (sampled text without a top-k cap)
   float* part_val = nullptr;
   const int* forced = nullptr;
   int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
@@ -161,6 +142,7 @@ struct mtts_engine {
     g.audio_len = audio_len; g.delayed = delayed; g.cur_ids = cur_ids; g.gen_ids = gen_ids; g.mask = mask;
     g.seen = seen; g.part_val = part_val; g.part_idx = part_idx; g.text_cand = text_cand; g.audio_cand = audio_cand;
     g.forced = forced;
+    g.wide_hist = wide_hist;
     return g;
   }
 };
@@ -192,6 +174,7 @@ int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const
 int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s,
                     bf16_t* hidden = nullptr, int n_embed = 0);
 hipStream_t enter(mtts_engine* e, void* user);
+bool pse_tripped(mtts_engine* e, hipStream_t s);
 void leave(mtts_engine* e, void* user);
 // local.cpp (MossTTSLocal)
 int local_create(mtts_engine* e);

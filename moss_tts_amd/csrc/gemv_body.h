@@ -21,8 +21,8 @@ __device__ __forceinline__ u32x4 norm8(u32x4 xv, u32x4 wv, float r) {
   return o;
 }
 
-// WT: outputs are stored write-through (sc1) for a consumer inside the same launch (qa.hip),
-// which then needs no release fence from this block, only a drain (cdna_hip_programming.md G16 R1)
+// WT: outputs are stored write-through (sc1) for a consumer inside the same launch, which then
+// needs no release fence from this block, only a drain (cdna_hip_programming.md G16 R1)
 template <int NB, int RT, int EPI, int PRO0, int NW, bool PIPE, class Wait, bool WT = false>
 __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&& wait) {
   constexpr bool PRER = PRO0 == PRO_NORM_PREROW;  // the same, one row per load (K / 8 == threads)
@@ -260,9 +260,14 @@ __device__ __forceinline__ void gemv_body(const GemvArgs& a, const int bt, Wait&
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(U * RT) : "memory");
       __syncthreads();  // every wave's chunks have landed
       const float* ssl = reinterpret_cast<const float*>(xs_dyn + (n8x + K8 + 63) / 64 * 64);
+      // the same order as PRO_NORM / PRO_NORM_PRE (4 contiguous per lane, pairwise, then the
+      // wave), so every prologue form gives the same bits (gemv_ex checks n_ss % 4 == 0)
       for (int b = wave; b < a.B; b += NW) {
         float ss = 0.f;
-        for (int t = lane; t < a.n_ss; t += 64) ss += ssl[b * a.n_ss + t];
+        for (int t4 = lane * 4; t4 < a.n_ss; t4 += 256) {
+          const float4 v = *reinterpret_cast<const float4*>(ssl + b * a.n_ss + t4);
+          ss += (v.x + v.y) + (v.z + v.w);
+        }
         ss = wave_sum(ss);
         if (lane == 0) r_s[b] = 1.0f / sqrtf(ss / (float)a.K + a.eps);
       }

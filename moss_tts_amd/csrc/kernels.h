@@ -190,6 +190,7 @@ struct GenBufs {
   int* text_cand;        // [B]
   int* audio_cand;       // [B, n_vq]
   const int* forced;     // [max_new] text override for sampled rows (-1 none) or nullptr
+  int* wide_hist;        // [B, 65536] key bins of the wide text sampler (text_top_k <= 0 or > TOPK_CAP)
 };
 
 // gemv.hip
@@ -226,37 +227,6 @@ int attn_decode_keys_per_block();
 int attn_publish_max_splits();
 // workspace of attn_decode: ticket counters (zero-filled once by the owner) + partials
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);
-// fused.hip: decode attention + o_proj as one launch (block roles by arrival ticket);
-// go = the o_proj GemvArgs (EPI_RESADD, ss_out); sync = 4 zeroed ints owned by the caller
-hipError_t attn_oproj(const DecAttnArgs& da, const GemvArgs& go, int* sync, int B, hipStream_t s);
-int fused_attn_splits(int Cmax);
-
-// ao.hip: decode attention + o_proj + residual as one launch without block roles: every
-// block recomputes its KV head's attention from L2 and streams its own o_proj weight slab
-constexpr int AO_MAXB = 1;
-struct AOArgs {
-  const bf16_t* qkv;    // [B, (Hq + 2 Hkv) * D]  output of the q|k|v GEMV
-  const bf16_t *qn_w, *kn_w, *cos_t, *sin_t;
-  bf16_t *kc, *vc;      // layer cache, K [B][Hkv][Cmax][D], V^T [B][Hkv][D][Cmax] (rows of this launch)
-  const uint8_t* mask;  // [B][Cmax]
-  const int* pos;       // device: position of the new token
-  const bf16_t* wo;     // packed o_proj tiles [NRT][KT]
-  bf16_t* h;            // [B, ldh] residual stream (in / out)
-  int ldh;
-  float* ss_out;        // [B, ld_ss] per-16-column sums of squares of the new h
-  int ld_ss;
-  float* part;          // attn_o_ws_floats(H, Hkv)
-  int* cnt;             // attn_o_chunks(H) tickets, zero between launches
-  int B, H, NRT, KT, Hq, Hkv, D, Cmax;
-  float eps, scale;
-  int probe;  // timing probe (MTTS_AO_PROBE; results invalid): 1 no attention, 2 no weight DMA, 3 no split-K epilogue,
-              // 4 attention in row chunk 0 only
-};
-int attn_o_chunks(int H);
-size_t attn_o_ws_floats(int H, int Hkv);
-bool attn_o_supported(int B, int Hq, int Hkv, int D, int H);
-hipError_t attn_o(const AOArgs& a, hipStream_t s);
-
 // splitk.hip: split-K decode GEMV with the residual epilogue (projections with few 16-row tiles):
 // splits > 1 from gemv_splitk_splits; part: gemv_splitk_ws_floats fp32, cnt: n_tiles zeroed ints
 int gemv_splitk_splits(int n_tiles, int KT, int B);
@@ -267,48 +237,6 @@ hipError_t gemv_splitk(const GemvArgs& a, int S, float* part, int* cnt, hipStrea
 bool gemv_splitk2_pick(int n_tiles, int KT, int B, int* RT, int* S);
 size_t gemv_splitk2_ws_floats(int n_tiles, int S);
 hipError_t gemv_splitk2(const GemvArgs& a, int RT, int S, float* part, int* cnt, hipStream_t s);
-
-// qa.hip: the q|k|v GEMV (fused input RMSNorm) and the decode attention as one launch (block
-// attention units prefetch K / V, then wait for the projection); sync = 16 zeroed ints owned
-// by the caller (word 9: a wait timed out).  Partials as attn_decode's publish-only form.
-constexpr int QA_MAXB = 8;
-bool qkv_attn_supported(const GemvArgs& g, const DecAttnArgs& da, int B);
-hipError_t qkv_attn(const GemvArgs& g, const DecAttnArgs& da, int* sync, int B, hipStream_t s);
-
-// mega.hip: the decoder-layer stack of one decode step as one persistent launch
-constexpr int MEGA_MAXB = 2;
-constexpr size_t MEGA_LDS_LIMIT = 160 * 1024;
-struct MegaLayer {
-  const bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
-  bf16_t *kc, *vc;  // this layer's caches (row 0)
-};
-
-struct MegaArgs {
-  const MegaLayer* L;
-  int layers;
-  bf16_t* h;        // [B, H] residual stream (in / out)
-  float* ss;        // [B, H/16] its per-16-column sums of squares (in / out)
-  bf16_t* qkvb;     // [B, qkv_rows]
-  bf16_t* act;      // [B, I]
-  float* part;      // attention partials [B][Hkv][ns][G*(D+2)]
-  const bf16_t *cos_t, *sin_t;
-  const uint8_t* mask;  // [B][Cmax] (rows of this launch)
-  const int* pos;
-  int B, H, Hq, Hkv, D, I, qkv_rows, Cmax, ns;
-  float eps, scale;
-  bf16_t* attnb;    // [B, Hq*D] attention output
-  uint32_t* sync;   // mega_sync_words: stage counters [layers][5], attention tickets
-                    // [layers][MEGA_MAXB][Hkv], exit ticket, error word (= w_err)
-  int w_err;        // mega_err_word(layers, Hkv)
-  uint64_t* trace;  // nullptr, or [layers][5][P][4] s_memrealtime stamps (wait, ready, staged, done)
-  int lds_x1, lds_x2;  // LDS byte offsets of the two activation regions (dynamic LDS)
-};
-
-size_t mega_lds_bytes(int B, int H, int HqD, int I);
-int mega_sync_words(int layers, int Hkv);  // zeroed words the launch needs (multiple of 4)
-int mega_err_word(int layers, int Hkv);    // index of the error word in them
-int mega_grid(int device, size_t lds);  // workgroups per launch (one per CU), 0: unsupported
-hipError_t mega_decode(const MegaArgs& a, int P, hipStream_t s);
 
 // pse.hip: the batch-1 decode stack as one persistent launch with a per-CU LDS-DMA weight ring
 // running ahead of the data-tagged hand-offs (MossTTSDelay-8B shape, 256 CUs)
@@ -336,7 +264,7 @@ struct PseArgs {
 constexpr int PSE_TRACE_EV = 20;
 size_t pse_lds_bytes();
 int pse_grid(int device);
-bool pse_supported(int device, int B, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);
+bool pse_supported(int device, int B, int layers, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);
 size_t pse_ws_bytes();  // zero-filled once by the owner
 hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s);
 uint32_t* pse_err_word(void* ws);

@@ -35,7 +35,6 @@ struct LocalParts {
   float* ss = nullptr;
   float* part = nullptr;
   int* att_cnt = nullptr;
-  int* fsync = nullptr;
   bf16_t *hid = nullptr, *eb = nullptr, *actF = nullptr, *zero = nullptr, *z = nullptr, *zn = nullptr, *logits = nullptr;
   int ld_logits = 0;
   int64_t* next = nullptr;  // [Bmax][C] tokens of the frame being built (the next forward's input)
@@ -56,7 +55,7 @@ static Stack local_stack(mtts_engine* e) {
   st.cos_t = nullptr; st.sin_t = nullptr;  // MossTTSLocalTransformer: no positional embedding
   st.mask = p.mask;
   st.h = p.h; st.xn = p.xn; st.qkvb = p.qkvb; st.qb = nullptr; st.attnb = p.attnb; st.act = p.act;
-  st.ss = p.ss; st.part = p.part; st.att_cnt = p.att_cnt; st.fsync = p.fsync;
+  st.ss = p.ss; st.part = p.part; st.att_cnt = p.att_cnt;
   // <= 33 channel positions: one attention block per head, so it writes its rows itself and
   // the depth o_proj reads them as a plain GEMV (no partial merge in its prologue)
   static const bool no_direct = getenv("MTTS_LOCAL_ATTN_MERGE") && getenv("MTTS_LOCAL_ATTN_MERGE")[0] == '1';
@@ -130,7 +129,6 @@ int local_alloc_capacity(mtts_engine* e) {
       (rc = e->alloc(&p.qkvb, (size_t)B * p.qkv_rows)) || (rc = e->alloc(&p.attnb, (size_t)B * Hq * D)) ||
       (rc = e->alloc(&p.act, (size_t)B * p.LI)) || (rc = e->alloc(&p.ss, (size_t)B * (LH / 16))) ||
       (rc = e->alloc(&p.part, (size_t)B * ns * Hq * (D + 2))) || (rc = e->alloc(&p.att_cnt, (size_t)B * Hkv)) ||
-      (rc = e->alloc(&p.fsync, 4)) ||
       (rc = e->alloc(&p.hid, (size_t)B * H)) || (rc = e->alloc(&p.eb, (size_t)B * H)) ||
       (rc = e->alloc(&p.actF, (size_t)B * F)) || (rc = e->alloc(&p.zero, (size_t)B * LH)) ||
       (rc = e->alloc(&p.z, (size_t)B * H)) || (rc = e->alloc(&p.zn, (size_t)B * H)) ||
@@ -143,7 +141,6 @@ int local_alloc_capacity(mtts_engine* e) {
   HIPCHK(hipMemcpy(p.lpos, pos.data(), LOCAL_CMAX * sizeof(int), hipMemcpyHostToDevice));
   HIPCHK(hipMemset(p.mask, 1, (size_t)B * LOCAL_CMAX));  // the depth stack attends to every channel so far
   HIPCHK(hipMemset(p.att_cnt, 0, (size_t)B * Hkv * sizeof(int)));
-  HIPCHK(hipMemset(p.fsync, 0, 4 * sizeof(int)));
   HIPCHK(hipMemset(p.zero, 0, (size_t)B * LH * 2));
   HIPCHK(hipMemset(p.next, 0, (size_t)B * C * 8));
   HIPCHK(hipMemset(p.seen, 0, (size_t)B * C * e->audio_rows));

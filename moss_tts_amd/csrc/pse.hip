@@ -879,8 +879,10 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-bool pse_supported(int device, int B, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax) {
+bool pse_supported(int device, int B, int layers, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax) {
   if (B != 1 || H != H_ || Hq != HQ_ || Hkv != HKV_ || D != D_ || I != I_ || qkv_rows != QKVR_ || Cmax % 64) return false;
+  // the loader's pointer table holds PSE_MAXL layers; a hand-off tag carries layer * 5 + op in 8 bits
+  if (layers < 1 || layers > PSE_MAXL || layers * 5 > 256) return false;
   return pse_grid(device) == 256;
 }
 
@@ -905,7 +907,7 @@ size_t pse_ws_bytes() {
 }
 
 hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
-  if (a0.layers < 1 || a0.layers > PSE_MAXL || a0.Cmax % 64) return hipErrorInvalidValue;
+  if (a0.layers < 1 || a0.layers > PSE_MAXL || a0.layers * 5 > 256 || a0.Cmax % 64) return hipErrorInvalidValue;
   PseArgs a = a0;
   uint64_t* g = reinterpret_cast<uint64_t*>(ws);
   a.g_qkv = g; g += 768 * 16;

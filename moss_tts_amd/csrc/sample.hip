@@ -152,7 +152,7 @@ __global__ __launch_bounds__(TSEL_NT) void text_select_kernel(GenBufs g) {
     }
     return;
   }
-  const int K = st.text_top_k;  // validated on the host: 1..TOPK_CAP
+  const int K = st.text_top_k;  // <= 0: no top-k filter (inference_utils.py:136)
   int n;
   if (isa) {
     if (t == 0) {
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(TSEL_NT) void text_select_kernel(GenBufs g) {
       if (vg > -INFINITY) sm.cand[n++] = cand_word(okey16(vg), d.gen_slot);
       if (vd > -INFINITY) sm.cand[n++] = cand_word(okey16(vd), d.delay_slot);
       if (n == 2 && sm.cand[1] < sm.cand[0]) { const auto x = sm.cand[0]; sm.cand[0] = sm.cand[1]; sm.cand[1] = x; }
-      sm.s_n = min(n, K);
+      sm.s_n = K > 0 ? min(n, K) : n;
     }
     __syncthreads();
     n = sm.s_n;
@@ -172,6 +172,12 @@ __global__ __launch_bounds__(TSEL_NT) void text_select_kernel(GenBufs g) {
       if ((ban_im_end && i == d.im_end) || (step == 0 && i == 151662)) return -INFINITY;
       return scaled(row[i], temp);
     };
+    if (K <= 0 || K > TOPK_CAP) {  // wide candidate set: key-bin form (topk.h block_wide_draw)
+      const float u = philox_uniform(st.seed, (uint32_t)step, (uint32_t)b, 0u);
+      const int tok = block_wide_draw<TSEL_NT>(val, st.vocab, K, st.text_top_p, u, g.wide_hist + (size_t)b * WIDE_BINS);
+      if (t == 0) g.text_cand[b] = tok >= 0 ? tok : d.pad;
+      return;
+    }
     n = block_topk_sorted<TSEL_NT>(val, st.vocab, K, TIES_EXACT_K, sm, nullptr);
   }
   const float u = philox_uniform(st.seed, (uint32_t)step, (uint32_t)b, 0u);

@@ -180,4 +180,202 @@ __device__ int block_topk_sorted(F val, int V, int K, int ties, TopkSmem& sm, in
   return n;
 }
 
+// ---------------------------------------------------------------------------
+// Wide candidate sets: sample_token with top_k <= 0 (no top-k filter, `inference_utils.py:136`)
+// or top_k above TOPK_CAP -- up to the whole 151,936-id text row.  No candidate list is built:
+// the scores are bf16-exact, so every score is one of 65,536 keys and the candidates in
+// (score desc, index asc) order are the key bins in descending key order, each bin a run of
+// EQUAL scores in index order.  All of top-k (torch.topk: exactly min(K, #finite), lowest
+// indices among the threshold ties), top-p (apply_top_p_optimized :44-59) and the multinomial
+// draw then work on bin counts [hist, global scratch of WIDE_BINS ints, owned by the block]:
+//   c_k    candidates in bin k (the threshold bin keeps `need` of its ties)
+//   ev_k = exp(s_k - s_max);  S = sum_k fp32(c_k * ev_k)
+//   p_k  = bf16(ev_k / S);  cumulative probability after the r-th element of bin k
+//          cum = fp32(P_t + fp32(L + fp32(r * p_k))), L = the thread chunk's sequential sum of
+//          the bins before k, P_t = the exclusive sum of the earlier chunks' totals
+//   keep up to the first element whose bf16(cum) > top_p (it stays: the shift-right rule)
+//   q_k = bf16(ev_k / S2) over the survivors, target = u * Q, the drawn element is the first
+//   whose cumulative q (same form) exceeds target, i.e. the r-th index of its bin.
+// Sums run in a fixed order: thread t of NT owns the 64 bins at descending positions
+// [64 t, 64 t + 64) and sums them sequentially; chunk totals are summed sequentially.
+// oracle.moss_delay.wide_draw restates this bit for bit.  Returns the token index (-1: no finite
+// score).  All NT threads must call it; NT * 64 == WIDE_BINS.
+constexpr int WIDE_BINS = 65536;
+template <int NT, class F>
+__device__ int block_wide_draw(F val, int V, int K, float top_p, float u, int* hist) {
+  static_assert(NT * 64 == WIDE_BINS, "64 bins per thread");
+  typedef __attribute__((address_space(1))) int gi32;
+  // the bins live in L2 (agent-scope atomics and loads; never a stale L1 line)
+  auto hld = [&](int key) { return __hip_atomic_load((gi32*)(hist + key), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const int t = threadIdx.x;
+  __shared__ float wf[NT];
+  __shared__ int wi[NT];
+  __shared__ int w_thr, w_need, w_topkey, w_cut, w_cut_t, w_cut_key, w_cut_r, w_tok;
+  __shared__ float w_tot;
+  for (int i = t; i < WIDE_BINS; i += NT) __hip_atomic_store((gi32*)(hist + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int i = t; i < V; i += NT) {
+    const float v = val(i);
+    if (v > -INFINITY) __hip_atomic_fetch_add((gi32*)(hist + okey16(v)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int key0 = WIDE_BINS - 1 - 64 * t;  // this thread's bins: key0, key0 - 1, ..., key0 - 63
+  // finite scores per chunk -> exclusive prefix (integers: exact)
+  int mine = 0;
+  for (int j = 0; j < 64; ++j) mine += hld(key0 - j);
+  wi[t] = mine;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0, top = -1;
+    for (int w = 0; w < NT; ++w) {
+      const int c = wi[w];
+      wi[w] = run;
+      if (top < 0 && c > 0) top = w;
+      run += c;
+    }
+    w_topkey = -1;
+    if (top >= 0)
+      for (int j = 0; j < 64; ++j)
+        if (hld(WIDE_BINS - 1 - 64 * top - j) > 0) { w_topkey = WIDE_BINS - 1 - 64 * top - j; break; }
+    w_thr = -1;  // no top-k cut: every finite score is a candidate
+    w_need = 0;
+    w_cut = K > 0 && K < run;
+    w_tok = -1;
+  }
+  __syncthreads();
+  if (w_topkey < 0) return -1;
+  if (w_cut) {
+    // torch.topk: the chunk where the running count first reaches K holds the threshold key;
+    // `need` of its ties (the lowest indices) are candidates
+    const int before = wi[t];
+    if (before < K && before + mine >= K) {
+      int cum = before;
+      for (int j = 0; j < 64; ++j) {
+        const int c = hld(key0 - j);
+        if (cum + c >= K) {
+          w_thr = key0 - j;
+          w_need = K - cum;
+          break;
+        }
+        cum += c;
+      }
+    }
+    __syncthreads();
+  }
+  const int thr = w_thr, need = w_need;
+  const float mx = okey16_val((uint32_t)w_topkey);
+  // candidates of bin `key` among the first (lim_key, lim_r) survivors (lim_key -1: all)
+  auto cnt = [&](int key, int lim_key, int lim_r) -> int {
+    if (key < lim_key) return 0;
+    if (key == lim_key) return lim_r;
+    if (thr < 0 || key > thr) return hld(key);
+    return key == thr ? need : 0;
+  };
+  // (no contraction: every product and sum rounds on its own, as oracle.moss_delay.wide_draw)
+  auto mass = [](int c, float x) { return __fmul_rn((float)c, x); };
+  // fixed-order sum of fp32(c * f(key)); leaves the exclusive chunk prefixes in wf
+  auto chunk_sums = [&](auto f, int lim_key, int lim_r) -> float {
+    float part = 0.f;
+    for (int j = 0; j < 64; ++j) {
+      const int c = cnt(key0 - j, lim_key, lim_r);
+      if (c) part = __fadd_rn(part, mass(c, f(key0 - j)));
+    }
+    wf[t] = part;
+    __syncthreads();
+    if (t == 0) {
+      float run = 0.f;
+      for (int w = 0; w < NT; ++w) { const float x = wf[w]; wf[w] = run; run = __fadd_rn(run, x); }
+      w_tot = run;
+    }
+    __syncthreads();
+    return w_tot;
+  };
+  // the first element whose cumulative value fp32(P_t + fp32(L + fp32(r * f))) passes `pass`
+  // -> (w_cut_key, w_cut_r); -1 when none does
+  auto first_cross = [&](auto f, int lim_key, int lim_r, auto pass) {
+    if (t == 0) { w_cut_t = NT; w_cut_key = -1; w_cut_r = 0; }
+    __syncthreads();
+    const float P = wf[t];
+    float L = 0.f;
+    int ck = -1, cr = 0;
+    for (int j = 0; j < 64 && ck < 0; ++j) {
+      const int key = key0 - j, c = cnt(key, lim_key, lim_r);
+      if (!c) continue;
+      const float x = f(key);
+      if (pass(__fadd_rn(P, __fadd_rn(L, mass(c, x))))) {
+        int lo = 1, hi = c;  // the smallest r that passes (monotone in r)
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (pass(__fadd_rn(P, __fadd_rn(L, mass(mid, x))))) hi = mid;
+          else lo = mid + 1;
+        }
+        ck = key;
+        cr = lo;
+      }
+      L = __fadd_rn(L, mass(c, x));
+    }
+    if (ck >= 0) atomicMin(&w_cut_t, t);
+    __syncthreads();
+    if (ck >= 0 && w_cut_t == t) { w_cut_key = ck; w_cut_r = cr; }
+    __syncthreads();
+  };
+  auto evf = [&](int key) { return expf(okey16_val((uint32_t)key) - mx); };
+  int lim_key = -1, lim_r = 0;
+  if (top_p < 1.0f) {
+    const float S = chunk_sums(evf, -1, 0);
+    auto pf = [&](int key) { return rbf(evf(key) / S); };
+    chunk_sums(pf, -1, 0);
+    first_cross(pf, -1, 0, [&](float cum) { return rbf(cum) > top_p; });
+    lim_key = w_cut_key;  // -1 (never crossed): every candidate survives
+    lim_r = w_cut_r;
+  }
+  const float S2 = chunk_sums(evf, lim_key, lim_r);
+  auto qf = [&](int key) { return rbf(evf(key) / S2); };
+  const float Q = chunk_sums(qf, lim_key, lim_r);
+  const float target = __fmul_rn(u, Q);
+  first_cross(qf, lim_key, lim_r, [&](float cum) { return cum > target; });
+  if (w_cut_key < 0) {  // rounding left the target past the last survivor: take the last one
+    __syncthreads();
+    if (t == 0) {
+      int k = lim_key, r = lim_r;
+      if (lim_key < 0)
+        for (k = 0; k < WIDE_BINS; ++k)
+          if ((r = cnt(k, -1, 0)) > 0) break;
+      w_cut_key = k;
+      w_cut_r = r;
+    }
+    __syncthreads();
+  }
+  const int dk = w_cut_key, dr = w_cut_r;
+  // the dr-th (1-based) index of bin dk in index order: contiguous index chunks + block scan
+  const int chunk = (V + NT - 1) / NT;
+  const int lo_i = min(V, t * chunk), hi_i = min(V, lo_i + chunk);
+  int c = 0;
+  for (int i = lo_i; i < hi_i; ++i) {
+    const float v = val(i);
+    c += (v > -INFINITY && (int)okey16(v) == dk) ? 1 : 0;
+  }
+  wi[t] = c;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int w = 0; w < NT; ++w) { const int x = wi[w]; wi[w] = run; run += x; }
+  }
+  __syncthreads();
+  int rank = wi[t];
+  if (rank < dr && rank + c >= dr) {
+    for (int i = lo_i; i < hi_i; ++i) {
+      const float v = val(i);
+      if (v > -INFINITY && (int)okey16(v) == dk && ++rank == dr) {
+        w_tok = i;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  return w_tok;
+}
+
 }  // namespace mtts

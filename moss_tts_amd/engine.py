@@ -131,10 +131,6 @@ class Engine:
     def init_random(self, seed: int = 0):
         N.check(N.load().mtts_engine_init_random(self._h, seed), "init_random")
 
-    def mega_workgroups(self) -> int:
-        """Workgroups of the persistent decode launch (0: one launch per stage)."""
-        return int(N.load().mtts_mega_workgroups(self._h))
-
     def pse_active(self) -> bool:
         """Whether batch-1 decode steps run the decoder stack as one persistent launch (pse.hip)."""
         return bool(N.load().mtts_pse_active(self._h))
@@ -143,13 +139,9 @@ class Engine:
         """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
         return int(N.load().mtts_pse_ctx_max(self._h))
 
-    def attn_o_active(self, batch: int) -> bool:
-        """Whether a decode step of `batch` rows runs attention + o_proj as one launch (ao.hip)."""
-        return bool(N.load().mtts_attn_o_active(self._h, batch))
-
-    def qkv_attn_active(self, batch: int) -> bool:
-        """Whether a decode step of `batch` rows runs q|k|v + attention as one launch (qa.hip)."""
-        return bool(N.load().mtts_qkv_attn_active(self._h, batch))
+    def inject_pse_timeout(self):
+        """fault injection (tests): the persistent launch's next check sees a timed-out wait"""
+        N.check(N.load().mtts_pse_inject_timeout(self._h), "pse_inject_timeout")
 
     def weight_bytes(self):
         v = ctypes.c_uint64()

@@ -180,7 +180,7 @@ def apply_rope(ctx, x, cos, sin):
 
 def linear(ctx, x, w):
     """nn.Linear without bias: fp32 accumulate, one rounding of the output."""
-    return ctx.r(x.astype(np.float32) @ w.T.astype(np.float32))
+    return ctx.r(np.asarray(x, np.float32) @ np.asarray(w, np.float32).T)
 
 
 def silu(x):
@@ -448,8 +448,120 @@ def torch_draw(vals, top_p, u, ids=None):
     return int(order[keep - 1]), 0.0
 
 
+# ----------------------------------------------------------------------------
+# wide candidate sets (text top_k <= 0 or > TOPK_CAP): the key-bin form of the engine
+# (`moss_tts_amd/csrc/topk.h` block_wide_draw), restated bit for bit
+# ----------------------------------------------------------------------------
+TOPK_CAP = 2048
+WIDE_BINS, WIDE_NT = 65536, 1024
+
+
+def okey16(v):
+    """order-preserving 16-bit key of bf16-exact floats (+0 / -0 share one)"""
+    v = np.where(np.asarray(v, np.float32) == 0, np.float32(0), np.asarray(v, np.float32)).astype(np.float32)
+    u = (v.view(np.uint32) >> 16).astype(np.uint32)
+    return np.where(u & 0x8000, ~u & 0xFFFF, u | 0x8000).astype(np.int64)
+
+
+def okey16_val(k):
+    k = np.asarray(k, np.uint32)
+    u = np.where(k & 0x8000, k & 0x7FFF, ~k & 0xFFFF).astype(np.uint32)
+    return (u << 16).view(np.float32)
+
+
+def _wide_bins(x, K):
+    """candidate counts per descending key position (position p = key 65535 - p): every finite
+    score, or torch.topk's exactly-K with the lowest indices among the threshold ties"""
+    x = np.asarray(x, np.float32)
+    fin = x > -np.inf
+    cnt = np.bincount(okey16(x[fin]), minlength=WIDE_BINS)[::-1].astype(np.int64).copy()
+    n = int(cnt.sum())
+    if K is not None and 0 < K < n:
+        cum = np.cumsum(cnt)
+        p = int(np.searchsorted(cum, K))
+        cnt[p] = K - (int(cum[p - 1]) if p else 0)
+        cnt[p + 1:] = 0
+    return cnt
+
+
+def _wide_sums(cnt, f):
+    """the engine's fixed-order sum of fp32(c * f): per 64-bin chunk sequential, chunk totals
+    sequential; returns (total, exclusive chunk prefixes, inclusive in-chunk prefixes)"""
+    f32 = np.float32
+    m = np.where(cnt > 0, (cnt.astype(f32) * np.nan_to_num(f, nan=0.0, posinf=0.0)).astype(f32), f32(0)).astype(f32)
+    incl = np.cumsum(m.reshape(WIDE_NT, 64), axis=1, dtype=f32)
+    tot = np.cumsum(incl[:, -1], dtype=f32)
+    P = np.concatenate([[f32(0)], tot[:-1]]).astype(f32)
+    return f32(tot[-1]), P, incl
+
+
+def _wide_first(cnt, f, P, incl, passes):
+    """first element (position, r) whose cumulative fp32(P_t + fp32(L + fp32(r * f))) passes"""
+    f32 = np.float32
+    full = (P[:, None] + incl).astype(f32).reshape(-1)
+    hit = np.nonzero((cnt > 0) & passes(full))[0]
+    if hit.size == 0:
+        return -1, 0
+    pos = int(hit[0])
+    t, j = divmod(pos, 64)
+    L = f32(incl[t, j - 1]) if j else f32(0)
+    x = f32(f[pos])
+    lo, hi = 1, int(cnt[pos])
+    while lo < hi:
+        mid = (lo + hi) // 2
+        if passes(np.array([f32(P[t] + f32(L + f32(f32(mid) * x)))], np.float32))[0]:
+            hi = mid
+        else:
+            lo = mid + 1
+    return pos, lo
+
+
+def wide_keep(x, K, top_p):
+    """apply_top_k (:19-26) + apply_top_p_optimized (:44-59) + the softmax (:139) in the key-bin
+    form: returns (cnt, q) -- survivors per descending key position and their bf16 probability"""
+    f32 = np.float32
+    cnt = _wide_bins(x, K)
+    if cnt.sum() == 0:
+        return cnt, np.zeros(WIDE_BINS, f32)
+    keys = WIDE_BINS - 1 - np.arange(WIDE_BINS)
+    with np.errstate(invalid="ignore", over="ignore"):
+        mx = f32(okey16_val(keys[np.nonzero(cnt)[0][0]]))
+        ev = np.exp((okey16_val(keys) - mx).astype(f32)).astype(f32)
+        if top_p is not None and top_p < 1.0:
+            S, _, _ = _wide_sums(cnt, ev)
+            pf = _bf.rnd((ev / S).astype(f32))
+            _, P, incl = _wide_sums(cnt, pf)
+            pos, r = _wide_first(cnt, pf, P, incl, lambda c: _bf.rnd(c) > f32(top_p))
+            if pos >= 0:
+                cnt = cnt.copy()
+                cnt[pos] = r
+                cnt[pos + 1:] = 0
+        S2, _, _ = _wide_sums(cnt, ev)
+        q = _bf.rnd((ev / S2).astype(f32))
+    return cnt, np.where(cnt > 0, q, f32(0)).astype(f32)
+
+
+def wide_draw(x, K, top_p, u):
+    """the engine's draw over a wide candidate set at uniform u: the token index (-1: none)"""
+    f32 = np.float32
+    x = np.asarray(x, np.float32)
+    cnt, q = wide_keep(x, K, top_p)
+    if cnt.sum() == 0:
+        return -1
+    Q, P, incl = _wide_sums(cnt, q)
+    target = f32(f32(u) * Q)
+    pos, r = _wide_first(cnt, q, P, incl, lambda c: c > target)
+    if pos < 0:  # rounding: the last survivor
+        pos = int(np.nonzero(cnt)[0][-1])
+        r = int(cnt[pos])
+    key = WIDE_BINS - 1 - pos
+    fin = x > -np.inf
+    idx = np.nonzero(fin & (okey16(np.where(fin, x, 0)) == key))[0]
+    return int(idx[r - 1])
+
+
 def sample_token(ctx, logits, prev_tokens=None, repetition_penalty=1.0, top_p=None,
-                 top_k=None, do_sample=True, rng=None, ctrs=None):
+                 top_k=None, do_sample=True, rng=None, ctrs=None, wide=False):
     """`inference_utils.py:111-145`.  Greedy is exact.  With do_sample and a `PhiloxDraw`
     rng, row r draws with u = rng.u(*ctrs[r]) through `topk_candidates` + `torch_draw`
     (the engine's stream); another rng draws from `sampling_distribution` (the
@@ -461,6 +573,11 @@ def sample_token(ctx, logits, prev_tokens=None, repetition_penalty=1.0, top_p=No
     if isinstance(rng, PhiloxDraw):
         out = []
         for r_, row in enumerate(np.asarray(logits, np.float32)):
+            w = wide if np.isscalar(wide) else wide[r_]
+            if w and (top_k is None or top_k <= 0 or top_k > TOPK_CAP):
+                # the engine's text sampler without a sortable top-k (sample.hip -> topk.h)
+                out.append(wide_draw(row, top_k, top_p, rng.u(*ctrs[r_])))
+                continue
             cand = topk_candidates(row, top_k)
             pos, _ = torch_draw(row[cand], top_p, rng.u(*ctrs[r_]), ids=cand)
             out.append(cand[pos])
@@ -534,7 +651,8 @@ def decide_step(ctx, cfg, lg, step, st, gen, sp, rng=None, forced_text=None, tra
     if samp_text.any():
         rows = np.nonzero(samp_text)[0]
         nt[samp_text] = sample_token(ctx, t[samp_text], top_p=sp["text_top_p"], top_k=sp["text_top_k"],
-                                     do_sample=text_do_sample, rng=rng, ctrs=[(step, b, 0) for b in rows])
+                                     do_sample=text_do_sample, rng=rng, ctrs=[(step, b, 0) for b in rows],
+                                     wide=~is_audio[rows])  # audio-mode rows: the 2 allowed ids, sorted form
     if forced_text is not None:
         f = np.asarray(forced_text)
         fs = f[:, step] if f.ndim == 2 else np.full(B, f[step] if step < len(f) else -1)

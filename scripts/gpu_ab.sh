@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of one engine switch on the GPU box: the given tests, the default bench with the switch
 # on (env as given) and off (OFF_ENV), and a rocprofv3 kernel-trace timeline of one decode step.
-#   TESTS="tests/test_ao_gpu.py" ON_ENV="MTTS_AO=1" OFF_ENV="MTTS_AO=0" bash scripts/gpu_ab.sh
+#   TESTS="tests/test_pse_gpu.py" ON_ENV="MTTS_PSE=1" OFF_ENV="MTTS_PSE=0" bash scripts/gpu_ab.sh
 set -u
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/ab

@@ -37,6 +37,10 @@ CASES = [
     ("text_k50", 3, 151936, 50, 1.0, 1.0, 2.5),
     ("text_k1000_p90", 3, 151936, 1000, 0.9, 1.0, 1.5),
     ("text_k2048_p30", 2, 151936, 2048, 0.3, 1.0, 6.0),
+    # wide candidate sets (the engine's key-bin sampler): no top-k filter, top_k above 2,048
+    ("text_nok_p100", 2, 151936, 0, 1.0, 1.0, 2.5),
+    ("text_nok_p90", 2, 151936, 0, 0.9, 1.0, 1.5),
+    ("text_k2500_p95", 2, 151936, 2500, 0.95, 1.0, 1.5),
 ]
 
 

@@ -1,0 +1,140 @@
+"""BASELINE configs[3] as benchmarked: MossTTSLocal at batch 8 with n_vq 32 (1 + 32 channels per
+frame) against the oracle (`oracle/moss_local.py`, pinned to the reference's own modules by
+tests/test_oracle_local.py).
+
+Shape: the MossTTSLocal-1.7B depth stage exactly -- local transformer 4 layers of h 1536 / I 8960
+with the backbone's 16 / 8 heads x 128, adapters with I 2048, 33 channel heads over h 2048 -- on a
+2-layer backbone of the 1.7B layer shape (h 2048, I 6144).  That runs the paths the benchmark
+runs at B = 8: the depth down_proj as the split-K GEMV (96 row tiles, K 8960), the 4-wave depth
+attention over the channel positions, the adapter gate|up gathering the next channel's embedding
+rows by token id, `local_pick` over 8 rows, and the 33-channel loop in one hipGraph.
+
+Reference: `moss_tts_local/modeling_moss_tts.py:377-456` (`CustomMixin._sample`), :515-530 (input
+embedding sum).  Tolerance as tests/test_local_gpu.py: logits within 12 bf16 ulps of the row
+scale, argmax equal on a clear top-2 margin; greedy ids equal or first diverging on a near-tie."""
+import numpy as np
+import pytest
+
+from oracle import moss_local as L
+from tests.parity_util import margin_top2, ulp_bf16
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+B = 8
+CFG = L.LCfg(hidden=2048, layers=2, n_heads=16, n_kv=8, head_dim=128, inter=6144, n_vq=32,
+             local_hidden=1536, local_layers=4, local_inter=8960, mlp_ffn=2048)
+
+
+class DeviceRows:
+    """embedding table kept on the device; the oracle gathers only the rows it indexes"""
+
+    def __init__(self, t):
+        self.t = t
+
+    def __getitem__(self, ids):
+        ids = np.asarray(ids)
+        rows = self.t[torch.from_numpy(ids.reshape(-1)).to(self.t.device)].float().cpu().numpy()
+        return rows.reshape(ids.shape + (rows.shape[-1],))
+
+
+@pytest.fixture(scope="module")
+def setup():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from moss_tts_amd.engine import Engine, EngineConfig
+    g = torch.Generator(device="cuda").manual_seed(8)
+    Wd = {}
+    for name, shape, kind in L.weight_specs(CFG):
+        sc, off = L._scale(kind, shape)
+        Wd[name] = (off + sc * (2 * torch.rand(shape, generator=g, device="cuda") - 1)).to(torch.bfloat16)
+    eng = Engine(EngineConfig(hidden=CFG.hidden, layers=CFG.layers, n_heads=CFG.n_heads, n_kv=CFG.n_kv,
+                              head_dim=CFG.head_dim, inter=CFG.inter, vocab=CFG.vocab, n_vq=CFG.n_vq,
+                              rope_theta=CFG.rope_theta, rms_eps=CFG.eps, max_batch=B, max_ctx=192,
+                              max_prefill_tokens=1024, model_kind=1, local_hidden=CFG.local_hidden,
+                              local_layers=CFG.local_layers, local_inter=CFG.local_inter, local_mlp_ffn=CFG.mlp_ffn,
+                              eos_token_id=CFG.eos_token_id, audio_pad_code=CFG.audio_pad_code,
+                              audio_start_token_id=CFG.audio_start_token_id), 0)
+    eng.load_state_dict(Wd)
+    W = {k: (DeviceRows(v) if k.startswith("model.embedding_list.0.") else v.float().cpu().numpy())
+         for k, v in Wd.items()}
+    del Wd
+    torch.cuda.empty_cache()
+    yield eng, W
+    eng.close()
+
+
+def prompts(T, seed):
+    """B unpadded clone-style prompts: text ids, a reference-audio block of user-slot rows with
+    codes, the assistant header ending in audio_start (moss_tts_local/processing_moss_tts.py)"""
+    rng = np.random.default_rng(seed)
+    C = CFG.n_vq + 1
+    ids = np.full((B, T, C), CFG.audio_pad_code, np.int64)
+    ids[..., 0] = rng.integers(200, 20000, (B, T))
+    ids[:, 8:20, 0] = 151654
+    ids[:, 8:20, 1:] = rng.integers(0, 1024, (B, 12, CFG.n_vq))
+    ids[:, -1, 0] = CFG.audio_start_token_id
+    return ids
+
+
+def band(got, want, k):
+    fin = np.isfinite(want)
+    assert (np.isfinite(got) == fin).all(), k
+    scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
+    u = ulp_bf16(np.broadcast_to(scale, want.shape))
+    err = np.abs(got - np.where(fin, want, 0))[fin]
+    assert (err <= 12 * u[fin]).all(), (k, float(err.max()), float(u.max()))
+    srt = np.sort(np.where(fin, want, -np.inf), axis=-1)
+    clear = (srt[:, -1] - srt[:, -2]) > 24 * u[:, 0]
+    assert (np.argmax(got, -1) == np.argmax(want, -1))[clear].all(), k
+
+
+def test_local_b8_teacher_forced_logits(setup):
+    """every channel's logits of two frames (frame 0 from the 40-token prompts, frame 1 one
+    backbone step later), teacher-forced with the same random frames on both sides"""
+    eng, W = setup
+    T = 40
+    ids = prompts(T, 1)
+    rng = np.random.default_rng(2)
+    C = CFG.n_vq + 1
+    frames = np.concatenate([rng.integers(200, 20000, (B, 2, 1)), rng.integers(0, 1024, (B, 2, CFG.n_vq))], 2)
+    allr = np.concatenate([ids, frames], 1)
+    got = []
+    for f in range(2):
+        x, past = (allr[:, :T], 0) if f == 0 else (allr[:, T + f - 1:T + f], T + f - 1)
+        mask = np.ones((B, past + x.shape[1]), np.uint8)
+        lg = eng.local_forward(torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(mask), past,
+                               torch.from_numpy(np.ascontiguousarray(allr[:, T + f])))
+        got += [t.float().cpu().numpy() for t in lg]
+    trace = []
+    L.generate(W, CFG, ids, max_new_tokens=2, dtype="bf16", trace=trace, forced=frames)
+    assert len(got) == len(trace) == 2 * C
+    for k in range(2 * C):
+        band(got[k], trace[k], k)
+
+
+def test_local_b8_generate(setup):
+    """greedy generate (hipGraph frames, device pick) vs the oracle's greedy _sample loop"""
+    eng, W = setup
+    T, steps = 40, 3
+    ids = prompts(T, 3)
+    out = eng.local_generate_ids(torch.from_numpy(ids), None, steps).cpu().numpy()
+    want_rows = L.generate(W, CFG, ids, max_new_tokens=steps, dtype="bf16")
+    want = np.stack([np.concatenate([ids[b, :T - r[0] - 1], r[1]], 0) for b, r in enumerate(want_rows)])
+    assert out.shape[2] == ids.shape[2] and np.array_equal(out[:, :T], ids)
+    n = min(out.shape[1], want.shape[1])
+    diff = np.argwhere(out[:, :n] != want[:, :n])
+    if diff.size == 0:
+        assert out.shape == want.shape
+        return
+    f = int(diff[:, 1].min()) - T
+    assert f >= 0
+    trace = []
+    L.generate(W, CFG, ids, max_new_tokens=f + 1, dtype="bf16", trace=trace, forced=want[:, T:T + f + 1])
+    C = CFG.n_vq + 1
+    rows = diff[diff[:, 1] == T + f]
+    for b in np.unique(rows[:, 0]):
+        i = int(rows[rows[:, 0] == b, 2].min())
+        lg = trace[f * C + i][b]
+        u = float(ulp_bf16(np.abs(lg[np.isfinite(lg)]).max()))
+        assert margin_top2(lg) <= 24 * u, f"frame {f} row {b} channel {i}: divergence without a near tie"

@@ -190,3 +190,42 @@ def test_pse_generation_crosses_the_context_range(engines):
         row = lg[:V] if j == 0 else lg[V + (j - 1) * A: V + j * A - 1]
         top = np.sort(row[np.isfinite(row)])[-2:]
         assert top[1] - top[0] <= 8 * ulp_bf16(np.abs(top[1])), (r, int(j), top)
+
+
+def test_pse_timeout_falls_back_to_launches(engines):
+    """A persistent launch that gives up waiting (its workgroups not all resident: other work on
+    the device) must not surface as an error: a teacher-forced step re-runs on the per-op
+    launches (bit-identical to them), generate() restarts there, and the engine stays on them.
+    The timeout is injected through the error word (mtts_pse_inject_timeout)."""
+    from moss_tts_amd.engine import sampling_params
+    ref, _ = engines
+    e = make(True)
+    try:
+        ids, mask = prompt(120, 3, 17)
+        want = decode_logits(ref, ids, mask, 120, 3)
+        lg = e.forward(torch.from_numpy(ids[:, :120].copy()), torch.from_numpy(mask[:, :120]), 0)
+        got = []
+        e.inject_pse_timeout()  # the first decode step's check trips (the prefill is the GEMM path)
+        for s in range(3):
+            p = 120 + s
+            lg = e.forward(torch.from_numpy(ids[:, p:p + 1].copy()), torch.from_numpy(mask[:, :p + 1]), p)
+            got.append(lg.float().cpu().numpy()[0])
+        assert not e.pse_active()
+        assert all(np.array_equal(w, g) for w, g in zip(want, got))
+    finally:
+        e.close()
+    e = make(True)
+    try:
+        ids, mask = prompt(100, 0, 19)
+        ids[0, -1, 0] = 151652
+        sp = sampling_params(text_temperature=0, audio_temperature=0)
+        forced = torch.full((24,), 151656, dtype=torch.int32)
+        want = ref.generate_ids(torch.from_numpy(ids), torch.from_numpy(mask.astype(bool)), 24, sp,
+                                forced_text=forced).cpu().numpy()
+        e.inject_pse_timeout()
+        got = e.generate_ids(torch.from_numpy(ids), torch.from_numpy(mask.astype(bool)), 24, sp,
+                             forced_text=forced).cpu().numpy()
+        assert not e.pse_active()
+        assert np.array_equal(want, got)
+    finally:
+        e.close()

@@ -26,6 +26,14 @@ PARAMS = [
                               audio_top_p=1.0, audio_top_k=0, audio_repetition_penalty=0.9), 3),
     ("g_nvq32_bf16", dict(text_temperature=0.0, text_top_p=1.0, text_top_k=50, audio_temperature=1.7,
                           audio_top_p=0.8, audio_top_k=25, audio_repetition_penalty=1.0), 11),
+    # wide text candidate sets (key-bin sampler, topk.h block_wide_draw): no top-k filter
+    # (inference_utils.py:136), with and without top-p, and a top_k above the sorted form's 2,048
+    ("g_nvq4_bf16", dict(text_temperature=1.5, text_top_p=1.0, text_top_k=0, audio_temperature=1.7,
+                         audio_top_p=0.8, audio_top_k=25, audio_repetition_penalty=1.0), 13),
+    ("g_nvq16_bf16", dict(text_temperature=1.0, text_top_p=0.9, text_top_k=-1, audio_temperature=1.0,
+                          audio_top_p=0.95, audio_top_k=0, audio_repetition_penalty=1.1), 17),
+    ("g_nvq4_stop_fp32", dict(text_temperature=0.8, text_top_p=0.95, text_top_k=5000, audio_temperature=1.2,
+                              audio_top_p=1.0, audio_top_k=50, audio_repetition_penalty=1.0), 19),
 ]
 
 
@@ -57,7 +65,7 @@ def _heads(lg, cfg):
     return [lg[:, :cfg.vocab]] + [lg[:, cfg.vocab + j * A: cfg.vocab + (j + 1) * A] for j in range(cfg.n_vq)]
 
 
-@pytest.mark.parametrize("name,kw,seed", PARAMS, ids=[p[0] for p in PARAMS])
+@pytest.mark.parametrize("name,kw,seed", PARAMS, ids=[f"{p[0]}-k{p[1]['text_top_k']}" for p in PARAMS])
 def test_sampled_steps_match_oracle(gpu, golden, name, kw, seed):
     from moss_tts_amd.engine import GenerateSession, sampling_params
     g, c, cfg, W = _case(golden, name)
@@ -69,7 +77,7 @@ def test_sampled_steps_match_oracle(gpu, golden, name, kw, seed):
     st = O.init_state(cfg, ids)
     rng = O.PhiloxDraw(seed)
     hist = ids.copy()
-    sampled_text = sampled_audio = 0
+    sampled_text = sampled_audio = free_text = 0
     for step in range(c["steps"]):
         if step:
             if sess.finished:
@@ -79,6 +87,7 @@ def test_sampled_steps_match_oracle(gpu, golden, name, kw, seed):
         rows = sess.fetch().cpu().numpy()
         assert rows.shape[1] == T + step + 1
         samp_text = ~st["is_stopping"] & (st["delayed"] > cfg.n_vq)
+        free_text += int((samp_text & ~st["is_audio"]).sum())  # text mode: the full masked row
         nt, na = O.decide_step(ctx, cfg, _heads(lg, cfg), step, st, hist, kw, rng=rng)
         got = rows[:, T + step]
         assert np.array_equal(got[:, 0], nt), (step, got[:, 0], nt)
@@ -88,6 +97,8 @@ def test_sampled_steps_match_oracle(gpu, golden, name, kw, seed):
         hist = rows
     eng.close()
     assert sampled_audio > 0 and sampled_text > 0
+    if kw["text_temperature"] > 0 and not 0 < kw["text_top_k"] <= 2048:
+        assert free_text > 0, "the wide text sampler was never exercised"
 
 
 def test_sampled_generate_properties(gpu, golden):
@@ -112,17 +123,17 @@ def test_sampled_generate_properties(gpu, golden):
     assert ((gen[..., 1:] >= 0) & (gen[..., 1:] <= cfg.audio_pad_code)).all()
 
 
-def test_top_k_limits(gpu, golden):
-    """sampled text keeps at most 2,048 candidates: text_top_k 0 (whole vocab) or above is
-    refused loudly; any audio top_k (1,025 codes) is accepted"""
+def test_top_k_range(gpu, golden):
+    """every top_k the reference accepts runs (inference_utils.py:136: <= 0 = no filter, any k
+    up to the vocab): text 0 / -1 / 2,048 / 4,096 / the whole vocab, audio 0 / 5,000; sampled
+    ids stay inside the vocab"""
     from moss_tts_amd.engine import sampling_params
     name = "g_nvq4_bf16"
     g, c, cfg, W = _case(golden, name)
     ids, mask = torch.from_numpy(g[name + "/input_ids"]), torch.from_numpy(g[name + "/mask"])
     eng = _engine(cfg, W)
-    for k in (0, 4096):
-        with pytest.raises(RuntimeError):
-            eng.generate_ids(ids, mask, 4, sampling_params(text_top_k=k))
-    out = eng.generate_ids(ids, mask, 4, sampling_params(audio_top_k=5000, text_top_k=2048))
-    assert out.shape[1] >= ids.shape[1] + 1
+    for tk, ak in ((0, 25), (-1, 0), (2048, 5000), (4096, 25), (cfg.vocab, 25)):
+        out = eng.generate_ids(ids, mask, 6, sampling_params(text_top_k=tk, audio_top_k=ak)).cpu().numpy()
+        assert out.shape[1] >= ids.shape[1] + 1
+        assert ((out[..., 0] >= 0) & (out[..., 0] < cfg.vocab)).all()
     eng.close()
