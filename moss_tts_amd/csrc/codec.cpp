@@ -218,6 +218,7 @@ extern "C" int mtts_codec_load_weight(mtts_codec* k, const char* name, const voi
     const int DL = c.stages[c.n_stages - 1].hidden;
     if (bytes != (size_t)c.patch * DL * 2) return fail(MTTS_E_INVALID, "size mismatch for " + n);
     const bf16_t* from = reinterpret_cast<const bf16_t*>(src);
+    if (on_dev) HIPCHK(hipDeviceSynchronize());  // the source may be in flight on the caller's stream
     if (!on_dev) {
       if (int rc = ensure_staging(&k->W, bytes)) return rc;
       HIPCHK(hipMemcpyAsync(k->W.staging, src, bytes, hipMemcpyHostToDevice, k->W.stream));

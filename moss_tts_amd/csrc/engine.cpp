@@ -297,6 +297,10 @@ bool layer_target(const LayerW& w, const std::string& rest, int H, int I, int Hq
 int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void* src, size_t bytes, int on_dev) {
   hipStream_t s = e->stream;
   if (bytes != t.expect * 2) return fail(MTTS_E_INVALID, std::string("size mismatch for ") + name);
+  // a device source may still be in flight on another stream of the caller (e.g. a torch tensor
+  // just produced on torch's stream): the engine stream does not order after it, so wait for the
+  // whole device once per load (one-time cost)
+  if (on_dev) HIPCHK(hipDeviceSynchronize());
   if (!t.pack) {
     HIPCHK(hipMemcpyAsync(t.dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   } else {

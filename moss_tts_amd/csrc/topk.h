@@ -321,7 +321,9 @@ __device__ int block_wide_draw(F val, int V, int K, float top_p, float u, int* h
     if (ck >= 0 && w_cut_t == t) { w_cut_key = ck; w_cut_r = cr; }
     __syncthreads();
   };
-  auto evf = [&](int key) { return expf(okey16_val((uint32_t)key) - mx); };
+  // exp in double, rounded once to fp32: correctly rounded, so the oracle's numpy exp gives the
+  // same bits (fp32 expf implementations differ in the last place)
+  auto evf = [&](int key) { return (float)exp((double)(okey16_val((uint32_t)key) - mx)); };
   int lim_key = -1, lim_r = 0;
   if (top_p < 1.0f) {
     const float S = chunk_sums(evf, -1, 0);

@@ -526,7 +526,8 @@ def wide_keep(x, K, top_p):
     keys = WIDE_BINS - 1 - np.arange(WIDE_BINS)
     with np.errstate(invalid="ignore", over="ignore"):
         mx = f32(okey16_val(keys[np.nonzero(cnt)[0][0]]))
-        ev = np.exp((okey16_val(keys) - mx).astype(f32)).astype(f32)
+        # exp of the fp32 difference in double, rounded once (the engine's correctly rounded form)
+        ev = np.exp((okey16_val(keys) - mx).astype(f32).astype(np.float64)).astype(f32)
         if top_p is not None and top_p < 1.0:
             S, _, _ = _wide_sums(cnt, ev)
             pf = _bf.rnd((ev / S).astype(f32))
