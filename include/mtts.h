@@ -155,6 +155,18 @@ int mtts_local_generate_begin(mtts_engine* eng, const int64_t* input_ids_dev, co
                               int T, int max_new_tokens, int n_vq_for_inference, const mtts_sampling* sampling,
                               void* stream);
 int mtts_local_generate_decode(mtts_engine* eng, int n_steps, void* stream);
+/* Per-channel processors of generation_config.do_samples / .layers (:356-368) for the next
+ * mtts_local_generate_begin / mtts_local_generate calls: channel i < n takes ch[i] (temperature,
+ * top_k <= 0 = none, top_p 1 = none, repetition_penalty, ignored on channel 0); the sampling
+ * struct then only supplies the seed.  n = 0 reverts to its text_* / audio_* split. */
+typedef struct mtts_channel_sampling {
+  int do_sample;
+  float temperature;
+  int top_k;
+  float top_p;
+  float repetition_penalty;
+} mtts_channel_sampling;
+int mtts_local_set_sampling(mtts_engine* eng, const mtts_channel_sampling* ch, int n);
 int mtts_local_generate(mtts_engine* eng, const int64_t* input_ids_dev, const uint8_t* attention_mask_dev, int B, int T,
                         int max_new_tokens, int n_vq_for_inference, const mtts_sampling* sampling, int chunk_steps,
                         int* n_rows, void* stream);

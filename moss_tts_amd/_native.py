@@ -51,6 +51,11 @@ class MttsCodecConfig(ctypes.Structure):
                 ("max_batch", ctypes.c_int), ("max_frames", ctypes.c_int), ("max_chunk_frames", ctypes.c_int)]
 
 
+class MttsChannelSampling(ctypes.Structure):
+    _fields_ = [("do_sample", ctypes.c_int), ("temperature", ctypes.c_float), ("top_k", ctypes.c_int),
+                ("top_p", ctypes.c_float), ("repetition_penalty", ctypes.c_float)]
+
+
 P = ctypes.c_void_p
 I = ctypes.c_int
 F = ctypes.c_float
@@ -81,6 +86,7 @@ _SIGS = {
     "mtts_generate": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, I, ctypes.POINTER(I), P]),
     "mtts_local_generate_begin": (I, [P, P, P, I, I, I, I, ctypes.POINTER(MttsSampling), P]),
     "mtts_local_generate_decode": (I, [P, I, P]),
+    "mtts_local_set_sampling": (I, [P, ctypes.POINTER(MttsChannelSampling), I]),
     "mtts_local_generate": (I, [P, P, P, I, I, I, I, ctypes.POINTER(MttsSampling), I, ctypes.POINTER(I), P]),
     "mtts_local_forward": (I, [P, P, P, I, I, I, I, P, P, I, P]),
     "mtts_local_frame_bytes": (I, [P, I, ctypes.POINTER(U64)]),

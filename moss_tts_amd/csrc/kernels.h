@@ -154,6 +154,15 @@ struct DecAttnArgs {
 
 constexpr int TOPK_CAP = 2048;  // largest sampler candidate set (topk.h); the host rejects top_k above it
 
+// MossTTSLocal: one channel's processor set (moss_tts_local/modeling_moss_tts.py:356-368)
+constexpr int LOCAL_MAXC = 64;
+struct ChSampling {
+  int sample;          // do_samples[i]: 0 = argmax of the raw logits
+  float temp, top_p;   // TemperatureLogitsWarper / TopPLogitsWarper (1.0: absent)
+  float pen;           // RepetitionPenaltyLogitsProcessor (1.0: absent; never on channel 0)
+  int top_k;           // TopKLogitsWarper (<= 0: absent)
+};
+
 struct GenDev {
   // scalars
   int T0;          // prompt length
@@ -172,6 +181,7 @@ struct GenDev {
   unsigned long long seed;
   MttsIds ids;
   int topk_overflow;  // a sampler cut threshold ties at TOPK_CAP (reported by poll)
+  ChSampling lch[LOCAL_MAXC];  // MossTTSLocal: per-channel processors
 };
 
 struct GenBufs {

@@ -41,6 +41,7 @@ struct LocalParts {
   int* finished = nullptr;  // [Bmax]
   uint8_t* seen = nullptr;  // [Bmax][C][audio_rows] channel histories (repetition penalty)
   int n_ch = 0;
+  std::vector<ChSampling> ch_table;  // mtts_local_set_sampling: per-channel processors (empty: from mtts_sampling)
   bool no_graph = false;
   std::unordered_map<long long, hipGraphExec_t> graphs;
 };
@@ -387,10 +388,31 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   const mtts_config& c = e->c;
   if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
     return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
-  if (sp && sp->text_temperature > 0.f && (sp->text_top_k <= 0 || sp->text_top_k > 1024))
-    return fail(MTTS_E_UNSUPPORTED, "sampled text channel needs top_k in [1, 1024]");
-  if (sp && sp->audio_temperature > 0.f && sp->audio_top_k > 1024) return fail(MTTS_E_UNSUPPORTED, "audio top_k > 1024");
   LocalParts& p = *e->lp;
+  // per-channel processors (:356-368): the table set by mtts_local_set_sampling, else channel 0
+  // from the text_* fields and every codebook channel from the audio_* fields
+  ChSampling chs[LOCAL_MAXC];
+  for (int c = 0; c < p.C; ++c) {
+    ChSampling& q = chs[c];
+    if (c < (int)p.ch_table.size()) {
+      q = p.ch_table[c];
+    } else if (!sp) {
+      q = ChSampling{0, 1.f, 1.f, 1.f, 0};
+    } else if (c == 0) {
+      q = ChSampling{sp->text_temperature > 0.f, sp->text_temperature > 0.f ? sp->text_temperature : 1.f,
+                     sp->text_top_p, 1.f, sp->text_top_k};
+    } else {
+      q = ChSampling{sp->audio_temperature > 0.f, sp->audio_temperature > 0.f ? sp->audio_temperature : 1.f,
+                     sp->audio_top_p, sp->audio_repetition_penalty, sp->audio_top_k};
+    }
+    if (c == 0) q.pen = 1.f;  // the reference attaches no repetition penalty to the text channel
+    // keep-all-ties top-k holds <= TOPK_CAP candidates: the text channel needs a cap that leaves
+    // room for ties; the 1,025-code audio rows fit whole
+    if (q.sample && c == 0 && (q.top_k <= 0 || q.top_k > 1024))
+      return fail(MTTS_E_UNSUPPORTED, "sampled text channel needs top_k in [1, 1024]");
+    if (q.sample && q.top_k > 1024) return fail(MTTS_E_UNSUPPORTED, "channel top_k > 1024");
+    if (q.sample && !(q.temp > 0.f)) return fail(MTTS_E_INVALID, "sampled channel needs a positive temperature");
+  }
   hipStream_t s = enter(e, stream);
   GenDev& g = e->hst;
   std::memset(&g, 0, sizeof(g));
@@ -399,16 +421,8 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   g.vocab = c.vocab; g.audio_rows = e->audio_rows;
   // generation_config.layers (:356-368): channel 0 <- text_*, channels >= 1 <- audio_*;
   // do_samples[i] = temperature > 0; repetition penalty on audio channels only (i != 0)
-  if (sp) {
-    g.text_sample = sp->text_temperature > 0.f;
-    g.audio_sample = sp->audio_temperature > 0.f;
-    g.text_temp = g.text_sample ? sp->text_temperature : 1.f;
-    g.audio_temp = g.audio_sample ? sp->audio_temperature : 1.f;
-    g.text_top_p = sp->text_top_p; g.audio_top_p = sp->audio_top_p;
-    g.text_top_k = sp->text_top_k; g.audio_top_k = sp->audio_top_k;
-    g.rep_penalty = sp->audio_repetition_penalty;
-    g.seed = sp->seed;
-  }
+  for (int c = 0; c < p.C; ++c) g.lch[c] = chs[c];
+  if (sp) g.seed = sp->seed;
   e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = nullptr;
   p.n_ch = n_channels(e, n_vq_for_inference);
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
@@ -419,6 +433,17 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   if (rc) return rc;
   e->steps_issued = 1;
   leave(e, stream);
+  return 0;
+}
+
+extern "C" int mtts_local_set_sampling(mtts_engine* e, const mtts_channel_sampling* ch, int n) {
+  if (!e || n < 0 || (n > 0 && !ch)) return fail(MTTS_E_INVALID, "null argument");
+  if (!e->lp) return fail(MTTS_E_UNSUPPORTED, "not a MossTTSLocal engine");
+  if (n > e->lp->C) return fail(MTTS_E_INVALID, "more channel settings than channels");
+  e->lp->ch_table.clear();
+  for (int i = 0; i < n; ++i)
+    e->lp->ch_table.push_back(ChSampling{ch[i].do_sample != 0, ch[i].temperature, ch[i].top_p,
+                                         ch[i].repetition_penalty, ch[i].top_k});
   return 0;
 }
 
@@ -522,11 +547,7 @@ extern "C" int mtts_k_local_pick(const uint16_t* logits, int ld, int V, int ch, 
   GenDev g;
   std::memset(&g, 0, sizeof(g));
   g.step = step; g.audio_rows = audio_rows; g.seed = seed;
-  g.text_sample = g.audio_sample = temperature > 0.f;
-  g.text_temp = g.audio_temp = temperature > 0.f ? temperature : 1.f;
-  g.text_top_k = g.audio_top_k = top_k;
-  g.text_top_p = g.audio_top_p = top_p;
-  g.rep_penalty = penalty;
+  g.lch[ch] = ChSampling{temperature > 0.f, temperature > 0.f ? temperature : 1.f, top_p, penalty, top_k};
   GenDev* d = nullptr;
   HIPCHK(hipMallocAsync((void**)&d, sizeof(GenDev), s));
   HIPCHK(hipMemcpyAsync(d, &g, sizeof(g), hipMemcpyHostToDevice, s));

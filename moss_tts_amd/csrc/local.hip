@@ -149,9 +149,8 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ s
   __shared__ float ev[TOPK_CAP];
   const int b = blockIdx.x, t = threadIdx.x;
   const bf16_t* row = logits + (size_t)b * ld;
-  const bool audio = ch > 0;
-  const int sample = audio ? st->audio_sample : st->text_sample;
-  if (!sample) {
+  const ChSampling cs = st->lch[ch];
+  if (!cs.sample) {
     ArgMax a{-INFINITY, 0x7fffffff};
     if ((ld & 7) == 0 && ((uintptr_t)row & 15) == 0) {  // 16-byte loads (the text channel: ~19 per thread instead of ~150 2-byte loads)
       const int nv = V >> 3;
@@ -175,11 +174,9 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ s
     }
     return;
   }
-  const float temp = audio ? st->audio_temp : st->text_temp;
-  const float pen = audio ? st->rep_penalty : 1.0f;
-  const int top_k = audio ? st->audio_top_k : st->text_top_k;
-  const float top_p = audio ? st->audio_top_p : st->text_top_p;
-  const uint8_t* sn = (audio && pen != 1.0f) ? seen + ((size_t)b * C + ch) * st->audio_rows : nullptr;
+  const float temp = cs.temp, pen = ch > 0 ? cs.pen : 1.0f, top_p = cs.top_p;
+  const int top_k = cs.top_k;
+  const uint8_t* sn = (ch > 0 && pen != 1.0f) ? seen + ((size_t)b * C + ch) * st->audio_rows : nullptr;
   auto val = [&](int i) -> float {
     float v = bf2f(row[i]);
     if (sn && sn[i]) v = v < 0.f ? rbf(v * pen) : rbf(v / pen);

@@ -224,6 +224,15 @@ class Engine:
         N.check(N.load().mtts_generate_fetch(self._h, _ptr(out), n.value, _stream_ptr(self.device)), "fetch")
         return out
 
+    def local_set_sampling(self, channels):
+        """MossTTSLocal per-channel processors for the following generations: a list of
+        (do_sample, temperature, top_k, top_p, repetition_penalty) per channel (top_k <= 0 /
+        top_p 1 / penalty 1 = that processor absent); [] reverts to the sampling struct's split"""
+        arr = (N.MttsChannelSampling * max(1, len(channels)))()
+        for i, (d, t, k, p, r) in enumerate(channels):
+            arr[i] = N.MttsChannelSampling(int(bool(d)), float(t), int(k), float(p), float(r))
+        N.check(N.load().mtts_local_set_sampling(self._h, arr, len(channels)), "local_set_sampling")
+
     def local_frame_bytes(self, n_vq_for_inference: int = -1) -> int:
         v = ctypes.c_uint64()
         N.check(N.load().mtts_local_frame_bytes(self._h, n_vq_for_inference, ctypes.byref(v)), "local_frame_bytes")

@@ -7,9 +7,8 @@ local_to_speech_embedding_mlps, layer_norm_before_lm_heads, lm_heads) and the
 
 generation_config (README `moss_tts_local/README.md:203-220`): `n_vq_for_inference`,
 `do_samples` (per channel), `layers` (per channel dict of repetition_penalty / temperature /
-top_k / top_p), `max_new_tokens` or `max_length`, `eos_token_id`.  The engine takes one
-processor set for channel 0 and one shared by every codebook channel (the README's layout);
-other layouts raise NotImplementedError.
+top_k / top_p), `max_new_tokens` or `max_length`, `eos_token_id`.  Every channel takes its own
+processor set (mtts_local_set_sampling).  A sampled text channel needs a top_k (<= 1,024).
 """
 import copy
 import os
@@ -137,34 +136,21 @@ class MossTTSDelayModel(PreTrainedModel):
 
     # ---- generate -----------------------------------------------------------------
     def _sampling(self, gc, n_ch: int):
-        """generation_config.do_samples / layers -> engine sampling parameters (:356-368)"""
+        """generation_config.do_samples / layers -> the engine's per-channel processor table
+        (`:356-368`: RepetitionPenalty (never on channel 0) -> Temperature -> TopK -> TopP, each
+        only when its key is set; channels with do_samples[i] False take the argmax)"""
         do = list(getattr(gc, "do_samples", None) or [bool(getattr(gc, "do_sample", False))] * self.channels)
         layers = list(getattr(gc, "layers", None) or [{}] * self.channels)
         if len(do) < n_ch or len(layers) < n_ch:
             raise ValueError("generation_config.do_samples / layers must cover every generated channel")
-
-        def knobs(i):
-            if not do[i]:
-                return (0.0, 0, 1.0, 1.0)
+        table = []
+        for i in range(n_ch):
             lc = layers[i] or {}
-            t = lc.get("temperature")
-            k = lc.get("top_k")
-            p = lc.get("top_p")
-            r = lc.get("repetition_penalty")
-            return (1.0 if t is None else float(t), 0 if k is None else int(k), 1.0 if p is None else float(p),
-                    1.0 if (r is None or i == 0) else float(r))
-
-        text = knobs(0)
-        audio = [knobs(i) for i in range(1, n_ch)]
-        if audio and any(a != audio[0] for a in audio):
-            raise NotImplementedError("per-codebook processor settings must be equal for channels >= 1")
-        a = audio[0] if audio else (0.0, 0, 1.0, 1.0)
-        if text[0] > 0 and text[1] <= 0:
-            raise NotImplementedError("sampling the text channel needs top_k (<= 1024)")
+            t, k, p, r = (lc.get(x) for x in ("temperature", "top_k", "top_p", "repetition_penalty"))
+            table.append((bool(do[i]), 1.0 if t is None else float(t), 0 if k is None else int(k),
+                          1.0 if p is None else float(p), 1.0 if (r is None or i == 0) else float(r)))
         seed = int(torch.randint(0, 2 ** 62, (1,)).item())
-        return sampling_params(text_temperature=text[0], text_top_k=text[1], text_top_p=text[2],
-                               audio_temperature=a[0], audio_top_k=a[1], audio_top_p=a[2],
-                               audio_repetition_penalty=a[3], seed=seed)
+        return table, sampling_params(text_temperature=0.0, audio_temperature=0.0, seed=seed)
 
     @torch.inference_mode()
     def generate(self, input_ids: torch.LongTensor, attention_mask: Optional[torch.Tensor] = None,
@@ -190,8 +176,12 @@ class MossTTSDelayModel(PreTrainedModel):
                 raise NotImplementedError("one eos_token_id")
             eos = eos[0]
         eng = self.engine(B, T + max_new, int(eos))
-        sp = self._sampling(gc, n_ch)
-        gen = eng.local_generate_ids(input_ids, attention_mask, max_new, nq, sampling=sp).to(input_ids.device)
+        table, sp = self._sampling(gc, n_ch)
+        eng.local_set_sampling(table)
+        try:
+            gen = eng.local_generate_ids(input_ids, attention_mask, max_new, nq, sampling=sp).to(input_ids.device)
+        finally:
+            eng.local_set_sampling([])
         starts = find_last_equal_C(input_ids[..., 0], self.config.audio_start_token_id)
         lengths = T - starts - 1
         return [(lengths[b], gen[b, int(starts[b]):]) for b in range(B)]

@@ -258,3 +258,41 @@ def test_local_model_generate_dropin(gpu, gl):
         [{"repetition_penalty": 1.1, "temperature": 1.0, "top_p": 0.95, "top_k": 50}] * cfg.n_vq
     out = model.generate(input_ids=ids, generation_config=gc)
     assert out[0][1].shape[1] == cfg.n_vq + 1
+
+
+def test_local_per_channel_processors(gpu, gl):
+    """generation_config.do_samples / layers set per channel (`:356-368`): every channel takes
+    its own processor set.  (1) sampled channels with top_k = 1 (any temperature / top_p) equal
+    the argmax, so a table alternating greedy and top-1 channels reproduces the greedy run; (2) one
+    sampled channel with a wide top_k changes that channel only from there on: the channels before
+    it in the first frame stay the greedy ones, and two seeds draw differently."""
+    from transformers import GenerationConfig
+    name = "l_nvq8_depth4_bf16"
+    g, c, cfg, W = lcase(gl, name)
+    ids = torch.from_numpy(g[name + "/input_ids"]).cuda()
+    model = build_local_model(cfg, W)
+    C = cfg.n_vq + 1
+    steps = 6
+
+    def run(do, layers, seed=0):
+        gc = GenerationConfig(max_new_tokens=steps, eos_token_id=cfg.eos_token_id)
+        gc.n_vq_for_inference = cfg.n_vq
+        gc.do_samples, gc.layers = do, layers
+        torch.manual_seed(seed)
+        return [r.cpu() for _, r in model.generate(input_ids=ids, generation_config=gc)]
+
+    greedy = run([False] * C, [{}] * C)
+    top1 = [{"temperature": 0.5 + 0.1 * i, "top_k": 1, "top_p": 0.9, "repetition_penalty": 1.0} for i in range(C)]
+    mixed = run([i % 2 == 1 for i in range(C)], top1)
+    assert all(torch.equal(a, b) for a, b in zip(greedy, mixed))
+    j0 = 3
+    layers = [{}] * C
+    layers[j0] = {"temperature": 2.0, "top_k": 1000, "top_p": 1.0}
+    do = [i == j0 for i in range(C)]
+    a, b = run(do, layers, 1), run(do, layers, 2)
+    T = ids.shape[1]
+    starts = L.find_last_equal_C(g[name + "/input_ids"][..., 0], cfg.audio_start_token_id)
+    for r in range(len(greedy)):
+        f0 = T - int(starts[r])  # first generated row of this row's output
+        assert torch.equal(a[r][f0, :j0], greedy[r][f0, :j0]) and torch.equal(b[r][f0, :j0], greedy[r][f0, :j0])
+    assert any(not torch.equal(x[:, j0], y[:, j0]) for x, y in zip(a, b))
