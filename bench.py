@@ -407,8 +407,15 @@ def main_local(args, world, rank, local):
         frame_bytes = fb + kv_pos * B * (T + frames / 2)
         ms = ctypes.c_float()
         nb = ctypes.c_uint64()
-        Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 2, 0, B, 50, ctypes.byref(ms), ctypes.byref(nb)), "time_gemv")
+        # the frame's dominant launch: the depth stack's gate|up (4 layers x 33 channels per frame;
+        # r02_h_local_kernel_stats.csv: 21 % of GPU time, then the depth down at 17 %)
+        Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 6, 0, B, 200, ctypes.byref(ms), ctypes.byref(nb)), "time_gemv")
         ach = nb.value / (ms.value * 1e-3) / 1e9
+        ms_dn = ctypes.c_float()
+        nb_dn = ctypes.c_uint64()
+        Nn.check(Nn.load().mtts_engine_time_gemv(eng._h, 7, 0, B, 200, ctypes.byref(ms_dn), ctypes.byref(nb_dn)),
+                 "time_gemv")
+        ach_dn = nb_dn.value / (ms_dn.value * 1e-3) / 1e9
         traffic, traffic_src = pmc_traffic("local")
         res = {
             "metric": METRIC, "value": round(audio_total / dt_max, 4), "unit": "audio-s/s",
@@ -430,8 +437,13 @@ def main_local(args, world, rank, local):
             "frame_hbm_frac": round(frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
-                         "kernel": "gemv_kernel gate|up (fused RMSNorm prologue, SwiGLU epilogue), backbone, layers rotated", "alg_bytes_per_launch": int(nb.value),
-                         "avg_launch_us": round(ms.value * 1e3, 2)},
+                         "kernel": "depth-stack gate|up GEMV (fused RMSNorm prologue, SwiGLU epilogue; the frame's "
+                                   "most-time kernel), B rows, the 4 depth layers walked as the channel loop does "
+                                   "(their weights stay MALL-resident across a frame)",
+                         "alg_bytes_per_launch": int(nb.value), "avg_launch_us": round(ms.value * 1e3, 2),
+                         "depth_down": {"achieved": round(ach_dn, 1), "frac": round(ach_dn / HBM_PEAK_GBS, 4),
+                                        "alg_bytes_per_launch": int(nb_dn.value),
+                                        "avg_launch_us": round(ms_dn.value * 1e3, 2)}},
         }
         if not args.no_cpu_baseline and world == 1:
             res["cpu_baseline"] = cpu_baseline_local(int(T), frames)

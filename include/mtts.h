@@ -90,7 +90,9 @@ int mtts_engine_weight_bytes(const mtts_engine* eng, uint64_t* bytes);
  * model -- which: 0 q|k|v, 1 o_proj, 2 gate|up+SwiGLU, 3 down, 4 heads -- and its
  * algorithmic bytes per launch (weights once + activations + outputs); which 5: the
  * persistent streaming decode stack (every layer in one launch, B = 1, at the engine's
- * current decode position; bytes = all layer weights + the K/V rows read). */
+ * current decode position; bytes = all layer weights + the K/V rows read); which 6 / 7
+ * (MossTTSLocal): the depth stack's gate|up+SwiGLU / down of depth layer `layer`, launched as
+ * the channel loop launches them, walking the depth layers. */
 int mtts_engine_time_gemv(mtts_engine* eng, int which, int layer, int B, int iters, float* avg_ms,
                           uint64_t* alg_bytes);
 

@@ -947,6 +947,12 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
                                      uint64_t* alg_bytes) {
   if (!e || !avg_ms || !alg_bytes || iters <= 0) return fail(MTTS_E_INVALID, "null argument");
   const mtts_config& c = e->c;
+  if (which == 6 || which == 7) {
+    // MossTTSLocal: the depth stack's gate|up (6) / down (7), the Local frame's dominant launches
+    if (!e->lp) return fail(MTTS_E_UNSUPPORTED, "no depth stack in a MossTTSDelay engine");
+    hipSetDevice(e->device);
+    return local_time_proj(e, which - 4, layer, B, iters, avg_ms, alg_bytes);
+  }
   if (layer < 0 || layer >= c.layers || B <= 0 || B > c.max_batch) return fail(MTTS_E_INVALID, "bad layer/B");
   hipSetDevice(e->device);
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, I = c.inter;

@@ -184,3 +184,5 @@ void local_clear_graphs(mtts_engine* e);
 int local_init_random(mtts_engine* e, uint64_t seed);
 // 1: the name belongs to the local stage and was loaded (or failed: *rc set); 0: not a local name
 int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev, int* rc);
+// mtts_engine_time_gemv's depth-stack cases: proj 2 = gate|up, 3 = down of depth layer `layer`
+int local_time_proj(mtts_engine* e, int proj_kind, int layer, int B, int iters, float* avg_ms, uint64_t* alg_bytes);

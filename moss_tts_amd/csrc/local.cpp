@@ -291,6 +291,53 @@ int local_init_random(mtts_engine* e, uint64_t seed) {
   return 0;
 }
 
+// One depth-stack projection at the decode shape, launched as run_layers launches it (gate|up:
+// Qwen3RMSNorm prologue + SwiGLU epilogue; down: residual add + sum-of-squares epilogue, split-K
+// where proj() picks it).  Consecutive launches walk the depth layers the way the channel loop
+// does, so the weights come from wherever the frame finds them (the 4 depth layers stay in the
+// MALL across a frame's 33 channels); the algorithmic bytes count them once per launch.
+int local_time_proj(mtts_engine* e, int proj_kind, int layer, int B, int iters, float* avg_ms, uint64_t* alg_bytes) {
+  const LocalParts& p = *e->lp;
+  if (proj_kind != 2 && proj_kind != 3) return fail(MTTS_E_INVALID, "depth projection: 2 (gate|up) or 3 (down)");
+  if (layer < 0 || layer >= p.LL || B <= 0 || B > e->c.max_batch || iters <= 0) return fail(MTTS_E_INVALID, "bad layer/B");
+  const Stack st = local_stack(e);
+  const int H = st.H, I = st.I, NT = H / 16;
+  hipStream_t s = e->stream;
+  HIPCHK(hipMemsetAsync(st.ss, 0, (size_t)B * NT * sizeof(float), s));
+  auto launch = [&](int l) -> int {
+    const LayerW& w = st.L[l % p.LL];
+    if (proj_kind == 2) {
+      GemvArgs g = gemv_args(w.gu, st.xn, H, st.act, I, B, I, H);
+      if (int rc = normed_input(e, st, g, w.post_norm, B, s, 0)) return rc;
+      g.force_nw = e->nw[2]; g.force_u = e->nu[2];
+      HIPCHK(proj(e, g, EPI_SWIGLU, s));
+    } else {
+      GemvArgs g = gemv_args(w.down, st.act, I, st.h, H, B, H, I);
+      g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3]; g.force_u = e->nu[3];
+      HIPCHK(proj(e, g, EPI_RESADD, s));
+    }
+    return 0;
+  };
+  if (int rc = launch(layer)) return rc;
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
+  HIPCHK(hipEventRecord(a, s));
+  for (int i = 0; i < iters; ++i)
+    if (int rc = launch(layer + 1 + i)) return rc;
+  HIPCHK(hipEventRecord(b, s));
+  HIPCHK(hipEventSynchronize(b));
+  float ms = 0.f;
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  hipEventDestroy(a);
+  hipEventDestroy(b);
+  *avg_ms = ms / iters;
+  const uint64_t rows = proj_kind == 2 ? 2ull * I : (uint64_t)H, K = proj_kind == 2 ? H : I,
+                 N = proj_kind == 2 ? I : H;
+  *alg_bytes = 2ull * rows * K + 2ull * B * K + 2ull * B * N * (proj_kind == 3 ? 2 : 1);
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // speech_embedding_to_local_mlp(x) -> the depth stack's residual stream (+ its per-16-column
 // sums of squares for the first layer's input norm); x [B, H], or with tok != nullptr the

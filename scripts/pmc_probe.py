@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Launch the bench's dominant kernel on its own (the decode step's gate|up GEMV instance, via
 mtts_engine_time_gemv: layers rotated, so no launch re-reads a matrix the previous one left in
-the 256 MB MALL; --config pse: the batch-1 persistent streaming decode launch, every layer) for
+the 256 MB MALL; --config local: the depth stack's gate|up at B=8, its 4 layers walked as the
+frame walks them; --config pse: the batch-1 persistent streaming decode launch, every layer) for
 rocprofv3 PMC passes:
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D -o f --output-format csv -- python3 scripts/pmc_probe.py --config clone
@@ -36,7 +37,7 @@ def run(cfg_name, iters):
         B = 1
     eng = Engine(cfg, 0)
     eng.init_random(0)
-    which = 2
+    which = 6 if cfg_name == "local" else 2  # local: the depth stack's gate|up (the frame's dominant launch)
     if cfg_name == "pse":  # the batch-1 decode stack as one persistent launch (pse.hip)
         if not eng.pse_active():
             raise SystemExit("persistent streaming decode inactive")
