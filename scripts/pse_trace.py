@@ -73,4 +73,30 @@ for l in range(1, layers):
     a0, a1 = tr[l - 1, 9], tr[l, 9]
     lay.append(np.median(a1 - a0) / 100)
 print("median layer period (down done -> down done) us:", np.round(lay, 1))
+# per-phase table over the steady-state layers (1 .. L-1): each phase = the median over CUs of
+# its closing event minus the median of its opening event, then the median over layers
+PH = [("h gather + input norm", 0, 1), ("q|k|v stream + publish", 1, 2), ("attention chain (q|k|v done -> o input)", 2, 4),
+      ("o_proj stream + publish", 4, 5), ("h gather + post norm", 5, 6), ("gate|up stream + publish", 6, 7),
+      ("act gather", 7, 8), ("down stream + publish", 8, 9)]
+med = lambda l, ev: np.median(tr[l, ev][tr[l, ev] > 0]) / 100
+rows = []
+for name, a0, a1 in PH:
+    d = [med(l, a1) - med(l, a0) for l in range(1, layers)]
+    rows.append((name, float(np.median(d))))
+# the attention CUs' own view of the chain
+att = [("A: q|k|v gather", 2, 15), ("A: chunks", 16, 17), ("A: unit merge + publish", 17, 3)]
+for name, a0, a1 in att:
+    d = []
+    for l in range(1, layers):
+        v0, v1 = tr[l, a0], tr[l, a1]
+        ok = (v0 > 0) & (v1 > 0)
+        if ok.any():
+            d.append(np.median(v1[ok] - v0[ok]) / 100)
+    if d:
+        rows.append((name, float(np.median(d))))
+print("| phase (steady-state layer, median) | us |")
+print("|---|---|")
+for name, v in rows:
+    print(f"| {name} | {v:.2f} |")
+print(f"| layer period | {float(np.median(lay)):.2f} |")
 e.close()

@@ -1,0 +1,29 @@
+"""AddressSanitizer run of libmtts's host code: tests/native/asan_driver is the
+engine / Local / codec sources compiled with host-side ASan (`make -C tests/native`, done on
+the build side like libmtts itself) plus a C driver that walks every C entry point and its error
+paths.  Any heap overflow, use-after-free or leak in engine.cpp / local.cpp / codec.cpp fails
+the run; leaks inside the ROCm runtime are suppressed (tests/native/lsan.supp)."""
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+EXE = os.path.join(HERE, "native", "asan_driver")
+
+
+def test_asan_driver_clean():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if not os.path.exists(EXE):
+        pytest.skip("tests/native/asan_driver not built (make -C tests/native)")
+    env = dict(os.environ)
+    env["ASAN_OPTIONS"] = "detect_leaks=1:protect_shadow_gap=0:halt_on_error=1:verify_asan_link_order=0"
+    env["LSAN_OPTIONS"] = "suppressions=" + os.path.join(HERE, "native", "lsan.supp")
+    r = subprocess.run([EXE], env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-4000:]
+    assert "ERROR: AddressSanitizer" not in out and "ERROR: LeakSanitizer" not in out, out[-4000:]
+    assert "asan driver: ok (0 failed checks)" in out, out[-4000:]
