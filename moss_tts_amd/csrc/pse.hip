@@ -115,6 +115,21 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
+// slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles of CU c
+__device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, int c, int s) {
+  const int l = s / SPL, r = s - l * SPL;
+  if (r < 12) {  // q|k|v: unit 3c + r / 4 = (row tile, K half), 4 slots each
+    const int u = 3 * c + r / 4, t = u >> 1, half = u & 1;
+    return wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
+  } else if (r < 20) {  // o_proj row tile c, 8 slots
+    return wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
+  } else if (r < 68) {  // gate|up pairs 3c .. 3c+2: gate tile (8 slots), then up tile (8)
+    const int q = r - 20, pr = 3 * c + q / 16, rt = 2 * pr + (q % 16) / 8;
+    return wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
+  }
+  return wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;  // down row tile c, 24 slots
+}
+
 // LDS words shared by the loader and the consumers
 struct Ctl {
   int full[LW];   // per loader wave k: its slots (k, k + LW, ...) whose DMA has retired
@@ -156,6 +171,9 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 #ifndef PSE_AU
 #define PSE_AU 2
 #endif
+#ifndef PSE_HSPLIT
+#define PSE_HSPLIT 1  // attention units split a KV head's q heads (1) or its keys (0)
+#endif
 __host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
   return (d >= 0 && d % 7 == 0 && d / 7 < HKV_ * PSE_AU) ? d / 7 : -1;
@@ -169,7 +187,9 @@ extern __shared__ __attribute__((aligned(16))) unsigned char pse_lds[];
 #define PSE_CTL (reinterpret_cast<Ctl*>(pse_lds + L_CTL))
 
 struct Ctx {
-  const PseArgs& a;
+  uint32_t* err;  // the launch's error word
+  float eps;
+  int probe;
   int c, lane, wave, tid;
   uint32_t epoch;
   int bar_gen;
@@ -179,7 +199,7 @@ __device__ __forceinline__ bool failed(const Ctx& x) {
   return __hip_atomic_load(&PSE_CTL->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != 0;
 }
 __device__ __forceinline__ void give_up(Ctx& x, uint32_t code) {
-  st32(x.a.err, code);
+  st32(x.err, code);
   __hip_atomic_store(&PSE_CTL->abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
@@ -238,7 +258,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
         pend &= ~(1u << i);
       }
     if (!__any(pend != 0)) break;
-    if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.a.err)))) {
+    if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
       ok = false;
       break;
@@ -270,7 +290,7 @@ __device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, const 
   float s = 0.f;
   if (4 * x.lane < n_ss) s = (ss[4 * x.lane] + ss[4 * x.lane + 1]) + (ss[4 * x.lane + 2] + ss[4 * x.lane + 3]);
   s = wave_sum(s);
-  const float r = 1.0f / sqrtf(s / (float)K + x.a.eps);
+  const float r = 1.0f / sqrtf(s / (float)K + x.eps);
   u32x4* xv = reinterpret_cast<u32x4*>(xs);
   const u32x4* wv = reinterpret_cast<const u32x4*>(w);
   for (int i = x.tid; i < K / 8; i += CW * 64) {
@@ -300,7 +320,7 @@ __device__ __forceinline__ void consume_slot(Ctx& x, int seq, int kt0, f32x4& ac
     __builtin_amdgcn_s_sleep(PSE_CSLEEP);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-  if (x.a.probe == 2) {
+  if (x.probe == 2) {
     if (x.lane == 0) __hip_atomic_store(&PSE_CTL->freed[x.wave - LW], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     return;
   }
@@ -347,12 +367,49 @@ __device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
 // over 32-key chunks, the CW partials merged in a fixed order -> G x D outputs as granules.
 // graw: the gathered q|k|v K-half partials, [tile][half][16] fp32 (q tiles, k tiles, v tiles).
 // (false on a failed wait)
-__device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) {
+// Not inlined: the attention's chunk state (K / V^T fragments, online-softmax accumulators) is
+// ~200 VGPRs; inlined, it pushed the whole kernel past the 256-VGPR budget of 2 waves per SIMD
+// and spilled registers live across every other phase (scratch reloads on the hand-off paths of
+// all 256 CUs).  As a call, only the 16 attention CUs save / restore around it.  Every argument is
+// a plain value (no pointer into the kernel's arguments or private memory).  Returns the
+// consumer barrier count, -1 on a failed wait.
+#ifndef PSE_ATT_NOINLINE
+#define PSE_ATT_NOINLINE 1
+#endif
+#if PSE_ATT_NOINLINE
+#define PSE_ATT_INL __attribute__((noinline))
+#else
+#define PSE_ATT_INL __forceinline__
+#endif
+__device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask,
+                                                   const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
+                                                   uint64_t* g_att, uint64_t* g_attp, uint32_t* err, uint64_t* trace,
+                                                   float eps, float scale, int Cmax_, uint32_t epoch, int bar_gen,
+                                                   int l, int unit, uint32_t tq) {
+  const int c = blockIdx.x;
+  Ctx x{err, eps, 0, c, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64, epoch, bar_gen};
+  struct {
+    const int* pos;
+    const uint8_t* mask;
+    const bf16_t *cos_t, *sin_t;
+    uint64_t *g_att, *g_attp, *trace;
+    float eps, scale;
+    int Cmax;
+  } a{pos_p, mask, cos_t, sin_t, g_att, g_attp, trace, eps, scale, Cmax_};
   const int g = unit / PSE_AU, ku = unit % PSE_AU;
+#if PSE_HSPLIT
+  // unit ku of KV head g: q heads h0 .. h0 + HU - 1 of the group over EVERY key (no cross-unit
+  // merge); the key-split form (PSE_HSPLIT=0) gives each unit every head over 1 / PSE_AU of the
+  // keys and merges unit partials into unit 0
+  constexpr int HU = G_ / PSE_AU;
+  const int h0 = ku * HU;
+#else
+  constexpr int HU = G_;
+  const int h0 = 0;
+#endif
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16;
-  const PseArgs& a = x.a;
-  const PseLayer& Lw = a.L[l];
+  const PseLayer& Lw = *Lp;
   const int pos = *a.pos;
   const int lane = x.lane, w = x.wave - LW, g4 = lane >> 4, c16 = lane & 15;
   const int Cmax = a.Cmax;
@@ -392,11 +449,17 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
   };
   u32x4 ktA[2][QS], vtA[DT];
   uint32_t mkA[2];
+#if PSE_HSPLIT
+  // this wave's chunks: w, then every CW
+  const int ch0 = w;
+  constexpr int CSTEP = CW;
+#else
   // this wave's chunks: ku CW + w, then every PSE_AU CW
   const int ch0 = ku * CW + w;
   constexpr int CSTEP = PSE_AU * CW;
+#endif
   // this wave's jobs' norm weights and the RoPE row at pos (2 dims per lane)
-  constexpr int JW = (G + 2 + CW - 1) / CW;  // jobs per wave
+  constexpr int JW = (HU + 2 + CW - 1) / CW;  // jobs per wave
   uint32_t pnw[JW], pcs = 0, psn = 0;
   // the first chunk and the prologue's inputs go out right behind the q|k|v gather's first
   // sweep (the cached keys do not depend on it)
@@ -406,16 +469,15 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
 #pragma unroll
     for (int jj = 0; jj < JW; ++jj) {
       const int j = w + jj * CW;
-      pnw[jj] = j <= G ? reinterpret_cast<const uint32_t*>(j < G ? Lw.q_norm : Lw.k_norm)[lane] : 0u;
+      pnw[jj] = j <= HU ? reinterpret_cast<const uint32_t*>(j < HU ? Lw.q_norm : Lw.k_norm)[lane] : 0u;
     }
     pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
     psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
   };
   if (PSE_APAUSE && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (!gather<NG / (CW * 64)>(x, x.a.g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
+  if (!gather<NG / (CW * 64)>(x, g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
                               nullptr, prefetch))
-    return false;
-  const int c = x.c;
+    return -1;
   if (w == 0) PSE_STAMP(l, 15);
   // q|k|v row value: sum of the two K-half partials, rounded to bf16 (the projection output)
   auto val = [&](int base_tile, int i) {
@@ -423,15 +485,16 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
     return rbf(p[0] + p[16]);
   };
   for (int i = x.tid; i < 16 * D; i += CW * 64)
-    if (i / D >= G) q_s[i] = 0;
-  // jobs: j < G q head j, G: k, G + 1: v; wave w takes jobs w, w + CW; a lane holds 2 dims
+    if (i / D >= HU) q_s[i] = 0;
+  // jobs: j < HU q head h0 + j (q_s row j), HU: k, HU + 1: v; wave w takes jobs w, w + CW; a
+  // lane holds 2 dims
 #pragma unroll
   for (int jj = 0; jj < JW; ++jj) {
     const int j = w + jj * CW;
-    if (j >= G + 2) continue;
-    const int bt = j < G ? j * (D / 16) : (j == G ? G * (D / 16) : (G + 1) * (D / 16));
+    if (j >= HU + 2) continue;
+    const int bt = j < HU ? (h0 + j) * (D / 16) : (j == HU ? G * (D / 16) : (G + 1) * (D / 16));
     const float x0 = val(bt, 2 * lane), x1 = val(bt, 2 * lane + 1);
-    if (j == G + 1) {
+    if (j == HU + 1) {
       v_s[2 * lane] = x0;
       v_s[2 * lane + 1] = x1;
       if (ku == 0) {  // one unit appends the new token to the cache
@@ -452,7 +515,7 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
     const float c0 = __uint_as_float(pcs << 16), c1 = __uint_as_float(pcs & 0xffff0000u);
     const float s0 = __uint_as_float(psn << 16), s1 = __uint_as_float(psn & 0xffff0000u);
     const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)), o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
-    if (j < G) {
+    if (j < HU) {
       q_s[j * D + 2 * lane] = f2bf(o0);
       q_s[j * D + 2 * lane + 1] = f2bf(o1);
     } else {
@@ -564,18 +627,42 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
     compute(ch, ktA, vtA, mkA);
   }
   if (w == 0) PSE_STAMP(l, 17);
-  if (lane < G) {
-    ml_s[(w * G + lane) * 2] = m_run;
-    ml_s[(w * G + lane) * 2 + 1] = l_run;
+  if (lane < HU) {
+    ml_s[(w * HU + lane) * 2] = m_run;
+    ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int h = g4 * 4 + r;
-      if (h < G) acc_s[(w * G + h) * D + dt * 16 + c16] = o_run[dt][r];
+      if (h < HU) acc_s[(w * HU + h) * D + dt * 16 + c16] = o_run[dt][r];
     }
   cbar(x);
+#if PSE_HSPLIT
+  {
+    // merge the CW wave partials of this unit's heads in a fixed order (thread e / 2: 2 output
+    // dims of local head h), then publish them: they are final
+    const int e = 2 * x.tid, h = e / D, d = e % D;
+    if (e < HU * D) {
+      float M = -INFINITY;
+#pragma unroll
+      for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
+      float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < CW; ++ww) {
+        const float mw = ml_s[(ww * HU + h) * 2];
+        const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
+        L += f * ml_s[(ww * HU + h) * 2 + 1];
+        o0 += f * acc_s[(ww * HU + h) * D + d];
+        o1 += f * acc_s[(ww * HU + h) * D + d + 1];
+      }
+      st64(a.g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+    }
+    cbar(x);
+    return x.bar_gen;
+  }
+#endif
   // merge the CW wave partials in a fixed order: thread e2 holds 2 output dims of head h,
   // unnormalised (M, L, O) of this unit
   const int e = 2 * x.tid, h = e / D, d = e % D;  // G * D / 2 == CW * 64 threads
@@ -606,14 +693,14 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
       st64(pp + G * D + G + h, gran(__float_as_uint(L), tp));
     }
     cbar(x);
-    return true;
+    return x.bar_gen;
   }
   // unit 0: the other units' partials (contiguous), merged in unit order -> the output granules
   float* pg = reinterpret_cast<float*>(pse_lds + L_GRAW);  // (q|k|v partials and q_s are dead)
   if (!gather<((PSE_AU - 1) * PW + CW * 64 - 1) / (CW * 64)>(x, a.g_attp + (size_t)(unit + 1) * PW, (PSE_AU - 1) * PW,
                                                             tagof(x.epoch, l, OP_ATT) | 0x80000000u,
                                                             reinterpret_cast<uint32_t*>(pg), (PSE_AU - 1) * PW))
-    return false;
+    return -1;
   if (w == 0) PSE_STAMP(l, 18);
   float MM = M;
 #pragma unroll
@@ -631,7 +718,7 @@ __device__ __forceinline__ bool attention(Ctx& x, int l, int unit, uint32_t tq) 
   st64(a.g_att + (g * G * D + e) / 2, gran(LL > 0.f ? pack2(O0 / LL, O1 / LL) : 0u, tagof(x.epoch, l, OP_ATT)));
   }
   cbar(x);
-  return true;
+  return x.bar_gen;
 }
 
 }  // namespace
@@ -662,20 +749,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     // published in full[k]
     const int k = wave;
     int marked = 0, m = 0;
-    // slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles
-    auto slot_src = [&](int s) -> const bf16_t* {
-      const int l = s / SPL, r = s - l * SPL;
-      if (r < 12) {  // q|k|v: unit 3c + r / 4 = (row tile, K half), 4 slots each
-        const int u = 3 * c + r / 4, t = u >> 1, half = u & 1;
-        return wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
-      } else if (r < 20) {  // o_proj row tile c, 8 slots
-        return wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
-      } else if (r < 68) {  // gate|up pairs 3c .. 3c+2: gate tile (8 slots), then up tile (8)
-        const int q = r - 20, pr = 3 * c + q / 16, rt = 2 * pr + (q % 16) / 8;
-        return wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
-      }
-      return wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;  // down row tile c, 24 slots
-    };
+    auto slot_src = [&](int s) { return pse_slot_src(wp, c, s); };
     for (int s = k; s < total; s += LW, ++m) {
       // ring slot s % NS is free once every consumer wave has read slot s - NS
       if (s >= NS) {
@@ -734,7 +808,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     __hip_atomic_store(&ctl->full[k], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   } else {
     // =================== consumers ===================
-    Ctx x{a, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
+    Ctx x{a.err, a.eps, a.probe, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
     if (PSE_GPRIO == 2) __builtin_amdgcn_s_setprio(2);  // (A/B: consumers ahead of the loader always)
     uint32_t* xs32 = reinterpret_cast<uint32_t*>(lds + L_XS);
     bf16_t* xs = reinterpret_cast<bf16_t*>(lds + L_XS);
@@ -796,7 +870,10 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       // ---------------- attention (one CU per KV head) ----------------
       if (att_u >= 0) {
         // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
-        const bool att_ok = attention(x, l, att_u, tq);
+        const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.g_attp, a.err, a.trace,
+                                 a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
+        const bool att_ok = bg >= 0;
+        if (att_ok) x.bar_gen = bg;
         if (PSE_APAUSE == 2 && x.tid == 0)  // (PSE_APAUSE 2: the loader waits out the whole attention)
           __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (!att_ok) break;
