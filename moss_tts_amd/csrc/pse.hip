@@ -171,6 +171,9 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 #ifndef PSE_AU
 #define PSE_AU 2
 #endif
+#ifndef PSE_RLOAD
+#define PSE_RLOAD 1  // register-staged loader (1) or LDS-DMA fills (0)
+#endif
 #ifndef PSE_HSPLIT
 #define PSE_HSPLIT 1  // attention units split a KV head's q heads (1) or its keys (0)
 #endif
@@ -750,6 +753,141 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     const int k = wave;
     int marked = 0, m = 0;
     auto slot_src = [&](int s) { return pse_slot_src(wp, c, s); };
+#if PSE_RLOAD
+    // Register-staged loader: each slot is loaded into one of 3 register buffers (16 x 16 B per
+    // lane) and copied into its ring slot once that slot is free, so the 3 slots in flight do not
+    // occupy ring slots (8 ready + 3 in flight, against 8 including the in-flight fills of the
+    // LDS-DMA loader).  The copy + reload of a buffer is ONE asm block with the buffer as "+v"
+    // operands: the compiler's own waitcnt insertion waits for every load in flight before any
+    // use of a loop-carried load result (measured: vmcnt(0) at each copy), so the count is
+    // explicit here -- vmcnt(32) = this buffer's loads, the two younger buffers' 32 still in
+    // flight.  Every copy / reload issues exactly 16 loads (a slot past the end re-reads the last
+    // slot), which keeps that count exact; loads are only ever addressed inside the weights (a
+    // prefetch past the last slot would index the pointer table past its last layer).
+    (void)m;
+    (void)marked;
+    u32x4 bA[SLOT_KB], bB[SLOT_KB], bC[SLOT_KB];
+    bool dead = false;
+    const uint32_t voff = (uint32_t)lane * 16u;
+    const uint32_t ring0 = (uint32_t)(uintptr_t)(lvoid*)(lds + L_RING) + voff;
+    auto src_of = [&](int s0) -> const void* {
+      const int s = min(s0, total - 1);
+      const int l = s / SPL, r = s - l * SPL;
+      if (a.trace && lane == 0 && s0 < total) {
+        const int ev = r == 0 ? 0 : (r == 12 ? 1 : (r == 20 ? 2 : (r == 68 ? 3 : (r == SPL - 1 ? 4 : -1))));
+        if (ev >= 0) ctl->lstamp[l & 1][ev] = __builtin_amdgcn_s_memrealtime();
+      }
+      if (PSE_APAUSE && s0 < total)  // this CU's attention is gathering its inputs: no new loads
+        for (uint32_t spins = 0; __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                                 !__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
+                                 spins < SPIN_LDS;
+             ++spins)
+          __builtin_amdgcn_s_sleep(1);
+      const uint64_t p = (uint64_t)(uintptr_t)slot_src(s);  // wave-uniform: into SGPRs
+      const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
+      return (const void*)(((uint64_t)hi << 32) | lo);
+    };
+#define PSE_RL_OPS                                                                                  \
+  [b0] "+v"(b[0]), [b1] "+v"(b[1]), [b2] "+v"(b[2]), [b3] "+v"(b[3]), [b4] "+v"(b[4]), [b5] "+v"(b[5]), \
+      [b6] "+v"(b[6]), [b7] "+v"(b[7]), [b8] "+v"(b[8]), [b9] "+v"(b[9]), [b10] "+v"(b[10]),          \
+      [b11] "+v"(b[11]), [b12] "+v"(b[12]), [b13] "+v"(b[13]), [b14] "+v"(b[14]), [b15] "+v"(b[15])
+// (s_nop 4 first: %[g] comes fresh from v_readfirstlane, and a VMEM instruction reading an SGPR
+// a VALU just wrote needs 5 wait states, which hipcc does not insert inside an asm string --
+// without them the loads take the SGPRs' previous contents as their base: the illegal-address
+// fault of the round-2 register loader)
+#define PSE_RL_LOADS                                                                                \
+  "s_nop 4\n\t"                                                                                    \
+  "global_load_dwordx4 %[b0], %[o0], %[g] offset:0 nt\n\t"                                        \
+  "global_load_dwordx4 %[b1], %[o0], %[g] offset:1024 nt\n\t"                                     \
+  "global_load_dwordx4 %[b2], %[o0], %[g] offset:2048 nt\n\t"                                     \
+  "global_load_dwordx4 %[b3], %[o0], %[g] offset:3072 nt\n\t"                                     \
+  "global_load_dwordx4 %[b4], %[o1], %[g] offset:0 nt\n\t"                                        \
+  "global_load_dwordx4 %[b5], %[o1], %[g] offset:1024 nt\n\t"                                     \
+  "global_load_dwordx4 %[b6], %[o1], %[g] offset:2048 nt\n\t"                                     \
+  "global_load_dwordx4 %[b7], %[o1], %[g] offset:3072 nt\n\t"                                     \
+  "global_load_dwordx4 %[b8], %[o2], %[g] offset:0 nt\n\t"                                        \
+  "global_load_dwordx4 %[b9], %[o2], %[g] offset:1024 nt\n\t"                                     \
+  "global_load_dwordx4 %[b10], %[o2], %[g] offset:2048 nt\n\t"                                    \
+  "global_load_dwordx4 %[b11], %[o2], %[g] offset:3072 nt\n\t"                                    \
+  "global_load_dwordx4 %[b12], %[o3], %[g] offset:0 nt\n\t"                                       \
+  "global_load_dwordx4 %[b13], %[o3], %[g] offset:1024 nt\n\t"                                    \
+  "global_load_dwordx4 %[b14], %[o3], %[g] offset:2048 nt\n\t"                                    \
+  "global_load_dwordx4 %[b15], %[o3], %[g] offset:3072 nt\n\t"
+    auto load = [&](u32x4 (&b)[SLOT_KB], int s_issue) {
+      const void* g = src_of(s_issue);
+      asm volatile(PSE_RL_LOADS
+                   : PSE_RL_OPS
+                   : [g] "s"(g), [o0] "v"(voff), [o1] "v"(voff + 4096u), [o2] "v"(voff + 8192u), [o3] "v"(voff + 12288u)
+                   : "memory");
+    };
+    // copy buffer b (slot s, loaded two buffers ago) into its ring slot, then reload b with slot s_issue
+    auto copy_load = [&](u32x4 (&b)[SLOT_KB], int s, int s_issue) {
+      if (s >= NS && !dead)
+        for (uint32_t spins = 0;; ++spins) {  // ring slot s % NS is free once every consumer read slot s - NS
+          int mn = 1 << 30;
+#pragma unroll
+          for (int w = 0; w < CW; ++w)
+            mn = min(mn, __hip_atomic_load(&ctl->freed[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+          if (mn >= s - NS + 1) break;
+          if (spins > SPIN_LDS || __hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+            dead = true;  // (the error word is written after the loop: no global store in between)
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      const void* g = src_of(s_issue);
+      const uint32_t dst = ring0 + (uint32_t)(s % NS) * (SLOT_KB * 1024u);
+      asm volatile("s_waitcnt vmcnt(32)\n\t"
+                   "ds_write_b128 %[d], %[b0] offset:0\n\t"
+                   "ds_write_b128 %[d], %[b1] offset:1024\n\t"
+                   "ds_write_b128 %[d], %[b2] offset:2048\n\t"
+                   "ds_write_b128 %[d], %[b3] offset:3072\n\t"
+                   "ds_write_b128 %[d], %[b4] offset:4096\n\t"
+                   "ds_write_b128 %[d], %[b5] offset:5120\n\t"
+                   "ds_write_b128 %[d], %[b6] offset:6144\n\t"
+                   "ds_write_b128 %[d], %[b7] offset:7168\n\t"
+                   "ds_write_b128 %[d], %[b8] offset:8192\n\t"
+                   "ds_write_b128 %[d], %[b9] offset:9216\n\t"
+                   "ds_write_b128 %[d], %[b10] offset:10240\n\t"
+                   "ds_write_b128 %[d], %[b11] offset:11264\n\t"
+                   "ds_write_b128 %[d], %[b12] offset:12288\n\t"
+                   "ds_write_b128 %[d], %[b13] offset:13312\n\t"
+                   "ds_write_b128 %[d], %[b14] offset:14336\n\t"
+                   "ds_write_b128 %[d], %[b15] offset:15360\n\t"
+                   "s_waitcnt lgkmcnt(0)\n\t" PSE_RL_LOADS
+                   : PSE_RL_OPS
+                   : [d] "v"(dst), [g] "s"(g), [o0] "v"(voff), [o1] "v"(voff + 4096u), [o2] "v"(voff + 8192u),
+                     [o3] "v"(voff + 12288u)
+                   : "memory");
+      if (!dead && s < total) __hip_atomic_store(&ctl->full[0], s + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    load(bA, 0);
+    load(bB, 1);
+    load(bC, 2);
+    for (int s = 0; s < total && !dead; s += 3) {
+      copy_load(bA, s, s + 3);
+      if (s + 1 >= total) break;
+      copy_load(bB, s + 1, s + 4);
+      if (s + 2 >= total) break;
+      copy_load(bC, s + 2, s + 5);
+    }
+    {  // every load in flight lands before the buffers' registers can be reused
+      u32x4(&b)[SLOT_KB] = bA;
+      asm volatile("s_waitcnt vmcnt(0)" : PSE_RL_OPS::"memory");
+    }
+    {
+      u32x4(&b)[SLOT_KB] = bB;
+      asm volatile("" : PSE_RL_OPS::"memory");
+    }
+    {
+      u32x4(&b)[SLOT_KB] = bC;
+      asm volatile("" : PSE_RL_OPS::"memory");
+    }
+#undef PSE_RL_OPS
+#undef PSE_RL_LOADS
+    if (dead) st32(a.err, 1u);
+    __hip_atomic_store(&ctl->full[0], dead ? 0 : total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
     for (int s = k; s < total; s += LW, ++m) {
       // ring slot s % NS is free once every consumer wave has read slot s - NS
       if (s >= NS) {
@@ -806,6 +944,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __hip_atomic_store(&ctl->full[k], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#endif
   } else {
     // =================== consumers ===================
     Ctx x{a.err, a.eps, a.probe, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
