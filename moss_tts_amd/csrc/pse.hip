@@ -115,6 +115,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
+#ifndef PSE_ACTPIPE
+#define PSE_ACTPIPE 1
+#endif
+// gate|up pair of CU c in round j (3 pairs per CU).  PSE_ACTPIPE: round j of every CU makes
+// the SwiGLU columns [4096 j, 4096 j + 4096), i.e. down_proj's k range of its slots 8j .. 8j+7,
+// so rounds 0 and 1 are published long before the down stream needs them and only round 2's
+// hand-off remains, hidden behind down's first 16 slots (the consumers below); otherwise
+// pairs 3c .. 3c+2.
+__device__ __forceinline__ int pse_gu_pair(int c, int j) { return PSE_ACTPIPE ? c + 256 * j : 3 * c + j; }
 // slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles of CU c
 __device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, int c, int s) {
   const int l = s / SPL, r = s - l * SPL;
@@ -123,8 +132,8 @@ __device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, i
     return wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
   } else if (r < 20) {  // o_proj row tile c, 8 slots
     return wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
-  } else if (r < 68) {  // gate|up pairs 3c .. 3c+2: gate tile (8 slots), then up tile (8)
-    const int q = r - 20, pr = 3 * c + q / 16, rt = 2 * pr + (q % 16) / 8;
+  } else if (r < 68) {  // gate|up pairs (round j = 0..2: pair pse_gu_pair(c, j)): gate tile (8 slots), then up tile (8)
+    const int q = r - 20, pr = pse_gu_pair(c, q / 16), rt = 2 * pr + (q % 16) / 8;
     return wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
   }
   return wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;  // down row tile c, 24 slots
@@ -1055,19 +1064,38 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
           const float gg = rbf(red_get(x, 0, lane & 15)), uu = rbf(red_get(x, 1, lane & 15));
           const float o = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
           const float on = __shfl_down(o, 1, 64);
-          if (lane < 16 && (lane & 1) == 0) st64(a.g_act + (3 * c + j) * 8 + lane / 2, gran(pack2(o, on), tg));
+          if (lane < 16 && (lane & 1) == 0) st64(a.g_act + pse_gu_pair(c, j) * 8 + lane / 2, gran(pack2(o, on), tg));
         }
         cbar(x);
         PSE_PRIO_DOWN();
       }
       if (wave == LW) PSE_STAMP(l, 7);
       // ---------------- down (+ residual) ----------------
+#if PSE_ACTPIPE
+      // rounds 0 and 1 (columns 0 .. 8191, published one and two gate|up rounds ago): one sweep
+      if (!gather<16>(x, a.g_act, I_ / 3, tg, xs32, I_ / 3)) break;
+      if (wave == LW) PSE_STAMP(l, 8);
+      {
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        // round 2's sweep goes out first; its 16 k-slots of rounds 0 and 1 are consumed while it
+        // flies (at normal priority: the raised one would starve the loader), then the rest
+        auto first16 = [&]() {
+          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+          #pragma unroll 1
+          for (int k = 0; k < 16; ++k) consume_slot(x, seq++, k * 16, acc);
+          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
+        };
+        if (!gather<8>(x, a.g_act + I_ / 3, I_ / 6, tg, xs32 + I_ / 3, I_ / 6, nullptr, first16)) break;
+        #pragma unroll 1
+        for (int k = 16; k < 24; ++k) consume_slot(x, seq++, k * 16, acc);
+#else
       if (!gather<24>(x, a.g_act, I_ / 2, tg, xs32, I_ / 2)) break;
       if (wave == LW) PSE_STAMP(l, 8);
       {
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         #pragma unroll 1
         for (int k = 0; k < 24; ++k) consume_slot(x, seq++, k * 16, acc);
+#endif
         PSE_PRIO_UP();
         red_put(x, 0, acc);
         cbar(x);

@@ -99,4 +99,15 @@ print("|---|---|")
 for name, v in rows:
     print(f"| {name} | {v:.2f} |")
 print(f"| layer period | {float(np.median(lay)):.2f} |")
+# stragglers: per CU, how far behind the median each op's completion runs (steady-state layers),
+# attention CUs (pse_att_unit: 255 - c = 7 u, u < 16) marked
+att = set(255 - 7 * u for u in range(16))
+for name, ev in (("o done", 5), ("gu done", 7), ("down done", 9)):
+    lag = np.stack([tr[l, ev] - np.median(tr[l, ev]) for l in range(1, layers)]) / 100  # [layer, CU] us
+    mean_lag = lag.mean(0)
+    worst = np.argsort(-mean_lag)[:12]
+    print(f"{name}: mean lag behind the median, worst CUs: " +
+          ", ".join(f"{c}{'*' if c in att else ''}:{mean_lag[c]:.1f}" for c in worst) +
+          f" | attention CUs mean {np.mean([mean_lag[c] for c in att]):.2f}, others {np.mean([mean_lag[c] for c in range(256) if c not in att]):.2f}"
+          + f" | by XCD (c % 8): " + " ".join(f"{x}:{np.mean(mean_lag[x::8]):.2f}" for x in range(8)))
 e.close()
