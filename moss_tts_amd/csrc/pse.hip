@@ -116,7 +116,7 @@ __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { retur
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
 #ifndef PSE_ACTPIPE
-#define PSE_ACTPIPE 1
+#define PSE_ACTPIPE 2  // 2: every act round's hand-off hidden (below); 1: round 2's; 0: none
 #endif
 // gate|up pair of CU c in round j (3 pairs per CU).  PSE_ACTPIPE: round j of every CU makes
 // the SwiGLU columns [4096 j, 4096 j + 4096), i.e. down_proj's k range of its slots 8j .. 8j+7,
@@ -1048,8 +1048,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       norm_stage(x, xs, ssl, NT, Lw.post_norm, H_);
       if (wave == LW) PSE_STAMP(l, 6);
       const uint32_t tg = tagof(epoch, l, OP_GU);
-      #pragma unroll 1
-      for (int j = 0; j < 3; ++j) {
+      auto gu_round = [&](int j) {
         f32x4 ag = (f32x4){0.f, 0.f, 0.f, 0.f}, au = ag;
         #pragma unroll 1
         for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, ag);
@@ -1068,10 +1067,42 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         }
         cbar(x);
         PSE_PRIO_DOWN();
-      }
+      };
+#if PSE_ACTPIPE == 2
+      gu_round(0);
+      gu_round(1);
+      // round 2 runs inside the gather of round 0's columns (published a round ago) -> xs
+      // k-tiles 128 .. 255 (the normed input in k-tiles 0 .. 127 is still being read)
+      auto gu2 = [&]() {
+        if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+        gu_round(2);
+        if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
+      };
+      if (!gather<8>(x, a.g_act, I_ / 6, tg, xs32 + I_ / 6, I_ / 6, nullptr, gu2)) break;
+#else
+      #pragma unroll 1
+      for (int j = 0; j < 3; ++j) gu_round(j);
+#endif
       if (wave == LW) PSE_STAMP(l, 7);
       // ---------------- down (+ residual) ----------------
-#if PSE_ACTPIPE
+#if PSE_ACTPIPE == 2
+      if (wave == LW) PSE_STAMP(l, 8);
+      {
+        // down's k-slots 8j .. 8j+7 read round j's columns: round 0 in xs k-tiles 128 .. 255,
+        // round 1 gathered into 256 .. 383 while round 0's slots run, round 2 into 0 .. 127 (the
+        // normed input is dead by then) while round 1's slots run
+        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+        auto slots = [&](int k0, int off) {
+          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+          #pragma unroll 1
+          for (int k = k0; k < k0 + 8; ++k) consume_slot(x, seq++, k * 16 + off, acc);
+          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
+        };
+        if (!gather<8>(x, a.g_act + I_ / 6, I_ / 6, tg, xs32 + I_ / 3, I_ / 6, nullptr, [&]() { slots(0, 128); })) break;
+        if (!gather<8>(x, a.g_act + I_ / 3, I_ / 6, tg, xs32, I_ / 6, nullptr, [&]() { slots(8, 128); })) break;
+        #pragma unroll 1
+        for (int k = 16; k < 24; ++k) consume_slot(x, seq++, k * 16 - 256, acc);
+#elif PSE_ACTPIPE
       // rounds 0 and 1 (columns 0 .. 8191, published one and two gate|up rounds ago): one sweep
       if (!gather<16>(x, a.g_act, I_ / 3, tg, xs32, I_ / 3)) break;
       if (wave == LW) PSE_STAMP(l, 8);
