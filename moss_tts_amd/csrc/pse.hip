@@ -115,9 +115,26 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
+#ifndef PSE_QFIRST
+#define PSE_QFIRST 1  // q|k|v: q tiles first on every CU; the attention runs its cached-key chunks before k / v arrive
+#endif
 #ifndef PSE_ACTPIPE
 #define PSE_ACTPIPE 2  // 2: every act round's hand-off hidden (below); 1: round 2's; 0: none
 #endif
+// q|k|v unit j (0..2) of CU c: (row tile, K half).  PSE_QFIRST: both halves of q row tile c,
+// then half c & 1 of k|v row tile 256 + c / 2 -- every q tile is complete two thirds into the
+// q|k|v stream, so the attention units start on q while k / v are still being produced;
+// otherwise units 3c .. 3c+2 in (tile, half) order.
+__device__ __forceinline__ void pse_qkv_unit(int c, int j, int* t, int* half) {
+  if (PSE_QFIRST) {
+    *t = j < 2 ? c : HQ_ * D_ / 16 + (c >> 1);
+    *half = j < 2 ? j : (c & 1);
+  } else {
+    const int u = 3 * c + j;
+    *t = u >> 1;
+    *half = u & 1;
+  }
+}
 // gate|up pair of CU c in round j (3 pairs per CU).  PSE_ACTPIPE: round j of every CU makes
 // the SwiGLU columns [4096 j, 4096 j + 4096), i.e. down_proj's k range of its slots 8j .. 8j+7,
 // so rounds 0 and 1 are published long before the down stream needs them and only round 2's
@@ -127,8 +144,9 @@ __device__ __forceinline__ int pse_gu_pair(int c, int j) { return PSE_ACTPIPE ? 
 // slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles of CU c
 __device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, int c, int s) {
   const int l = s / SPL, r = s - l * SPL;
-  if (r < 12) {  // q|k|v: unit 3c + r / 4 = (row tile, K half), 4 slots each
-    const int u = 3 * c + r / 4, t = u >> 1, half = u & 1;
+  if (r < 12) {  // q|k|v: unit r / 4 of CU c = (row tile, K half), 4 slots each
+    int t, half;
+    pse_qkv_unit(c, r / 4, &t, &half);
     return wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
   } else if (r < 20) {  // o_proj row tile c, 8 slots
     return wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
@@ -251,8 +269,8 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   // behind the sweep instead of delaying it, and the sweep's results are waited for alone)
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);  // sweeps issue ahead of the loader's fills
   bool ok = true;
-  for (uint32_t spins = 0;; ++spins) {
-    uint32_t lo[MAXP], hi[MAXP];
+  uint32_t lo[MAXP], hi[MAXP];
+  auto issue = [&]() {
 #pragma unroll
     for (int i = 0; i < MAXP; ++i) {
       const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (pend >> i & 1u) ? (uint32_t)(x.tid + i * CW * 64) * 8u : OOB,
@@ -260,7 +278,8 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
       lo[i] = v[0];
       hi[i] = v[1];
     }
-    if (spins == 0) after_first_issue();
+  };
+  auto take = [&]() {
 #pragma unroll
     for (int i = 0; i < MAXP; ++i)
       if ((pend >> i & 1u) && hi[i] == t) {
@@ -269,13 +288,21 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
         else dst1[j - n0] = lo[i];
         pend &= ~(1u << i);
       }
-    if (!__any(pend != 0)) break;
+  };
+  // the first sweep and the caller's work outside the poll loop (a hook inside it would share
+  // the loop's register allocation: the attention's chunk loop spilled there)
+  issue();
+  after_first_issue();
+  take();
+  for (uint32_t spins = 1; __any(pend != 0); ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
       ok = false;
       break;
     }
     __builtin_amdgcn_s_sleep(PSE_POLL_SLEEP);
+    issue();
+    take();
   }
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(PSE_GPRIO == 2 ? 2 : 0);
   cbar(x);
@@ -472,7 +499,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
 #endif
   // this wave's jobs' norm weights and the RoPE row at pos (2 dims per lane)
   constexpr int JW = (HU + 2 + CW - 1) / CW;  // jobs per wave
-  uint32_t pnw[JW], pcs = 0, psn = 0;
+  uint32_t pnw[JW], pcs = 0, psn = 0, knw = 0, mnew = 0;
   // the first chunk and the prologue's inputs go out right behind the q|k|v gather's first
   // sweep (the cached keys do not depend on it)
   constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the head's q|k|v granules
@@ -485,17 +512,59 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     }
     pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
     psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
+    if (PSE_QFIRST) {
+      knw = reinterpret_cast<const uint32_t*>(Lw.k_norm)[lane];
+      mnew = a.mask[pos];
+    }
   };
   if (PSE_APAUSE && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (!gather<NG / (CW * 64)>(x, g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
-                              nullptr, prefetch))
-    return -1;
-  if (w == 0) PSE_STAMP(l, 15);
   // q|k|v row value: sum of the two K-half partials, rounded to bf16 (the projection output)
   auto val = [&](int base_tile, int i) {
     const float* p = graw + (base_tile + i / 16) * 32 + i % 16;
     return rbf(p[0] + p[16]);
   };
+  // q / k RMSNorm + RoPE of one row (TF/.../modeling_qwen3.py:252-254, :148-170): 2 dims per lane
+  auto norm_rope = [&](float x0, float x1, uint32_t nw, float& o0, float& o1) {
+    const float ss = wave_sum(x0 * x0 + x1 * x1);
+    const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
+    const float n0 = rbf(__uint_as_float(nw << 16) * rbf(x0 * r)), n1 = rbf(__uint_as_float(nw & 0xffff0000u) * rbf(x1 * r));
+    constexpr int q4 = D / 4;
+    const bool lo = 2 * lane < D / 2;
+    const int partner = lo ? lane + q4 : lane - q4;
+    const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
+    const float sg = lo ? -1.f : 1.f;
+    const float c0 = __uint_as_float(pcs << 16), c1 = __uint_as_float(pcs & 0xffff0000u);
+    const float s0 = __uint_as_float(psn << 16), s1 = __uint_as_float(psn & 0xffff0000u);
+    o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
+    o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+  };
+#if PSE_QFIRST
+  static_assert(PSE_HSPLIT, "q-first attention assumes head-split units");
+  // (1) this unit's q heads only (their tiles are complete two thirds into the q|k|v stream)
+  constexpr int NQ = HU * (D_ / 16) * 32, NKV = 2 * (D_ / 16) * 32;
+  uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
+  if (!gather<(NQ + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + h0 * (D_ / 16) * 32, NQ, tq,
+                                              graw32 + h0 * (D_ / 16) * 32, NQ, nullptr, prefetch))
+    return -1;
+  if (w == 0) PSE_STAMP(l, 15);
+  for (int i = x.tid; i < 16 * D; i += CW * 64)
+    if (i / D >= HU) q_s[i] = 0;
+#pragma unroll
+  for (int jj = 0; jj < JW; ++jj) {
+    const int j = w + jj * CW;
+    if (j >= HU) continue;
+    const int bt = (h0 + j) * (D / 16);
+    float o0, o1;
+    norm_rope(val(bt, 2 * lane), val(bt, 2 * lane + 1), pnw[jj], o0, o1);
+    q_s[j * D + 2 * lane] = f2bf(o0);
+    q_s[j * D + 2 * lane + 1] = f2bf(o1);
+  }
+  cbar(x);
+#else
+  if (!gather<NG / (CW * 64)>(x, g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
+                              nullptr, prefetch))
+    return -1;
+  if (w == 0) PSE_STAMP(l, 15);
   for (int i = x.tid; i < 16 * D; i += CW * 64)
     if (i / D >= HU) q_s[i] = 0;
   // jobs: j < HU q head h0 + j (q_s row j), HU: k, HU + 1: v; wave w takes jobs w, w + CW; a
@@ -515,18 +584,8 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
       }
       continue;
     }
-    const float ss = wave_sum(x0 * x0 + x1 * x1);
-    const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
-    const float n0 = rbf(__uint_as_float(pnw[jj] << 16) * rbf(x0 * r)),
-                n1 = rbf(__uint_as_float(pnw[jj] & 0xffff0000u) * rbf(x1 * r));
-    constexpr int q4 = D / 4;
-    const bool lo = 2 * lane < D / 2;
-    const int partner = lo ? lane + q4 : lane - q4;
-    const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
-    const float sg = lo ? -1.f : 1.f;
-    const float c0 = __uint_as_float(pcs << 16), c1 = __uint_as_float(pcs & 0xffff0000u);
-    const float s0 = __uint_as_float(psn << 16), s1 = __uint_as_float(psn & 0xffff0000u);
-    const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)), o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+    float o0, o1;
+    norm_rope(x0, x1, pnw[jj], o0, o1);
     if (j < HU) {
       q_s[j * D + 2 * lane] = f2bf(o0);
       q_s[j * D + 2 * lane + 1] = f2bf(o1);
@@ -537,6 +596,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     }
   }
   cbar(x);
+#endif
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o_run[DT];
 #pragma unroll
@@ -546,7 +606,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     f32x4 sacc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (k0 + t * 16 + c16 == pos) {  // the new key, from LDS
+      if (!PSE_QFIRST && k0 + t * 16 + c16 == pos) {  // the new key, from LDS
 #pragma unroll
         for (int s2 = 0; s2 < QS; ++s2) {
           const int d0 = s2 * 32 + 8 * g4;
@@ -566,7 +626,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int dim = dt * 16 + c16, kb = k0 + 8 * g4;
-      if (kb + 8 > pos && kb <= pos) {  // the new value patched in, keys past pos zero
+      if (!PSE_QFIRST && kb + 8 > pos && kb <= pos) {  // the new value patched in, keys past pos zero
         u32x4 v = vt[dt];
         const uint32_t nv = (uint32_t)f2bf(v_s[dim]);
 #pragma unroll
@@ -585,7 +645,8 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + t * 16 + g4 * 4 + r;
-        const bool valid = key <= pos && ((mk[t] >> (8 * r)) & 0xffu);
+        // (PSE_QFIRST: the new key at pos joins in the final merge instead)
+        const bool valid = (PSE_QFIRST ? key < pos : key <= pos) && ((mk[t] >> (8 * r)) & 0xffu);
         sv[t][r] = valid ? sacc[t][r] * a.scale : -INFINITY;
         mc = fmaxf(mc, sv[t][r]);
       }
@@ -633,12 +694,38 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     };
   if (PSE_APAUSE == 1 && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  if (w == 0) PSE_STAMP(l, 16);
-  for (int ch = ch0; ch < nchunk; ch += CSTEP) {
-    if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
-    compute(ch, ktA, vtA, mkA);
+  auto chunks = [&]() {
+    if (w == 0) PSE_STAMP(l, 16);
+    for (int ch = ch0; ch < nchunk; ch += CSTEP) {
+      if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
+      compute(ch, ktA, vtA, mkA);
+    }
+    if (w == 0) PSE_STAMP(l, 17);
+  };
+#if PSE_QFIRST
+  // (2) the cached keys' chunks run while the new token's k / v partials are gathered
+  if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + G * (D_ / 16) * 32, NKV, tq,
+                                               graw32 + G * (D_ / 16) * 32, NKV, nullptr, chunks))
+    return -1;
+  // (3) k (wave 0: RMSNorm + RoPE) and v (wave 1); unit 0 appends them to the cache
+  if (w == 0) {
+    float o0, o1;
+    norm_rope(val(G * (D / 16), 2 * lane), val(G * (D / 16), 2 * lane + 1), knw, o0, o1);
+    k_s[2 * lane] = o0;
+    k_s[2 * lane + 1] = o1;
+    if (ku == 0) *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
+  } else if (w == 1) {
+    const float x0 = val((G + 1) * (D / 16), 2 * lane), x1 = val((G + 1) * (D / 16), 2 * lane + 1);
+    v_s[2 * lane] = x0;
+    v_s[2 * lane + 1] = x1;
+    if (ku == 0) {
+      vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
+      vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
+    }
   }
-  if (w == 0) PSE_STAMP(l, 17);
+#else
+  chunks();
+#endif
   if (lane < HU) {
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
@@ -656,10 +743,16 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     // merge the CW wave partials of this unit's heads in a fixed order (thread e / 2: 2 output
     // dims of local head h), then publish them: they are final
     const int e = 2 * x.tid, h = e / D, d = e % D;
-    if (e < HU * D) {
+    if (e < HU * D) {  // (D / 2 = 64 threads per head: one whole wave each)
       float M = -INFINITY;
 #pragma unroll
       for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
+#if PSE_QFIRST
+      // the new key at pos: its score q . k (this wave's head), as one more partial with p = 1
+      const float sn = wave_sum(bf2f(q_s[h * D + d]) * k_s[d] + bf2f(q_s[h * D + d + 1]) * k_s[d + 1]) * a.scale;
+      const bool nv = mnew != 0u;
+      if (nv) M = fmaxf(M, sn);
+#endif
       float L = 0.f, o0 = 0.f, o1 = 0.f;
 #pragma unroll
       for (int ww = 0; ww < CW; ++ww) {
@@ -669,6 +762,14 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
         o0 += f * acc_s[(ww * HU + h) * D + d];
         o1 += f * acc_s[(ww * HU + h) * D + d + 1];
       }
+#if PSE_QFIRST
+      if (nv) {
+        const float f = expf(sn - M);
+        L += f;
+        o0 += f * v_s[d];
+        o1 += f * v_s[d + 1];
+      }
+#endif
       st64(a.g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
     }
     cbar(x);
@@ -1002,7 +1103,8 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       const uint32_t tq = tagof(epoch, l, OP_QKV);
       #pragma unroll 1
       for (int j = 0; j < 3; ++j) {
-        const int u = 3 * c + j, half = u & 1;
+        int tile, half;
+        pse_qkv_unit(c, j, &tile, &half);
         f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
         #pragma unroll 1
         for (int k = 0; k < 4; ++k) consume_slot(x, seq++, half * 64 + k * 16, acc);
@@ -1010,7 +1112,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         red_put(x, 0, acc);
         cbar(x);
         if (wave == LW && lane < 16)
-          st64(a.g_qkv + qkv_gran(u >> 1) + (u & 1) * 16 + lane, gran(__float_as_uint(red_get(x, 0, lane)), tq));
+          st64(a.g_qkv + qkv_gran(tile) + half * 16 + lane, gran(__float_as_uint(red_get(x, 0, lane)), tq));
         cbar(x);
         PSE_PRIO_DOWN();
       }
