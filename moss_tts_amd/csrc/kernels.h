@@ -265,7 +265,7 @@ struct PseArgs {
   int Cmax;
   float eps, scale;
   // workspace (set by pse_decode): granules and words
-  uint64_t *g_qkv, *g_att, *g_attp, *g_h[2], *g_ss[2], *g_act;
+  uint64_t *g_qkv, *g_att, *g_h[2], *g_ss[2], *g_act;
   uint32_t *err, *epoch, *exit_cnt;
   uint64_t* trace;  // nullptr, or [layers][PSE_TRACE_EV][256] s_memrealtime stamps
   int probe;        // timing probe (MTTS_PSE_PROBE; results invalid): 1 loader issues no DMA,

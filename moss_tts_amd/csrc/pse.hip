@@ -12,20 +12,23 @@
 // keeps filling with the next op's weights.
 //
 // Geometry: one 320-thread workgroup per CU (the LDS request keeps it at one; all P = 256
-// resident).  Wave 0 is the LOADER: it streams this CU's weight slices, in op order, into an
-// LDS ring of PSE_NS 16 KiB slots by LDS-DMA (global_load_lds 16 B / lane,
-// non-temporal), and publishes each slot in an LDS FULL counter once its DMA has retired
-// (counted vmcnt).  Waves 1-4 are CONSUMERS: each takes 4 of a slot's 16 packed 1 KiB tiles
+// resident).  Wave 0 is the LOADER: it streams this CU's weight slices, in op order, through 3
+// register buffers (16 B / lane non-temporal loads, counted vmcnt) into an LDS ring of PSE_NS
+// 16 KiB slots, and publishes each slot in an LDS FULL counter once it is written.  (Round 2
+// filled the ring by LDS-DMA directly; staging through registers keeps the slots in flight out
+// of the ring.)  Waves 1-4 are CONSUMERS: each takes 4 of a slot's 16 packed 1 KiB tiles
 // (v_mfma_f32_16x16x32_bf16, A = the tile from LDS, B = the op's input vector staged in LDS),
 // reports the slot free, and at the end of a row tile the four partial tiles are reduced in LDS
 // in a fixed order (deterministic).
 //
-// Work split per layer (CU c of P = 256): q|k|v = 768 half tiles (row tile, K half), 3 per CU;
-// o_proj and down = row tile c (CU c owns residual columns 16c..16c+15 for the whole step);
-// gate|up = tile pairs 3c..3c+2.  92 slots (1.47 MB) per CU per layer.  The attention of KV
-// head g runs on the consumers of PSE_AU CUs (pse_att_unit: unit k takes every PSE_AU-th group
-// of chunks, unit 0 merges), whose loaders pause while it runs (PSE_APAUSE).  The engine takes
-// this launch only for contexts up to its PSE range (engine.cpp pse_choose).
+// Work split per layer (CU c of P = 256): q|k|v = 768 half tiles (row tile, K half), 3 per CU
+// (q tile c whole, then one k|v half tile: pse_qkv_unit); o_proj and down = row tile c (CU c owns
+// residual columns 16c..16c+15 for the whole step); gate|up = pairs c, c + 256, c + 512
+// (pse_gu_pair).  92 slots (1.47 MB) per CU per layer.  The attention of KV head g runs on the
+// consumers of PSE_AU CUs (pse_att_unit: unit k takes q heads k G / PSE_AU .. over every key),
+// whose loaders pause while it runs (PSE_APAUSE).  The loader stages slots through registers
+// (PSE_RLOAD).  The engine takes this launch only for contexts up to its PSE range
+// (engine.cpp pse_choose).
 //
 // Hand-offs: data-tagged granules (MI355X_MICROARCH.md "handoff-1to1" / "allgather"): 8 bytes
 // {32-bit payload, 32-bit tag} written by ONE write-through (sc1) store and read with sc1 loads;
@@ -42,7 +45,8 @@ constexpr int CW = 4;                   // consumer waves
 #ifndef PSE_LW
 #define PSE_LW 1
 #endif
-constexpr int LW = PSE_LW;              // loader waves (each its own vmcnt: 4 fills = 64 instructions)
+constexpr int LW = PSE_LW;              // loader waves
+static_assert(LW == 1, "the register-staged loader publishes one FULL counter");
 constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_POLL_SLEEP
 #define PSE_POLL_SLEEP 1  // s_sleep count between a gather's sweeps (x 64 cycles)
@@ -67,13 +71,8 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_NS
 #define PSE_NS 8
 #endif
-#ifndef PSE_FILLS
-#define PSE_FILLS 3
-#endif
 constexpr int NS = PSE_NS;              // ring slots
 constexpr int SLOT_KB = 16;             // 1 KiB tiles per slot
-constexpr int FILLS = PSE_FILLS;        // slot fills the loader keeps in flight (HBM latency under
-                                        // load ~5 us: bytes in flight set the rate)
 constexpr int SPL = 92;                 // slots per layer per CU
 constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
 enum { OP_QKV = 0, OP_ATT = 1, OP_O = 2, OP_GU = 3, OP_DOWN = 4 };
@@ -101,46 +100,22 @@ __device__ __forceinline__ void st32(void* p, uint32_t v) {
   do {                                                                                          \
     if (a.trace && lane == 0) a.trace[((size_t)(l) * PSE_TRACE_EV + (ev)) * 256 + c] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
-// LDS-DMA of 1 KiB (16 B per lane) to the wave-uniform LDS byte address lds_byte, non-temporal.
-// Inline asm so that hipcc does not see an LDS write in flight: for a builtin it drains vmcnt
-// (every fill) before each later LDS access of the loader (cdna_hip_programming.md §5.7); the
-// loader counts its fills itself.
-__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds_byte) {
-  uint32_t keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep)
-               : "v"(gsrc), "s"(lds_byte)
-               : "memory");
-}
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
-#ifndef PSE_QFIRST
-#define PSE_QFIRST 1  // q|k|v: q tiles first on every CU; the attention runs its cached-key chunks before k / v arrive
-#endif
-#ifndef PSE_ACTPIPE
-#define PSE_ACTPIPE 2  // 2: every act round's hand-off hidden (below); 1: round 2's; 0: none
-#endif
-// q|k|v unit j (0..2) of CU c: (row tile, K half).  PSE_QFIRST: both halves of q row tile c,
-// then half c & 1 of k|v row tile 256 + c / 2 -- every q tile is complete two thirds into the
-// q|k|v stream, so the attention units start on q while k / v are still being produced;
-// otherwise units 3c .. 3c+2 in (tile, half) order.
+// q|k|v unit j (0..2) of CU c: (row tile, K half) -- both halves of q row tile c, then half c & 1
+// of k|v row tile 256 + c / 2.  Every q tile is complete two thirds into the q|k|v stream, so the
+// attention units start on q while k / v are still being produced (round 3; units 3c .. 3c+2 in
+// (tile, half) order before: 2.824 -> 2.804 ms/step).
 __device__ __forceinline__ void pse_qkv_unit(int c, int j, int* t, int* half) {
-  if (PSE_QFIRST) {
-    *t = j < 2 ? c : HQ_ * D_ / 16 + (c >> 1);
-    *half = j < 2 ? j : (c & 1);
-  } else {
-    const int u = 3 * c + j;
-    *t = u >> 1;
-    *half = u & 1;
-  }
+  *t = j < 2 ? c : HQ_ * D_ / 16 + (c >> 1);
+  *half = j < 2 ? j : (c & 1);
 }
-// gate|up pair of CU c in round j (3 pairs per CU).  PSE_ACTPIPE: round j of every CU makes
-// the SwiGLU columns [4096 j, 4096 j + 4096), i.e. down_proj's k range of its slots 8j .. 8j+7,
-// so rounds 0 and 1 are published long before the down stream needs them and only round 2's
-// hand-off remains, hidden behind down's first 16 slots (the consumers below); otherwise
-// pairs 3c .. 3c+2.
-__device__ __forceinline__ int pse_gu_pair(int c, int j) { return PSE_ACTPIPE ? c + 256 * j : 3 * c + j; }
+// gate|up pair of CU c in round j (3 pairs per CU): round j of every CU makes the SwiGLU columns
+// [4096 j, 4096 j + 4096), i.e. down_proj's k range of its slots 8j .. 8j+7, so every round's
+// hand-off flies while earlier rounds' work runs (the consumers below; round 3, pairs 3c .. 3c+2
+// before: 2.981 -> 2.842 ms/step)
+__device__ __forceinline__ int pse_gu_pair(int c, int j) { return c + 256 * j; }
 // slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles of CU c
 __device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, int c, int s) {
   const int l = s / SPL, r = s - l * SPL;
@@ -192,17 +167,11 @@ static_assert(L_END <= 160 * 1024, "LDS");
 }  // namespace
 
 size_t pse_lds_bytes() { return (size_t)L_END; }
-// Attention units: PSE_AU per KV head, each a quarter of the 32-key chunks (round-robin), so a
-// wave holds one chunk up to 32 PSE_AU CW keys of context.  Unit index u = g * PSE_AU + k runs on
-// CU P - 1 - 7 u (spread over the XCDs under round-robin placement); -1: no attention unit.
+// Attention units: PSE_AU per KV head, each G / PSE_AU of the head's q heads over every key
+// (attention() below).  Unit index u = g * PSE_AU + k runs on CU P - 1 - 7 u (spread over the
+// XCDs under round-robin placement); -1: no attention unit.
 #ifndef PSE_AU
 #define PSE_AU 2
-#endif
-#ifndef PSE_RLOAD
-#define PSE_RLOAD 1  // register-staged loader (1) or LDS-DMA fills (0)
-#endif
-#ifndef PSE_HSPLIT
-#define PSE_HSPLIT 1  // attention units split a KV head's q heads (1) or its keys (0)
 #endif
 __host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
@@ -399,13 +368,19 @@ __device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
 }
 
 // ---------------------------------------------------------------------------
-// Attention of KV head g for the new token at pos (B = 1), by the CW consumer waves: q / k
-// RMSNorm + RoPE (TF/.../modeling_qwen3.py:252-254, :148-170), K / V appended at pos
-// (TF/cache_utils.py:127-145), softmax(q k^T / sqrt(D)) v over keys 0..pos with the
-// probabilities rounded to bf16 before P.V (the reference's bf16 SDPA), per-wave online softmax
-// over 32-key chunks, the CW partials merged in a fixed order -> G x D outputs as granules.
+// Attention unit (g, ku) for the new token at pos (B = 1), by the CW consumer waves: the KV
+// head's q heads h0 .. h0 + HU - 1 (HU = G / PSE_AU, h0 = ku HU) over EVERY key, so a unit's
+// outputs are final where they are computed (no cross-unit merge).  q / k RMSNorm + RoPE
+// (TF/.../modeling_qwen3.py:252-254, :148-170), K / V appended at pos (TF/cache_utils.py:127-145),
+// softmax(q k^T / sqrt(D)) v over keys 0..pos with the probabilities rounded to bf16 before P.V
+// (the reference's bf16 SDPA), per-wave online softmax over 32-key chunks, the CW wave partials
+// and the new key merged in a fixed order -> HU x D outputs as granules.
+//   1. gather this unit's q rows (their tiles are complete two thirds into the q|k|v stream,
+//      PSE_QFIRST) -- the first chunk's K / V^T and the prologue's inputs load behind the sweep;
+//   2. the cached keys' chunks (keys < pos) run while the new token's k / v partials are gathered;
+//   3. k / v RMSNorm + RoPE, appended by unit 0;
+//   4. merge: the CW wave partials, then the new key (score q . k, p = 1) -> publish.
 // graw: the gathered q|k|v K-half partials, [tile][half][16] fp32 (q tiles, k tiles, v tiles).
-// (false on a failed wait)
 // Not inlined: the attention's chunk state (K / V^T fragments, online-softmax accumulators) is
 // ~200 VGPRs; inlined, it pushed the whole kernel past the 256-VGPR budget of 2 waves per SIMD
 // and spilled registers live across every other phase (scratch reloads on the hand-off paths of
@@ -420,41 +395,26 @@ __device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
 #else
 #define PSE_ATT_INL __forceinline__
 #endif
-__device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask,
-                                                   const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
-                                                   uint64_t* g_att, uint64_t* g_attp, uint32_t* err, uint64_t* trace,
-                                                   float eps, float scale, int Cmax_, uint32_t epoch, int bar_gen,
-                                                   int l, int unit, uint32_t tq) {
+__device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask, const bf16_t* cos_t,
+                                     const bf16_t* sin_t, uint64_t* g_qkv, uint64_t* g_att, uint32_t* err,
+                                     uint64_t* trace, float eps, float scale, int Cmax, uint32_t epoch, int bar_gen,
+                                     int l, int unit, uint32_t tq) {
   const int c = blockIdx.x;
   Ctx x{err, eps, 0, c, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64, epoch, bar_gen};
   struct {
-    const int* pos;
-    const uint8_t* mask;
-    const bf16_t *cos_t, *sin_t;
-    uint64_t *g_att, *g_attp, *trace;
-    float eps, scale;
-    int Cmax;
-  } a{pos_p, mask, cos_t, sin_t, g_att, g_attp, trace, eps, scale, Cmax_};
-  const int g = unit / PSE_AU, ku = unit % PSE_AU;
-#if PSE_HSPLIT
-  // unit ku of KV head g: q heads h0 .. h0 + HU - 1 of the group over EVERY key (no cross-unit
-  // merge); the key-split form (PSE_HSPLIT=0) gives each unit every head over 1 / PSE_AU of the
-  // keys and merges unit partials into unit 0
-  constexpr int HU = G_ / PSE_AU;
-  const int h0 = ku * HU;
-#else
-  constexpr int HU = G_;
-  const int h0 = 0;
-#endif
+    uint64_t* trace;
+  } a{trace};  // (PSE_STAMP)
+  constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = G_ / PSE_AU;
+  static_assert(HU * D / 2 <= CW * 64 && D / 2 == 64, "merge: one wave per head, 2 dims per lane");
+  const int g = unit / PSE_AU, ku = unit % PSE_AU, h0 = ku * HU;
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
-  constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16;
+  uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
   const PseLayer& Lw = *Lp;
-  const int pos = *a.pos;
+  const int pos = *pos_p;
   const int lane = x.lane, w = x.wave - LW, g4 = lane >> 4, c16 = lane & 15;
-  const int Cmax = a.Cmax;
   bf16_t* kcache = Lw.kc + (size_t)g * Cmax * D;  // [Cmax][D]
   bf16_t* vcache = Lw.vc + (size_t)g * D * Cmax;  // [D][Cmax]
-  bf16_t* q_s = reinterpret_cast<bf16_t*>(pse_lds + L_ATT);           // [16][D] (heads >= G zero)
+  bf16_t* q_s = reinterpret_cast<bf16_t*>(pse_lds + L_ATT);           // [16][D] (rows >= HU zero)
   float* k_s = reinterpret_cast<float*>(q_s + 16 * D);              // [D]
   float* v_s = k_s + D;                                             // [D]
   bf16_t* p_s = reinterpret_cast<bf16_t*>(v_s + D);                 // [CW][16][KW]
@@ -463,10 +423,10 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   constexpr uint32_t OOBA = 0x7ffffff0u;
   const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(kcache, 0, Cmax * D * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(vcache, 0, Cmax * D * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(a.mask), 0, Cmax, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mask), 0, Cmax, 0x00020000);
   const int nchunk = pos / KW + 1;
   // a wave's 32-key chunk: K tiles (A operands), V^T fragments (B operands), mask words; keys
-  // >= pos read zero (branch-free buffer loads; the new key / value are patched in from LDS)
+  // >= pos read zero (branch-free buffer loads; the new key joins in the merge)
   auto load_chunk = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
     const int k0 = ch * KW;
 #pragma unroll
@@ -488,45 +448,28 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   };
   u32x4 ktA[2][QS], vtA[DT];
   uint32_t mkA[2];
-#if PSE_HSPLIT
-  // this wave's chunks: w, then every CW
+  // this wave's chunks: w, then every CW; its q job (wave w < HU: q row w) norm weight, wave 0's
+  // k norm weight, the RoPE row at pos (2 dims per lane) and the new token's mask byte
   const int ch0 = w;
   constexpr int CSTEP = CW;
-#else
-  // this wave's chunks: ku CW + w, then every PSE_AU CW
-  const int ch0 = ku * CW + w;
-  constexpr int CSTEP = PSE_AU * CW;
-#endif
-  // this wave's jobs' norm weights and the RoPE row at pos (2 dims per lane)
-  constexpr int JW = (HU + 2 + CW - 1) / CW;  // jobs per wave
-  uint32_t pnw[JW], pcs = 0, psn = 0, knw = 0, mnew = 0;
-  // the first chunk and the prologue's inputs go out right behind the q|k|v gather's first
-  // sweep (the cached keys do not depend on it)
-  constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the head's q|k|v granules
+  uint32_t qnw = 0, knw = 0, pcs = 0, psn = 0, mnew = 0;
   auto prefetch = [&]() {
     load_chunk(ch0, ktA, vtA, mkA);
-#pragma unroll
-    for (int jj = 0; jj < JW; ++jj) {
-      const int j = w + jj * CW;
-      pnw[jj] = j <= HU ? reinterpret_cast<const uint32_t*>(j < HU ? Lw.q_norm : Lw.k_norm)[lane] : 0u;
-    }
-    pcs = reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D)[lane];
-    psn = reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D)[lane];
-    if (PSE_QFIRST) {
-      knw = reinterpret_cast<const uint32_t*>(Lw.k_norm)[lane];
-      mnew = a.mask[pos];
-    }
+    qnw = w < HU ? reinterpret_cast<const uint32_t*>(Lw.q_norm)[lane] : 0u;
+    knw = reinterpret_cast<const uint32_t*>(Lw.k_norm)[lane];
+    pcs = reinterpret_cast<const uint32_t*>(cos_t + (size_t)pos * D)[lane];
+    psn = reinterpret_cast<const uint32_t*>(sin_t + (size_t)pos * D)[lane];
+    mnew = mask[pos];
   };
-  if (PSE_APAUSE && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   // q|k|v row value: sum of the two K-half partials, rounded to bf16 (the projection output)
   auto val = [&](int base_tile, int i) {
     const float* p = graw + (base_tile + i / 16) * 32 + i % 16;
     return rbf(p[0] + p[16]);
   };
-  // q / k RMSNorm + RoPE of one row (TF/.../modeling_qwen3.py:252-254, :148-170): 2 dims per lane
+  // q / k RMSNorm + RoPE of one row: 2 dims per lane
   auto norm_rope = [&](float x0, float x1, uint32_t nw, float& o0, float& o1) {
     const float ss = wave_sum(x0 * x0 + x1 * x1);
-    const float r = 1.0f / sqrtf(ss / (float)D + a.eps);
+    const float r = 1.0f / sqrtf(ss / (float)D + eps);
     const float n0 = rbf(__uint_as_float(nw << 16) * rbf(x0 * r)), n1 = rbf(__uint_as_float(nw & 0xffff0000u) * rbf(x1 * r));
     constexpr int q4 = D / 4;
     const bool lo = 2 * lane < D / 2;
@@ -538,65 +481,25 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
     o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
   };
-#if PSE_QFIRST
-  static_assert(PSE_HSPLIT, "q-first attention assumes head-split units");
-  // (1) this unit's q heads only (their tiles are complete two thirds into the q|k|v stream)
+  if (PSE_APAUSE && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // ---- 1. q ----
+  constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the KV head's q|k|v granules (qkv_gran)
   constexpr int NQ = HU * (D_ / 16) * 32, NKV = 2 * (D_ / 16) * 32;
-  uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
   if (!gather<(NQ + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + h0 * (D_ / 16) * 32, NQ, tq,
                                               graw32 + h0 * (D_ / 16) * 32, NQ, nullptr, prefetch))
     return -1;
   if (w == 0) PSE_STAMP(l, 15);
   for (int i = x.tid; i < 16 * D; i += CW * 64)
     if (i / D >= HU) q_s[i] = 0;
-#pragma unroll
-  for (int jj = 0; jj < JW; ++jj) {
-    const int j = w + jj * CW;
-    if (j >= HU) continue;
-    const int bt = (h0 + j) * (D / 16);
+  if (w < HU) {
+    const int bt = (h0 + w) * (D / 16);
     float o0, o1;
-    norm_rope(val(bt, 2 * lane), val(bt, 2 * lane + 1), pnw[jj], o0, o1);
-    q_s[j * D + 2 * lane] = f2bf(o0);
-    q_s[j * D + 2 * lane + 1] = f2bf(o1);
+    norm_rope(val(bt, 2 * lane), val(bt, 2 * lane + 1), qnw, o0, o1);
+    q_s[w * D + 2 * lane] = f2bf(o0);
+    q_s[w * D + 2 * lane + 1] = f2bf(o1);
   }
   cbar(x);
-#else
-  if (!gather<NG / (CW * 64)>(x, g_qkv + (size_t)g * NG, NG, tq, reinterpret_cast<uint32_t*>(pse_lds + L_GRAW), NG,
-                              nullptr, prefetch))
-    return -1;
-  if (w == 0) PSE_STAMP(l, 15);
-  for (int i = x.tid; i < 16 * D; i += CW * 64)
-    if (i / D >= HU) q_s[i] = 0;
-  // jobs: j < HU q head h0 + j (q_s row j), HU: k, HU + 1: v; wave w takes jobs w, w + CW; a
-  // lane holds 2 dims
-#pragma unroll
-  for (int jj = 0; jj < JW; ++jj) {
-    const int j = w + jj * CW;
-    if (j >= HU + 2) continue;
-    const int bt = j < HU ? (h0 + j) * (D / 16) : (j == HU ? G * (D / 16) : (G + 1) * (D / 16));
-    const float x0 = val(bt, 2 * lane), x1 = val(bt, 2 * lane + 1);
-    if (j == HU + 1) {
-      v_s[2 * lane] = x0;
-      v_s[2 * lane + 1] = x1;
-      if (ku == 0) {  // one unit appends the new token to the cache
-        vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
-        vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
-      }
-      continue;
-    }
-    float o0, o1;
-    norm_rope(x0, x1, pnw[jj], o0, o1);
-    if (j < HU) {
-      q_s[j * D + 2 * lane] = f2bf(o0);
-      q_s[j * D + 2 * lane + 1] = f2bf(o1);
-    } else {
-      k_s[2 * lane] = o0;
-      k_s[2 * lane + 1] = o1;
-      if (ku == 0) *reinterpret_cast<uint32_t*>(kcache + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
-    }
-  }
-  cbar(x);
-#endif
+  // ---- 2. the cached keys ----
   float m_run = -INFINITY, l_run = 0.f;
   f32x4 o_run[DT];
 #pragma unroll
@@ -606,16 +509,6 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     f32x4 sacc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
-      if (!PSE_QFIRST && k0 + t * 16 + c16 == pos) {  // the new key, from LDS
-#pragma unroll
-        for (int s2 = 0; s2 < QS; ++s2) {
-          const int d0 = s2 * 32 + 8 * g4;
-          u32x4 v;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] = pack2(k_s[d0 + 2 * i], k_s[d0 + 2 * i + 1]);
-          kt[t][s2] = v;
-        }
-      }
       sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s2 = 0; s2 < QS; ++s2)
@@ -623,31 +516,14 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
                                                          *reinterpret_cast<const bf16x8*>(&q_s[c16 * D + s2 * 32 + 8 * g4]),
                                                          sacc[t], 0, 0, 0);
     }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const int dim = dt * 16 + c16, kb = k0 + 8 * g4;
-      if (!PSE_QFIRST && kb + 8 > pos && kb <= pos) {  // the new value patched in, keys past pos zero
-        u32x4 v = vt[dt];
-        const uint32_t nv = (uint32_t)f2bf(v_s[dim]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int kk = kb + 2 * i;
-          const uint32_t lo = kk < pos ? (v[i] & 0xffffu) : (kk == pos ? nv : 0u);
-          const uint32_t hi = kk + 1 < pos ? (v[i] >> 16) : (kk + 1 == pos ? nv : 0u);
-          v[i] = lo | (hi << 16);
-        }
-        vt[dt] = v;
-      }
-    }
     float sv[2][4], mc = -INFINITY;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int key = k0 + t * 16 + g4 * 4 + r;
-        // (PSE_QFIRST: the new key at pos joins in the final merge instead)
-        const bool valid = (PSE_QFIRST ? key < pos : key <= pos) && ((mk[t] >> (8 * r)) & 0xffu);
-        sv[t][r] = valid ? sacc[t][r] * a.scale : -INFINITY;
+        const bool valid = key < pos && ((mk[t] >> (8 * r)) & 0xffu);
+        sv[t][r] = valid ? sacc[t][r] * scale : -INFINITY;
         mc = fmaxf(mc, sv[t][r]);
       }
     mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
@@ -692,8 +568,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    };
-  if (PSE_APAUSE == 1 && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
   auto chunks = [&]() {
     if (w == 0) PSE_STAMP(l, 16);
     for (int ch = ch0; ch < nchunk; ch += CSTEP) {
@@ -702,12 +577,10 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     }
     if (w == 0) PSE_STAMP(l, 17);
   };
-#if PSE_QFIRST
-  // (2) the cached keys' chunks run while the new token's k / v partials are gathered
   if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + G * (D_ / 16) * 32, NKV, tq,
                                                graw32 + G * (D_ / 16) * 32, NKV, nullptr, chunks))
     return -1;
-  // (3) k (wave 0: RMSNorm + RoPE) and v (wave 1); unit 0 appends them to the cache
+  // ---- 3. k (wave 0) and v (wave 1); unit 0 appends them ----
   if (w == 0) {
     float o0, o1;
     norm_rope(val(G * (D / 16), 2 * lane), val(G * (D / 16), 2 * lane + 1), knw, o0, o1);
@@ -723,9 +596,6 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
       vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
     }
   }
-#else
-  chunks();
-#endif
   if (lane < HU) {
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
@@ -738,97 +608,32 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
       if (h < HU) acc_s[(w * HU + h) * D + dt * 16 + c16] = o_run[dt][r];
     }
   cbar(x);
-#if PSE_HSPLIT
-  {
-    // merge the CW wave partials of this unit's heads in a fixed order (thread e / 2: 2 output
-    // dims of local head h), then publish them: they are final
-    const int e = 2 * x.tid, h = e / D, d = e % D;
-    if (e < HU * D) {  // (D / 2 = 64 threads per head: one whole wave each)
-      float M = -INFINITY;
+  // ---- 4. merge (thread e / 2: 2 output dims of local head h = wave w) and publish ----
+  const int e = 2 * x.tid, h = e / D, d = e % D;
+  if (e < HU * D) {
+    float M = -INFINITY;
 #pragma unroll
-      for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
-#if PSE_QFIRST
-      // the new key at pos: its score q . k (this wave's head), as one more partial with p = 1
-      const float sn = wave_sum(bf2f(q_s[h * D + d]) * k_s[d] + bf2f(q_s[h * D + d + 1]) * k_s[d + 1]) * a.scale;
-      const bool nv = mnew != 0u;
-      if (nv) M = fmaxf(M, sn);
-#endif
-      float L = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
+    // the new key: its score q . k (this wave's head), one more partial with p = bf16(1) = 1
+    const float sn = wave_sum(bf2f(q_s[h * D + d]) * k_s[d] + bf2f(q_s[h * D + d + 1]) * k_s[d + 1]) * scale;
+    const bool nv = mnew != 0u;
+    if (nv) M = fmaxf(M, sn);
+    float L = 0.f, o0 = 0.f, o1 = 0.f;
 #pragma unroll
-      for (int ww = 0; ww < CW; ++ww) {
-        const float mw = ml_s[(ww * HU + h) * 2];
-        const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
-        L += f * ml_s[(ww * HU + h) * 2 + 1];
-        o0 += f * acc_s[(ww * HU + h) * D + d];
-        o1 += f * acc_s[(ww * HU + h) * D + d + 1];
-      }
-#if PSE_QFIRST
-      if (nv) {
-        const float f = expf(sn - M);
-        L += f;
-        o0 += f * v_s[d];
-        o1 += f * v_s[d + 1];
-      }
-#endif
-      st64(a.g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+    for (int ww = 0; ww < CW; ++ww) {
+      const float mw = ml_s[(ww * HU + h) * 2];
+      const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
+      L += f * ml_s[(ww * HU + h) * 2 + 1];
+      o0 += f * acc_s[(ww * HU + h) * D + d];
+      o1 += f * acc_s[(ww * HU + h) * D + d + 1];
     }
-    cbar(x);
-    return x.bar_gen;
-  }
-#endif
-  // merge the CW wave partials in a fixed order: thread e2 holds 2 output dims of head h,
-  // unnormalised (M, L, O) of this unit
-  const int e = 2 * x.tid, h = e / D, d = e % D;  // G * D / 2 == CW * 64 threads
-  float M = -INFINITY;
-#pragma unroll
-  for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * G + h) * 2]);
-  float L = 0.f, o0 = 0.f, o1 = 0.f;
-#pragma unroll
-  for (int ww = 0; ww < CW; ++ww) {
-    const float mw = ml_s[(ww * G + h) * 2];
-    const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
-    L += f * ml_s[(ww * G + h) * 2 + 1];
-    o0 += f * acc_s[(ww * G + h) * D + d];
-    o1 += f * acc_s[(ww * G + h) * D + d + 1];
-  }
-  constexpr int PW = G * D + 2 * G;  // partial granules of one unit: O [G][D], M [G], L [G]
-  if constexpr (PSE_AU == 1) {
-    st64(a.g_att + (g * G * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
-  } else {
-  if (ku != 0) {
-    // units 1..: publish the partial for unit 0 of the head
-    const uint32_t tp = tagof(x.epoch, l, OP_ATT) | 0x80000000u;
-    uint64_t* pp = a.g_attp + (size_t)unit * PW;
-    st64(pp + e, gran(__float_as_uint(o0), tp));
-    st64(pp + e + 1, gran(__float_as_uint(o1), tp));
-    if (d == 0) {
-      st64(pp + G * D + h, gran(__float_as_uint(M), tp));
-      st64(pp + G * D + G + h, gran(__float_as_uint(L), tp));
+    if (nv) {
+      const float f = expf(sn - M);
+      L += f;
+      o0 += f * v_s[d];
+      o1 += f * v_s[d + 1];
     }
-    cbar(x);
-    return x.bar_gen;
-  }
-  // unit 0: the other units' partials (contiguous), merged in unit order -> the output granules
-  float* pg = reinterpret_cast<float*>(pse_lds + L_GRAW);  // (q|k|v partials and q_s are dead)
-  if (!gather<((PSE_AU - 1) * PW + CW * 64 - 1) / (CW * 64)>(x, a.g_attp + (size_t)(unit + 1) * PW, (PSE_AU - 1) * PW,
-                                                            tagof(x.epoch, l, OP_ATT) | 0x80000000u,
-                                                            reinterpret_cast<uint32_t*>(pg), (PSE_AU - 1) * PW))
-    return -1;
-  if (w == 0) PSE_STAMP(l, 18);
-  float MM = M;
-#pragma unroll
-  for (int k2 = 1; k2 < PSE_AU; ++k2) MM = fmaxf(MM, pg[(k2 - 1) * PW + G * D + h]);
-  float LL = 0.f, O0 = 0.f, O1 = 0.f;
-#pragma unroll
-  for (int k2 = 0; k2 < PSE_AU; ++k2) {
-    const float* q = pg + (k2 - 1) * PW;
-    const float mk = k2 == 0 ? M : q[G * D + h];
-    const float f = (mk == -INFINITY) ? 0.f : expf(mk - MM);
-    LL += f * (k2 == 0 ? L : q[G * D + G + h]);
-    O0 += f * (k2 == 0 ? o0 : q[e]);
-    O1 += f * (k2 == 0 ? o1 : q[e + 1]);
-  }
-  st64(a.g_att + (g * G * D + e) / 2, gran(LL > 0.f ? pack2(O0 / LL, O1 / LL) : 0u, tagof(x.epoch, l, OP_ATT)));
+    st64(g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
   }
   cbar(x);
   return x.bar_gen;
@@ -858,12 +663,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
   if (wave < LW) {
     // =================== loaders ===================
     if (PSE_LPRIO) __builtin_amdgcn_s_setprio(PSE_LPRIO);  // (A/B: the loader ahead of spinning consumers)
-    // loader wave k streams slots k, k + LW, ...; m = its own slot count, marked = its slots
-    // published in full[k]
-    const int k = wave;
-    int marked = 0, m = 0;
     auto slot_src = [&](int s) { return pse_slot_src(wp, c, s); };
-#if PSE_RLOAD
     // Register-staged loader: each slot is loaded into one of 3 register buffers (16 x 16 B per
     // lane) and copied into its ring slot once that slot is free, so the 3 slots in flight do not
     // occupy ring slots (8 ready + 3 in flight, against 8 including the in-flight fills of the
@@ -874,8 +674,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     // flight.  Every copy / reload issues exactly 16 loads (a slot past the end re-reads the last
     // slot), which keeps that count exact; loads are only ever addressed inside the weights (a
     // prefetch past the last slot would index the pointer table past its last layer).
-    (void)m;
-    (void)marked;
     u32x4 bA[SLOT_KB], bB[SLOT_KB], bC[SLOT_KB];
     bool dead = false;
     const uint32_t voff = (uint32_t)lane * 16u;
@@ -997,64 +795,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
 #undef PSE_RL_LOADS
     if (dead) st32(a.err, 1u);
     __hip_atomic_store(&ctl->full[0], dead ? 0 : total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-#else
-    for (int s = k; s < total; s += LW, ++m) {
-      // ring slot s % NS is free once every consumer wave has read slot s - NS
-      if (s >= NS) {
-        for (uint32_t spins = 0;; ++spins) {
-          int mn = 1 << 30;
-#pragma unroll
-          for (int w = 0; w < CW; ++w)
-            mn = min(mn, __hip_atomic_load(&ctl->freed[w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-          if (mn >= s - NS + 1) break;
-          if (marked < m) {  // stalled: retire every fill in flight so the consumers can drain the ring
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            marked = m;
-            __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          }
-          if (spins > SPIN_LDS || __hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            st32(a.err, 1u);
-            s = total;  // drain
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (s >= total) break;
-      }
-      // this CU's attention is gathering its inputs: no new fills (its sweeps and chunk loads
-      // would queue behind them); retire the ones in flight
-      if (PSE_APAUSE && __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        marked = m;
-        __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        for (uint32_t spins = 0; __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
-                                 !__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
-                                 spins < SPIN_LDS;
-             ++spins)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      const int l = s / SPL, r = s - l * SPL;
-      if (a.trace && lane == 0) {  // loader events into LDS (global stores would join its vmcnt count)
-        const int ev = r == 0 ? 0 : (r == 12 ? 1 : (r == 20 ? 2 : (r == 68 ? 3 : (r >= SPL - LW ? 4 : -1))));
-        if (ev >= 0) ctl->lstamp[l & 1][ev] = __builtin_amdgcn_s_memrealtime();
-      }
-      const bf16_t* src = slot_src(s);
-      const uint32_t dst = __builtin_amdgcn_readfirstlane(
-          (uint32_t)(uintptr_t)(lvoid*)(lds + L_RING + (s % NS) * SLOT_KB * 1024));
-      if (a.probe != 1) {
-#pragma unroll
-        for (int t = 0; t < SLOT_KB; ++t) glds16(reinterpret_cast<const u32x4*>(src) + t * 64 + lane, dst + t * 1024);
-      }
-      // keep FILLS - 1 of this wave's fills in flight behind this one; publish the older ones
-      if (m + 1 - marked >= FILLS) {
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((FILLS - 1) * SLOT_KB) : "memory");
-        marked = m + 1 - (FILLS - 1);
-        __hip_atomic_store(&ctl->full[k], marked, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(&ctl->full[k], m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-#endif
   } else {
     // =================== consumers ===================
     Ctx x{a.err, a.eps, a.probe, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
@@ -1120,7 +860,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       // ---------------- attention (one CU per KV head) ----------------
       if (att_u >= 0) {
         // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
-        const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.g_attp, a.err, a.trace,
+        const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.err, a.trace,
                                  a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
         const bool att_ok = bg >= 0;
         if (att_ok) x.bar_gen = bg;
@@ -1170,7 +910,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         cbar(x);
         PSE_PRIO_DOWN();
       };
-#if PSE_ACTPIPE == 2
       gu_round(0);
       gu_round(1);
       // round 2 runs inside the gather of round 0's columns (published a round ago) -> xs
@@ -1181,13 +920,8 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
       };
       if (!gather<8>(x, a.g_act, I_ / 6, tg, xs32 + I_ / 6, I_ / 6, nullptr, gu2)) break;
-#else
-      #pragma unroll 1
-      for (int j = 0; j < 3; ++j) gu_round(j);
-#endif
       if (wave == LW) PSE_STAMP(l, 7);
       // ---------------- down (+ residual) ----------------
-#if PSE_ACTPIPE == 2
       if (wave == LW) PSE_STAMP(l, 8);
       {
         // down's k-slots 8j .. 8j+7 read round j's columns: round 0 in xs k-tiles 128 .. 255,
@@ -1204,31 +938,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         if (!gather<8>(x, a.g_act + I_ / 3, I_ / 6, tg, xs32, I_ / 6, nullptr, [&]() { slots(8, 128); })) break;
         #pragma unroll 1
         for (int k = 16; k < 24; ++k) consume_slot(x, seq++, k * 16 - 256, acc);
-#elif PSE_ACTPIPE
-      // rounds 0 and 1 (columns 0 .. 8191, published one and two gate|up rounds ago): one sweep
-      if (!gather<16>(x, a.g_act, I_ / 3, tg, xs32, I_ / 3)) break;
-      if (wave == LW) PSE_STAMP(l, 8);
-      {
-        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        // round 2's sweep goes out first; its 16 k-slots of rounds 0 and 1 are consumed while it
-        // flies (at normal priority: the raised one would starve the loader), then the rest
-        auto first16 = [&]() {
-          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
-          #pragma unroll 1
-          for (int k = 0; k < 16; ++k) consume_slot(x, seq++, k * 16, acc);
-          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
-        };
-        if (!gather<8>(x, a.g_act + I_ / 3, I_ / 6, tg, xs32 + I_ / 3, I_ / 6, nullptr, first16)) break;
-        #pragma unroll 1
-        for (int k = 16; k < 24; ++k) consume_slot(x, seq++, k * 16, acc);
-#else
-      if (!gather<24>(x, a.g_act, I_ / 2, tg, xs32, I_ / 2)) break;
-      if (wave == LW) PSE_STAMP(l, 8);
-      {
-        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        #pragma unroll 1
-        for (int k = 0; k < 24; ++k) consume_slot(x, seq++, k * 16, acc);
-#endif
         PSE_PRIO_UP();
         red_put(x, 0, acc);
         cbar(x);
@@ -1279,8 +988,7 @@ int pse_grid(int device) {
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + HKV_ * PSE_AU * (HQ_ / HKV_ * (D_ + 2)) + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 +
-         64;
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 + 64;
 }
 
 hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
@@ -1289,7 +997,6 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
   uint64_t* g = reinterpret_cast<uint64_t*>(ws);
   a.g_qkv = g; g += 768 * 16;
   a.g_att = g; g += HQ_ * D_ / 2;
-  a.g_attp = g; g += HKV_ * PSE_AU * (HQ_ / HKV_ * (D_ + 2));
   // h granules of an op immediately followed by its sums of squares: one gather range
   a.g_h[0] = g; g += H_ / 2;
   a.g_ss[0] = g; g += H_ / 16;
