@@ -95,9 +95,10 @@ struct mtts_engine {
   bool xpack = true;
   // persistent streaming engine (pse.hip) for the batch-1 decode stack: MTTS_PSE=1 (A/B)
   bool pse = true;               // MTTS_PSE=0: per-op launches for batch-1 decode too
-  int pse_ctx_max = 576;         // PSE only while the context stays within this (MTTS_PSE_CTX):
-                                 // its attention (2 CUs per KV head) loses to the per-op
-                                 // split-K attention beyond ~600 cached keys
+  int pse_ctx_max = 768;         // PSE only while the context stays within this (MTTS_PSE_CTX):
+                                 // its attention (2 CUs per KV head, every key each) loses to
+                                 // the per-op split-K attention beyond ~850 cached keys
+                                 // (scripts/pse_ctx_sweep.py, round 3: 0.97 at 700, 1.02 at 900)
   bool pse_now = false;          // this forward / captured decode step may take the PSE path
   void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
   bool pse_ok = false;           // the shape and the device support it
