@@ -271,7 +271,7 @@ struct PseArgs {
   int probe;        // timing probe (MTTS_PSE_PROBE; results invalid): 1 loader issues no DMA,
                     // 2 consumers skip the slot reads and MFMAs
 };
-constexpr int PSE_TRACE_EV = 20;
+constexpr int PSE_TRACE_EV = 28;
 size_t pse_lds_bytes();
 int pse_grid(int device);
 bool pse_supported(int device, int B, int layers, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);

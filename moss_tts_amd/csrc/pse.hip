@@ -68,6 +68,9 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
+#ifndef PSE_TRACE2
+#define PSE_TRACE2 0  // (diagnostic: the input-norm h gather's own stamps replace the loader's)
+#endif
 #ifndef PSE_NS
 #define PSE_NS 8
 #endif
@@ -192,6 +195,9 @@ struct Ctx {
   int c, lane, wave, tid;
   uint32_t epoch;
   int bar_gen;
+#if PSE_TRACE2
+  uint64_t* tp;  // (PSE_TRACE2: gather stamps of the input-norm h gather into events 10-14)
+#endif
 };
 
 __device__ __forceinline__ bool failed(const Ctx& x) {
@@ -221,11 +227,18 @@ __device__ __forceinline__ void cbar(Ctx& x) {
 // Gather n consecutive granules g[0..n) carrying tag t into LDS: the first n0 payloads to
 // dst0, the rest to dst1; all consumer threads cooperate (n <= MAXP * 256) in ONE sweep loop (one
 // round trip per poll); false on timeout / abort.  Branch-free sc1 buffer loads (an out-of-range
-// offset reads zero): a load under a divergent branch would be waited for at once.
+// offset reads zero): a load under a divergent branch would be waited for at once.  SYNC: a
+// consumer barrier at the end, for data one wave gathers and another reads (the sums of squares,
+// the attention's rows); without it each wave goes on with the granules tid + 256 k it gathered
+// itself -- exactly the columns its consume_slot tiles read (norm_grp)
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
 struct NoHook {
   __device__ void operator()() const {}
 };
-template <int MAXP, typename Hook = NoHook>
+template <int MAXP, bool SYNC = true, typename Hook = NoHook>
 __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_t t, uint32_t* dst0, int n0,
                                        uint32_t* dst1 = nullptr, const Hook& after_first_issue = Hook()) {
   constexpr uint32_t OOB = 0x7ffffff0u;
@@ -260,10 +273,18 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   };
   // the first sweep and the caller's work outside the poll loop (a hook inside it would share
   // the loop's register allocation: the attention's chunk loop spilled there)
+#if PSE_TRACE2
+#define PSE_T2(ev, v) do { if (x.tp && x.wave == LW && x.lane == 0) x.tp[((ev) - 10) * 256] = (v); } while (0)
+#else
+#define PSE_T2(ev, v) do { } while (0)
+#endif
   issue();
+  PSE_T2(10, __builtin_amdgcn_s_memrealtime());
   after_first_issue();
   take();
-  for (uint32_t spins = 1; __any(pend != 0); ++spins) {
+  PSE_T2(14, __builtin_amdgcn_s_memrealtime());
+  uint32_t sweeps = 1;
+  for (uint32_t spins = 1; __any(pend != 0); ++spins, ++sweeps) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
       ok = false;
@@ -274,7 +295,17 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     take();
   }
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(PSE_GPRIO == 2 ? 2 : 0);
-  cbar(x);
+  PSE_T2(11, __builtin_amdgcn_s_memrealtime());
+  PSE_T2(13, (uint64_t)sweeps);
+  if (SYNC) {
+    cbar(x);
+  } else {  // the wave reads back only what its own lanes stored
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  PSE_T2(12, __builtin_amdgcn_s_memrealtime());
+  (void)sweeps;
   return ok && !failed(x);
 }
 
@@ -292,17 +323,39 @@ __device__ __forceinline__ int qkv_gran(int t) {
 
 // Qwen3RMSNorm of the staged vector in place (TF/.../modeling_qwen3.py:59-64):
 // xs = bf16(w * bf16(h * r)), r = 1 / sqrt(sum(ss) / K + eps), ss = the producers' per-16-column
-// sums of squares (n_ss of them, summed in a fixed order by every wave)
-__device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, const bf16_t* w, int K) {
+// sums of squares (n_ss of them, summed in a fixed order by every wave).  The weights w arrive in
+// registers: loaded behind the gather's first sweep, so their latency (a global load queued
+// behind the loader's fills) overlaps the hand-off instead of following it
+// The staged 4096-column vector in 8-column groups (u32x4 index i): consumer wave w reads k-tiles
+// t (32 columns) with t % 16 in [4w, 4w + 4) -- consume_slot's kt0 + 4w + i -- i.e. groups i with
+// i % 64 in [16w, 16w + 16), and the gathers (granule tid + 256 k -> columns 2 granule, 2 granule
+// + 1) write exactly those columns from the same wave.  norm_grp(x, j): this thread's group j of 2.
+__device__ __forceinline__ int norm_grp(const Ctx& x, int j) {
+  return 64 * ((x.lane >> 4) + 4 * j) + 16 * (x.wave - LW) + (x.lane & 15);
+}
+// the norm weights of this thread's two groups
+struct NormW {
+  u32x4 a, b;
+};
+__device__ __forceinline__ NormW norm_w(const Ctx& x, const bf16_t* w) {
+  const u32x4* wv = reinterpret_cast<const u32x4*>(w);
+  return NormW{wv[norm_grp(x, 0)], wv[norm_grp(x, 1)]};
+}
+// Each wave normalises only the columns it gathered and will consume: no barrier after the norm
+// (the sums of squares, gathered across the waves, are behind the gather's barrier)
+__device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, NormW nw) {
+  constexpr int K = H_;
+  static_assert(K / 8 == 2 * CW * 64 && CW == 4, "two 8-column groups per consumer thread");
   // (as the GEMV's norm prologue sums them: 4 per lane, then across the wave; n_ss <= 256)
   float s = 0.f;
   if (4 * x.lane < n_ss) s = (ss[4 * x.lane] + ss[4 * x.lane + 1]) + (ss[4 * x.lane + 2] + ss[4 * x.lane + 3]);
   s = wave_sum(s);
   const float r = 1.0f / sqrtf(s / (float)K + x.eps);
   u32x4* xv = reinterpret_cast<u32x4*>(xs);
-  const u32x4* wv = reinterpret_cast<const u32x4*>(w);
-  for (int i = x.tid; i < K / 8; i += CW * 64) {
-    const u32x4 hv = xv[i], nv = wv[i];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int i = norm_grp(x, j);
+    const u32x4 hv = xv[i], nv = j ? nw.b : nw.a;
     u32x4 o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -312,7 +365,10 @@ __device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, const 
     }
     xv[i] = o;
   }
-  cbar(x);
+  // this wave's own LDS writes are read back by its own lanes only (consume_slot)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // This consumer wave's 4 tiles of ring slot `seq`: acc += W_tiles . x over k tiles kt0 + 4w ..
@@ -406,6 +462,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   } a{trace};  // (PSE_STAMP)
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = G_ / PSE_AU;
   static_assert(HU * D / 2 <= CW * 64 && D / 2 == 64, "merge: one wave per head, 2 dims per lane");
+  static_assert(HU <= 4, "the unit's q rows sit in MFMA D rows 0 .. 3 (lanes 0-15)");
   const int g = unit / PSE_AU, ku = unit % PSE_AU, h0 = ku * HU;
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
   uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
@@ -481,6 +538,10 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
     o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
   };
+  if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 25);
+#if PSE_TRACE2
+  x.tp = trace ? trace + ((size_t)l * PSE_TRACE_EV + 20) * 256 + c : nullptr;  // the q gather: events 20-24
+#endif
   if (PSE_APAUSE && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   // ---- 1. q ----
   constexpr int NG = (G_ + 2) * (D_ / 16) * 32;  // the KV head's q|k|v granules (qkv_gran)
@@ -488,6 +549,9 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   if (!gather<(NQ + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + h0 * (D_ / 16) * 32, NQ, tq,
                                               graw32 + h0 * (D_ / 16) * 32, NQ, nullptr, prefetch))
     return -1;
+#if PSE_TRACE2
+  x.tp = nullptr;
+#endif
   if (w == 0) PSE_STAMP(l, 15);
   for (int i = x.tid; i < 16 * D; i += CW * 64)
     if (i / D >= HU) q_s[i] = 0;
@@ -501,9 +565,13 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   cbar(x);
   // ---- 2. the cached keys ----
   float m_run = -INFINITY, l_run = 0.f;
-  f32x4 o_run[DT];
+  // the running P.V output of the unit's HU real q rows: MFMA D rows 0 .. HU-1 (lanes 0-15, first
+  // HU of each lane's 4 rows); the padding rows are never kept (HU x DT instead of 4 x DT VGPRs)
+  float o_run[DT][HU];
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt) o_run[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
     const int k0 = ch * KW;
     f32x4 sacc[2];
@@ -553,18 +621,18 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
-    float al[4], be[4];
+    float al[HU], be[HU];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      al[r] = __shfl(alpha, g4 * 4 + r, 64);
-      be[r] = __shfl(beta, g4 * 4 + r, 64);
+    for (int r = 0; r < HU; ++r) {
+      al[r] = __shfl(alpha, r, 64);
+      be[r] = __shfl(beta, r, 64);
     }
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
                                                               (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
+      for (int r = 0; r < HU; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -580,6 +648,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + G * (D_ / 16) * 32, NKV, tq,
                                                graw32 + G * (D_ / 16) * 32, NKV, nullptr, chunks))
     return -1;
+  if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 18);
   // ---- 3. k (wave 0) and v (wave 1); unit 0 appends them ----
   if (w == 0) {
     float o0, o1;
@@ -600,14 +669,13 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
+  if (g4 == 0)
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
+    for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int h = g4 * 4 + r;
-      if (h < HU) acc_s[(w * HU + h) * D + dt * 16 + c16] = o_run[dt][r];
-    }
+      for (int r = 0; r < HU; ++r) acc_s[(w * HU + r) * D + dt * 16 + c16] = o_run[dt][r];
   cbar(x);
+  if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 19);
   // ---- 4. merge (thread e / 2: 2 output dims of local head h = wave w) and publish ----
   const int e = 2 * x.tid, h = e / D, d = e % D;
   if (e < HU * D) {
@@ -804,154 +872,174 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     float* ssl = reinterpret_cast<float*>(lds + L_MISC);  // [256] gathered sums of squares
     constexpr int NT = H_ / 16;
     const int att_u = pse_att_unit(c, P);
-    // residual columns 16c .. 16c+15 owned by this CU: lanes 0..15 of wave 1 (bf16 values)
-    float hres = (wave == LW && lane < 16) ? bf2f(a.h[c * 16 + lane]) : 0.f;
-    float hsq = 0.f;
-    int seq = 0;  // ring slot sequence number
-    // o / d: this lane's output row (wave 1, lanes < 16): hidden = residual + bf16(o)
-    // (TF/.../modeling_qwen3.py:311,322), published with its sum of squares
-    auto emit_h = [&](int which, uint32_t t, float o) {
-      if (wave != LW) return;
-      const float hv = rbf(hres + rbf(o));
-      hres = lane < 16 ? hv : 0.f;
-      const float sq = lane < 16 ? hv * hv : 0.f;
-      // the 16 columns' sum of squares in column order, as the GEMV epilogue forms it
-      float s16 = 0.f;
-#pragma unroll
-      for (int i = 0; i < 16; ++i) s16 += __shfl(sq, i, 64);
-      hsq = s16;
-      const float hn = __shfl_down(hv, 1, 64);
-      if (lane < 16 && (lane & 1) == 0) st64(a.g_h[which] + c * 8 + lane / 2, gran(pack2(hv, hn), t));
-      if (lane == 0) st64(a.g_ss[which] + c, gran(__float_as_uint(s16), t));
-    };
+    // The layer loop, instantiated twice: with the attention inlined (the 16 attention CUs) and
+    // without it (the rest).  Each instance gets its own register allocation, so the attention's
+    // chunk state neither spills the plain CUs' loop nor costs a call: as a noinline callee its
+    // ~96 callee-saved VGPRs went to scratch and back every layer (98 KiB each way per CU, 2.8 us
+    // of prologue on the attention chain, profiles/r03_n_pse_trace_t2.txt).
+    auto run = [&](auto att_c) __attribute__((always_inline)) {
+      constexpr bool ATT = decltype(att_c)::value;
+      // residual columns 16c .. 16c+15 owned by this CU: lanes 0..15 of wave 1 (bf16 values)
+      float hres = (wave == LW && lane < 16) ? bf2f(a.h[c * 16 + lane]) : 0.f;
+      float hsq = 0.f;
+      int seq = 0;  // ring slot sequence number
+      // o / d: this lane's output row (wave 1, lanes < 16): hidden = residual + bf16(o)
+      // (TF/.../modeling_qwen3.py:311,322), published with its sum of squares
+      auto emit_h = [&](int which, uint32_t t, float o) {
+        if (wave != LW) return;
+        const float hv = rbf(hres + rbf(o));
+        hres = lane < 16 ? hv : 0.f;
+        const float sq = lane < 16 ? hv * hv : 0.f;
+        // the 16 columns' sum of squares in column order, as the GEMV epilogue forms it
+        float s16 = 0.f;
+  #pragma unroll
+        for (int i = 0; i < 16; ++i) s16 += __shfl(sq, i, 64);
+        hsq = s16;
+        const float hn = __shfl_down(hv, 1, 64);
+        if (lane < 16 && (lane & 1) == 0) st64(a.g_h[which] + c * 8 + lane / 2, gran(pack2(hv, hn), t));
+        if (lane == 0) st64(a.g_ss[which] + c, gran(__float_as_uint(s16), t));
+      };
 
-    for (int l = 0; l < a.layers && !failed(x); ++l) {
-      const PseLayer& Lw = a.L[l];
-      if (wave == LW) PSE_STAMP(l, 0);
-      // ---------------- q|k|v (input RMSNorm fused) ----------------
-      if (l == 0) {  // the embedding row and its sums of squares (previous launch)
-        for (int i = x.tid; i < H_ / 2; i += CW * 64) xs32[i] = reinterpret_cast<const uint32_t*>(a.h)[i];
-        for (int i = x.tid; i < NT; i += CW * 64) ssl[i] = a.ss[i];
-        cbar(x);
-      } else {
-        if (!gather<9>(x, a.g_h[1], H_ / 2 + NT, tagof(epoch, l - 1, OP_DOWN), xs32, H_ / 2,
-                       reinterpret_cast<uint32_t*>(ssl)))
-          break;
-      }
-      norm_stage(x, xs, ssl, NT, Lw.in_norm, H_);
-      if (wave == LW) PSE_STAMP(l, 1);
-      const uint32_t tq = tagof(epoch, l, OP_QKV);
-      #pragma unroll 1
-      for (int j = 0; j < 3; ++j) {
-        int tile, half;
-        pse_qkv_unit(c, j, &tile, &half);
-        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        #pragma unroll 1
-        for (int k = 0; k < 4; ++k) consume_slot(x, seq++, half * 64 + k * 16, acc);
-        PSE_PRIO_UP();
-        red_put(x, 0, acc);
-        cbar(x);
-        if (wave == LW && lane < 16)
-          st64(a.g_qkv + qkv_gran(tile) + half * 16 + lane, gran(__float_as_uint(red_get(x, 0, lane)), tq));
-        cbar(x);
-        PSE_PRIO_DOWN();
-      }
-      if (wave == LW) PSE_STAMP(l, 2);
-      // ---------------- attention (one CU per KV head) ----------------
-      if (att_u >= 0) {
-        // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
-        const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.err, a.trace,
-                                 a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
-        const bool att_ok = bg >= 0;
-        if (att_ok) x.bar_gen = bg;
-        if (PSE_APAUSE == 2 && x.tid == 0)  // (PSE_APAUSE 2: the loader waits out the whole attention)
-          __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (!att_ok) break;
-        if (wave == LW) PSE_STAMP(l, 3);
-      }
-      // ---------------- o_proj (+ residual) ----------------
-      if (!gather<8>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2)) break;
-      if (wave == LW) PSE_STAMP(l, 4);
-      {
-        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        #pragma unroll 1
-        for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, acc);
-        PSE_PRIO_UP();
-        red_put(x, 0, acc);
-        cbar(x);
-        emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f);
-        cbar(x);
-        PSE_PRIO_DOWN();
-      }
-      if (wave == LW) PSE_STAMP(l, 5);
-      // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
-      if (!gather<9>(x, a.g_h[0], H_ / 2 + NT, tagof(epoch, l, OP_O), xs32, H_ / 2, reinterpret_cast<uint32_t*>(ssl)))
-        break;
-      norm_stage(x, xs, ssl, NT, Lw.post_norm, H_);
-      if (wave == LW) PSE_STAMP(l, 6);
-      const uint32_t tg = tagof(epoch, l, OP_GU);
-      auto gu_round = [&](int j) {
-        f32x4 ag = (f32x4){0.f, 0.f, 0.f, 0.f}, au = ag;
-        #pragma unroll 1
-        for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, ag);
-        #pragma unroll 1
-        for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, au);
-        PSE_PRIO_UP();
-        red_put(x, 0, ag);
-        red_put(x, 1, au);
-        cbar(x);
-        if (wave == LW) {
-          // bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
-          const float gg = rbf(red_get(x, 0, lane & 15)), uu = rbf(red_get(x, 1, lane & 15));
-          const float o = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
-          const float on = __shfl_down(o, 1, 64);
-          if (lane < 16 && (lane & 1) == 0) st64(a.g_act + pse_gu_pair(c, j) * 8 + lane / 2, gran(pack2(o, on), tg));
+      for (int l = 0; l < a.layers && !failed(x); ++l) {
+        const PseLayer& Lw = a.L[l];
+        if (wave == LW) PSE_STAMP(l, 0);
+        // ---------------- q|k|v (input RMSNorm fused) ----------------
+        NormW nw;
+        auto load_nw = [&]() { nw = norm_w(x, Lw.in_norm); };
+        if (l == 0) {  // the embedding row and its sums of squares (previous launch)
+          load_nw();
+          for (int i = x.tid; i < H_ / 2; i += CW * 64) xs32[i] = reinterpret_cast<const uint32_t*>(a.h)[i];
+          for (int i = x.tid; i < NT; i += CW * 64) ssl[i] = a.ss[i];
+          cbar(x);
+        } else {
+  #if PSE_TRACE2
+          x.tp = a.trace ? a.trace + ((size_t)l * PSE_TRACE_EV + 10) * 256 + c : nullptr;  // events 10-14
+  #endif
+          const bool ok = gather<9>(x, a.g_h[1], H_ / 2 + NT, tagof(epoch, l - 1, OP_DOWN), xs32, H_ / 2,
+                                    reinterpret_cast<uint32_t*>(ssl), load_nw);
+  #if PSE_TRACE2
+          x.tp = nullptr;
+  #endif
+          if (!ok) break;
         }
-        cbar(x);
-        PSE_PRIO_DOWN();
-      };
-      gu_round(0);
-      gu_round(1);
-      // round 2 runs inside the gather of round 0's columns (published a round ago) -> xs
-      // k-tiles 128 .. 255 (the normed input in k-tiles 0 .. 127 is still being read)
-      auto gu2 = [&]() {
-        if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
-        gu_round(2);
-        if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
-      };
-      if (!gather<8>(x, a.g_act, I_ / 6, tg, xs32 + I_ / 6, I_ / 6, nullptr, gu2)) break;
-      if (wave == LW) PSE_STAMP(l, 7);
-      // ---------------- down (+ residual) ----------------
-      if (wave == LW) PSE_STAMP(l, 8);
-      {
-        // down's k-slots 8j .. 8j+7 read round j's columns: round 0 in xs k-tiles 128 .. 255,
-        // round 1 gathered into 256 .. 383 while round 0's slots run, round 2 into 0 .. 127 (the
-        // normed input is dead by then) while round 1's slots run
-        f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        auto slots = [&](int k0, int off) {
-          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+        norm_stage(x, xs, ssl, NT, nw);
+        if (wave == LW) PSE_STAMP(l, 1);
+        const uint32_t tq = tagof(epoch, l, OP_QKV);
+        #pragma unroll 1
+        for (int j = 0; j < 3; ++j) {
+          int tile, half;
+          pse_qkv_unit(c, j, &tile, &half);
+          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
           #pragma unroll 1
-          for (int k = k0; k < k0 + 8; ++k) consume_slot(x, seq++, k * 16 + off, acc);
+          for (int k = 0; k < 4; ++k) consume_slot(x, seq++, half * 64 + k * 16, acc);
+          PSE_PRIO_UP();
+          red_put(x, 0, acc);
+          cbar(x);
+          if (wave == LW && lane < 16)
+            st64(a.g_qkv + qkv_gran(tile) + half * 16 + lane, gran(__float_as_uint(red_get(x, 0, lane)), tq));
+          cbar(x);
+          PSE_PRIO_DOWN();
+        }
+        if (wave == LW) PSE_STAMP(l, 2);
+        // ---------------- attention (one CU per KV head) ----------------
+        if constexpr (ATT) {
+          // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
+          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.err, a.trace,
+                                   a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
+          const bool att_ok = bg >= 0;
+          if (att_ok) x.bar_gen = bg;
+          if (PSE_APAUSE == 2 && x.tid == 0)  // (PSE_APAUSE 2: the loader waits out the whole attention)
+            __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (!att_ok) break;
+          if (wave == LW) PSE_STAMP(l, 3);
+        }
+        // ---------------- o_proj (+ residual) ----------------
+        if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2)) break;
+        if (wave == LW) PSE_STAMP(l, 4);
+        {
+          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+          #pragma unroll 1
+          for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, acc);
+          PSE_PRIO_UP();
+          red_put(x, 0, acc);
+          cbar(x);
+          emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f);
+          cbar(x);
+          PSE_PRIO_DOWN();
+        }
+        if (wave == LW) PSE_STAMP(l, 5);
+        // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
+        if (!gather<9>(x, a.g_h[0], H_ / 2 + NT, tagof(epoch, l, OP_O), xs32, H_ / 2, reinterpret_cast<uint32_t*>(ssl),
+                       [&]() { nw = norm_w(x, Lw.post_norm); }))
+          break;
+        norm_stage(x, xs, ssl, NT, nw);
+        if (wave == LW) PSE_STAMP(l, 6);
+        const uint32_t tg = tagof(epoch, l, OP_GU);
+        auto gu_round = [&](int j) {
+          f32x4 ag = (f32x4){0.f, 0.f, 0.f, 0.f}, au = ag;
+          #pragma unroll 1
+          for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, ag);
+          #pragma unroll 1
+          for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, au);
+          PSE_PRIO_UP();
+          red_put(x, 0, ag);
+          red_put(x, 1, au);
+          cbar(x);
+          if (wave == LW) {
+            // bf16(bf16(silu(bf16 g)) * bf16 u)   (TF/.../modeling_qwen3.py:81-83)
+            const float gg = rbf(red_get(x, 0, lane & 15)), uu = rbf(red_get(x, 1, lane & 15));
+            const float o = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
+            const float on = __shfl_down(o, 1, 64);
+            if (lane < 16 && (lane & 1) == 0) st64(a.g_act + pse_gu_pair(c, j) * 8 + lane / 2, gran(pack2(o, on), tg));
+          }
+          cbar(x);
+          PSE_PRIO_DOWN();
+        };
+        gu_round(0);
+        gu_round(1);
+        // round 2 runs inside the gather of round 0's columns (published a round ago) -> xs
+        // k-tiles 128 .. 255 (the normed input in k-tiles 0 .. 127 is still being read)
+        auto gu2 = [&]() {
+          if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+          gu_round(2);
           if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
         };
-        if (!gather<8>(x, a.g_act + I_ / 6, I_ / 6, tg, xs32 + I_ / 3, I_ / 6, nullptr, [&]() { slots(0, 128); })) break;
-        if (!gather<8>(x, a.g_act + I_ / 3, I_ / 6, tg, xs32, I_ / 6, nullptr, [&]() { slots(8, 128); })) break;
-        #pragma unroll 1
-        for (int k = 16; k < 24; ++k) consume_slot(x, seq++, k * 16 - 256, acc);
-        PSE_PRIO_UP();
-        red_put(x, 0, acc);
-        cbar(x);
-        emit_h(1, tagof(epoch, l, OP_DOWN), lane < 16 ? red_get(x, 0, lane) : 0.f);
-        cbar(x);
-        PSE_PRIO_DOWN();
+        if (!gather<8, false>(x, a.g_act, I_ / 6, tg, xs32 + I_ / 6, I_ / 6, nullptr, gu2)) break;
+        if (wave == LW) PSE_STAMP(l, 7);
+        // ---------------- down (+ residual) ----------------
+        if (wave == LW) PSE_STAMP(l, 8);
+        {
+          // down's k-slots 8j .. 8j+7 read round j's columns: round 0 in xs k-tiles 128 .. 255,
+          // round 1 gathered into 256 .. 383 while round 0's slots run, round 2 into 0 .. 127 (the
+          // normed input is dead by then) while round 1's slots run
+          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+          auto slots = [&](int k0, int off) {
+            if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+            #pragma unroll 1
+            for (int k = k0; k < k0 + 8; ++k) consume_slot(x, seq++, k * 16 + off, acc);
+            if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
+          };
+          if (!gather<8, false>(x, a.g_act + I_ / 6, I_ / 6, tg, xs32 + I_ / 3, I_ / 6, nullptr, [&]() { slots(0, 128); })) break;
+          if (!gather<8, false>(x, a.g_act + I_ / 3, I_ / 6, tg, xs32, I_ / 6, nullptr, [&]() { slots(8, 128); })) break;
+          #pragma unroll 1
+          for (int k = 16; k < 24; ++k) consume_slot(x, seq++, k * 16 - 256, acc);
+          PSE_PRIO_UP();
+          red_put(x, 0, acc);
+          cbar(x);
+          emit_h(1, tagof(epoch, l, OP_DOWN), lane < 16 ? red_get(x, 0, lane) : 0.f);
+          cbar(x);
+          PSE_PRIO_DOWN();
+        }
+        if (wave == LW) PSE_STAMP(l, 9);
+        if (a.trace && wave == LW && lane < 5 && !PSE_TRACE2)
+          a.trace[((size_t)l * PSE_TRACE_EV + 10 + lane) * 256 + c] = ctl->lstamp[l & 1][lane];
       }
-      if (wave == LW) PSE_STAMP(l, 9);
-      if (a.trace && wave == LW && lane < 5)
-        a.trace[((size_t)l * PSE_TRACE_EV + 10 + lane) * 256 + c] = ctl->lstamp[l & 1][lane];
-    }
-    // the final residual and its sums of squares for the heads (plain stores: the next launch)
-    if (wave == LW && lane < 16) a.h[c * 16 + lane] = f2bf(hres);
-    if (wave == LW && lane == 0) a.ss[c] = hsq;
+      // the final residual and its sums of squares for the heads (plain stores: the next launch)
+      if (wave == LW && lane < 16) a.h[c * 16 + lane] = f2bf(hres);
+      if (wave == LW && lane == 0) a.ss[c] = hsq;
+    };
+    if (att_u >= 0) run(BoolC<true>{});
+    else run(BoolC<false>{});
   }
   // exit: the last workgroup out advances the epoch for the next launch
   __syncthreads();

@@ -54,12 +54,15 @@ e = build(True, layers)
 print(f"pse: decode forward {run(e, T, 8):.3f} ms ({layers} layers)")
 if os.environ.get("PSE_NO_TRACE") == "1":
     sys.exit(0)
-EV = 20
+EV = 28
 n = layers * EV * 256
 buf = (ctypes.c_uint64 * n)()
 N.check(N.load().mtts_pse_trace(e._h, buf, n), "trace")
 tr = np.frombuffer(buf, np.uint64).reshape(layers, EV, 256).astype(np.float64)
-t0 = tr[0, 10][tr[0, 10] > 0].min()
+T2 = os.environ.get("PSE_T2") == "1"  # a PSE_TRACE2 build: events 10-14 are the input-norm h gather's
+if T2:
+    NAMES[10:15] = ["G issued", "G polled", "G cbar", "G sweeps", "G first take"]
+t0 = tr[0, 0][tr[0, 0] > 0].min() if T2 else tr[0, 10][tr[0, 10] > 0].min()
 for l in list(range(min(layers, 4))) + [layers - 1]:
     row = []
     for ev in range(19):
@@ -94,6 +97,33 @@ for name, a0, a1 in att:
             d.append(np.median(v1[ok] - v0[ok]) / 100)
     if d:
         rows.append((name, float(np.median(d))))
+if T2:
+    # the input-norm h gather, per CU then the median over CUs and layers (us); 'after the last
+    # producer' = against the latest down-done stamp of the previous layer
+    def st(f):
+        return float(np.median([np.median(f(l)) for l in range(1, layers)]))
+    g = lambda l, ev: tr[l, ev] / 100
+    print("h gather (input norm), median over CUs and layers:")
+    print(f"  enter -> first sweep issued      {st(lambda l: g(l, 10) - g(l, 0)):.2f} us")
+    print(f"  first sweep issued -> taken       {st(lambda l: g(l, 14) - g(l, 10)):.2f} us")
+    print(f"  poll loop after the first sweep   {st(lambda l: g(l, 11) - g(l, 14)):.2f} us")
+    print(f"  sweeps                             {st(lambda l: tr[l, 13]):.1f}")
+    print(f"  consumer barrier                   {st(lambda l: g(l, 12) - g(l, 11)):.2f} us")
+    print(f"  norm (+ barrier)                   {st(lambda l: g(l, 1) - g(l, 12)):.2f} us")
+    print(f"  last producer's down done -> polled {st(lambda l: g(l, 11) - g(l - 1, 9).max()):.2f} us")
+    print(f"  last producer's down done -> normed {st(lambda l: g(l, 1) - g(l - 1, 9).max()):.2f} us")
+    print(f"  own down done -> gather enter      {st(lambda l: g(l, 0) - g(l - 1, 9)):.2f} us")
+    a = lambda l, e0, e1: [v for v in (tr[l, e1] - tr[l, e0]) / 100 if abs(v) < 1e4 and v != 0]
+    print("attention CUs (median):")
+    for nm, e0, e1 in (("chunks done -> k/v gathered", 17, 18), ("k/v norm, RoPE, append, partials + barrier", 18, 19),
+                       ("merge + publish + barrier + return", 19, 3)):
+        print(f"  {nm:44s} {st(lambda l: np.array(a(l, e0, e1) or [np.nan])):.2f} us")
+    for nm, e0, e1 in (("own q|k|v done -> attention entry", 2, 25), ("entry -> q sweep issued", 25, 20),
+                       ("q sweep issued -> taken", 20, 24), ("q poll loop", 24, 21), ("q barrier", 21, 22)):
+        print(f"  {nm:44s} {st(lambda l: np.array(a(l, e0, e1) or [np.nan])):.2f} us")
+    print(f"  last att done -> o input (median CU)    {st(lambda l: np.array([np.median(g(l, 4)) - g(l, 3)[tr[l, 3] > 0].max()])):.2f} us")
+    print(f"  last q|k|v done -> A q|k|v gathered     {st(lambda l: np.array([np.median(g(l, 15)[tr[l, 15] > 0]) - g(l, 2).max()])):.2f} us")
+    print(f"  spread of down done over CUs (max - median) {st(lambda l: np.array([g(l - 1, 9).max() - np.median(g(l - 1, 9))])):.2f} us")
 print("| phase (steady-state layer, median) | us |")
 print("|---|---|")
 for name, v in rows:
