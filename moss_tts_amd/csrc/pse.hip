@@ -68,6 +68,9 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
+#ifndef PSE_RC
+#define PSE_RC 6  // ring slots a plain CU's consumer waves drain into registers during the attention wait
+#endif
 #ifndef PSE_TRACE2
 #define PSE_TRACE2 0  // (diagnostic: the input-norm h gather's own stamps replace the loader's)
 #endif
@@ -226,7 +229,7 @@ __device__ __forceinline__ void cbar(Ctx& x) {
 
 // Gather n consecutive granules g[0..n) carrying tag t into LDS: the first n0 payloads to
 // dst0, the rest to dst1; all consumer threads cooperate (n <= MAXP * 256) in ONE sweep loop (one
-// round trip per poll); false on timeout / abort.  Branch-free sc1 buffer loads (an out-of-range
+// round trip per poll), calling each_poll() after every sweep's results are in; false on timeout / abort.  Branch-free sc1 buffer loads (an out-of-range
 // offset reads zero): a load under a divergent branch would be waited for at once.  SYNC: a
 // consumer barrier at the end, for data one wave gathers and another reads (the sums of squares,
 // the attention's rows); without it each wave goes on with the granules tid + 256 k it gathered
@@ -238,9 +241,10 @@ struct BoolC {
 struct NoHook {
   __device__ void operator()() const {}
 };
-template <int MAXP, bool SYNC = true, typename Hook = NoHook>
+template <int MAXP, bool SYNC = true, typename Hook = NoHook, typename Poll = NoHook>
 __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_t t, uint32_t* dst0, int n0,
-                                       uint32_t* dst1 = nullptr, const Hook& after_first_issue = Hook()) {
+                                       uint32_t* dst1 = nullptr, const Hook& after_first_issue = Hook(),
+                                       const Poll& each_poll = Poll()) {
   constexpr uint32_t OOB = 0x7ffffff0u;
   const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(g), 0, n * 8, 0x00020000);
   uint32_t pend = 0;  // bit i: granule tid + i * 256 not seen yet
@@ -282,6 +286,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   PSE_T2(10, __builtin_amdgcn_s_memrealtime());
   after_first_issue();
   take();
+  each_poll();
   PSE_T2(14, __builtin_amdgcn_s_memrealtime());
   uint32_t sweeps = 1;
   for (uint32_t spins = 1; __any(pend != 0); ++spins, ++sweeps) {
@@ -293,6 +298,7 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
     __builtin_amdgcn_s_sleep(PSE_POLL_SLEEP);
     issue();
     take();
+    each_poll();
   }
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(PSE_GPRIO == 2 ? 2 : 0);
   PSE_T2(11, __builtin_amdgcn_s_memrealtime());
@@ -406,6 +412,59 @@ __device__ __forceinline__ void consume_slot(Ctx& x, int seq, int kt0, f32x4& ac
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wt[i]), __builtin_bit_cast(bf16x8, xb[i]),
                                                   acc, 0, 0, 0);
 }
+
+// The ring slot drain (plain CUs, PSE_RC > 0): while a consumer wave waits for an op's input,
+// it copies the op's next ring slots (its 4 tiles of each) into registers as they land and
+// releases them, so the loader streams that many slots further ahead through the wait; the op
+// then runs those slots from the registers.  rc_drain_one: slot seq (if it has landed) -> t[]
+__device__ __forceinline__ bool slot_ready(int seq) {
+  return __hip_atomic_load(&PSE_CTL->full[seq % LW], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > seq / LW;
+}
+__device__ __forceinline__ void slot_take(Ctx& x, int seq, u32x4 (&t)[4]) {
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  const u32x4* sl = reinterpret_cast<const u32x4*>(pse_lds + L_RING + (seq % NS) * SLOT_KB * 1024);
+  const int w = x.wave - LW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) t[i] = sl[(w * 4 + i) * 64 + x.lane];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (x.lane == 0) __hip_atomic_store(&PSE_CTL->freed[w], seq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// acc += this wave's 4 tiles t[] (a drained slot) . x over k tiles kt0 + 4w ..
+__device__ __forceinline__ void slot_mfma(Ctx& x, const u32x4 (&t)[4], int kt0, f32x4& acc) {
+  const u32x4* xv = reinterpret_cast<const u32x4*>(pse_lds + L_XS);
+  const int w = x.wave - LW;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const u32x4 xb = xv[(kt0 + w * 4 + i) * 4 + (x.lane >> 4)];
+    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, t[i]), __builtin_bit_cast(bf16x8, xb), acc,
+                                                  0, 0, 0);
+  }
+}
+
+// RC ring slots drained into registers (slot_take) during an op's input gather, one per call of
+// drain() as they land; take(i, ..): the op's i-th slot from the registers (i < nd) or the ring.
+// One instance per op, scoped to it, so the registers are live only from the gather to the op.
+template <int RC>
+struct SlotCache {
+  u32x4 rc[RC > 0 ? RC : 1][4];
+  int nd = 0;
+  __device__ __forceinline__ void drain(Ctx& x, int seq) {
+#pragma unroll
+    for (int k = 0; k < RC; ++k)
+      if (k == nd && slot_ready(seq + k)) {
+        slot_take(x, seq + k, rc[k]);
+        ++nd;
+      }
+  }
+  __device__ __forceinline__ void take(Ctx& x, int& seq, int i, int kt0, f32x4& acc) {
+    if (i < RC && i < nd) {
+      slot_mfma(x, rc[i < RC ? i : 0], kt0, acc);
+      ++seq;
+    } else {
+      consume_slot(x, seq++, kt0, acc);
+    }
+  }
+};
 
 // fixed-order reduction of the CW waves' partial tiles (two tiles r = 0, 1 in flight): put,
 // consumer barrier, then get(r, row) = the tile's output row (MFMA D layout: lane l holds rows
@@ -553,6 +612,8 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   x.tp = nullptr;
 #endif
   if (w == 0) PSE_STAMP(l, 15);
+  if (PSE_APAUSE == 1 && x.tid == 0)  // (PSE_APAUSE 1: the loader resumes once the q rows are in)
+    __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   for (int i = x.tid; i < 16 * D; i += CW * 64)
     if (i / D >= HU) q_s[i] = 0;
   if (w < HU) {
@@ -904,6 +965,12 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         const PseLayer& Lw = a.L[l];
         if (wave == LW) PSE_STAMP(l, 0);
         // ---------------- q|k|v (input RMSNorm fused) ----------------
+        // Ring slot drain (plain CUs, SlotCache): while the consumer waves wait for the attention
+        // output they copy o_proj's first RC ring slots into registers as they land, which lets the
+        // loader run RC slots further ahead through the attention (the longest wait of the layer);
+        // o_proj then runs those slots from registers.  (At the h gathers the same drain spilled
+        // 44+ VGPRs even at 2 slots: not used there.)
+        constexpr int RC = ATT ? 0 : (PSE_RC < 8 ? PSE_RC : 8);
         NormW nw;
         auto load_nw = [&]() { nw = norm_w(x, Lw.in_norm); };
         if (l == 0) {  // the embedding row and its sums of squares (previous launch)
@@ -954,12 +1021,18 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
           if (wave == LW) PSE_STAMP(l, 3);
         }
         // ---------------- o_proj (+ residual) ----------------
-        if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2)) break;
+        // (plain CUs: the o_proj slots drain into registers while the attention runs elsewhere)
+        SlotCache<RC> co;
+        if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr, NoHook(),
+                              [&]() { co.drain(x, seq); }))
+          break;
         if (wave == LW) PSE_STAMP(l, 4);
         {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < RC; ++k) co.take(x, seq, k, k * 16, acc);
           #pragma unroll 1
-          for (int k = 0; k < 8; ++k) consume_slot(x, seq++, k * 16, acc);
+          for (int k = RC; k < 8; ++k) consume_slot(x, seq++, k * 16, acc);
           PSE_PRIO_UP();
           red_put(x, 0, acc);
           cbar(x);
