@@ -22,9 +22,10 @@
 // in a fixed order (deterministic).
 //
 // Work split per layer (CU c of P = 256): q|k|v = 768 half tiles (row tile, K half), 3 per CU
-// (q tile c whole, then one k|v half tile: pse_qkv_unit); o_proj and down = row tile c (CU c owns
-// residual columns 16c..16c+15 for the whole step); gate|up = pairs c, c + 256, c + 512
-// (pse_gu_pair).  92 slots (1.47 MB) per CU per layer.  The attention of KV head g runs on the
+// (q tile c whole, then one k|v half tile: pse_qkv_unit; an attention CU's k|v half goes to its
+// neighbour: pse_nq); o_proj and down = row tile c (CU c owns residual columns 16c..16c+15 for
+// the whole step); gate|up = pairs c, c + 256, c + 512 (pse_gu_pair).  92 slots (1.47 MB) per CU
+// per layer (88 on the attention CUs, 96 on their helpers).  The attention of KV head g runs on the
 // consumers of PSE_AU CUs (pse_att_unit: unit k takes q heads k G / PSE_AU .. over every key),
 // whose loaders pause while it runs (PSE_APAUSE).  The loader stages slots through registers
 // (PSE_RLOAD).  The engine takes this launch only for contexts up to its PSE range
@@ -79,7 +80,6 @@ constexpr int THREADS = (LW + CW) * 64;
 #endif
 constexpr int NS = PSE_NS;              // ring slots
 constexpr int SLOT_KB = 16;             // 1 KiB tiles per slot
-constexpr int SPL = 92;                 // slots per layer per CU
 constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
 enum { OP_QKV = 0, OP_ATT = 1, OP_O = 2, OP_GU = 3, OP_DOWN = 4 };
 
@@ -109,33 +109,36 @@ __device__ __forceinline__ void st32(void* p, uint32_t v) {
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
-// q|k|v unit j (0..2) of CU c: (row tile, K half) -- both halves of q row tile c, then half c & 1
-// of k|v row tile 256 + c / 2.  Every q tile is complete two thirds into the q|k|v stream, so the
-// attention units start on q while k / v are still being produced (round 3; units 3c .. 3c+2 in
-// (tile, half) order before: 2.824 -> 2.804 ms/step).
+// q|k|v unit j of CU c: (row tile, K half) -- both halves of q row tile c, then (j = 2) half c & 1
+// of k|v row tile 256 + c / 2, and (j = 3, the helper CUs of pse_nq) the k|v half tile of CU
+// c + 1.  Every q tile is complete two thirds into the q|k|v stream, so the attention units start
+// on q while k / v are still being produced (round 3; units 3c .. 3c+2 in (tile, half) order
+// before: 2.824 -> 2.804 ms/step).
 __device__ __forceinline__ void pse_qkv_unit(int c, int j, int* t, int* half) {
-  *t = j < 2 ? c : HQ_ * D_ / 16 + (c >> 1);
-  *half = j < 2 ? j : (c & 1);
+  const int o = j == 3 ? c + 1 : c;
+  *t = j < 2 ? c : HQ_ * D_ / 16 + (o >> 1);
+  *half = j < 2 ? j : (o & 1);
 }
 // gate|up pair of CU c in round j (3 pairs per CU): round j of every CU makes the SwiGLU columns
 // [4096 j, 4096 j + 4096), i.e. down_proj's k range of its slots 8j .. 8j+7, so every round's
 // hand-off flies while earlier rounds' work runs (the consumers below; round 3, pairs 3c .. 3c+2
 // before: 2.981 -> 2.842 ms/step)
 __device__ __forceinline__ int pse_gu_pair(int c, int j) { return c + 256 * j; }
-// slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles of CU c
-__device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, int c, int s) {
-  const int l = s / SPL, r = s - l * SPL;
-  if (r < 12) {  // q|k|v: unit r / 4 of CU c = (row tile, K half), 4 slots each
+// slot s's 16 KiB: (layer, op, unit, k range) -> 16 contiguous packed 1 KiB tiles of CU c, which
+// runs nq q|k|v units (pse_nq): 4 nq + 80 slots per layer
+__device__ __forceinline__ const bf16_t* pse_slot_src(const bf16_t* const* wp, int c, int nq, int s) {
+  const int spl = 4 * nq + 80, l = s / spl, r = s - l * spl, rq = 4 * nq;
+  if (r < rq) {  // q|k|v: unit r / 4 of CU c = (row tile, K half), 4 slots each
     int t, half;
     pse_qkv_unit(c, r / 4, &t, &half);
     return wp[l * 4 + 0] + ((size_t)t * 128 + half * 64 + (r % 4) * 16) * 512;
-  } else if (r < 20) {  // o_proj row tile c, 8 slots
-    return wp[l * 4 + 1] + ((size_t)c * 128 + (r - 12) * 16) * 512;
-  } else if (r < 68) {  // gate|up pairs (round j = 0..2: pair pse_gu_pair(c, j)): gate tile (8 slots), then up tile (8)
-    const int q = r - 20, pr = pse_gu_pair(c, q / 16), rt = 2 * pr + (q % 16) / 8;
+  } else if (r < rq + 8) {  // o_proj row tile c, 8 slots
+    return wp[l * 4 + 1] + ((size_t)c * 128 + (r - rq) * 16) * 512;
+  } else if (r < rq + 56) {  // gate|up pairs (round j = 0..2: pair pse_gu_pair(c, j)): gate tile (8 slots), then up tile (8)
+    const int q = r - rq - 8, pr = pse_gu_pair(c, q / 16), rt = 2 * pr + (q % 16) / 8;
     return wp[l * 4 + 2] + ((size_t)rt * 128 + (q % 8) * 16) * 512;
   }
-  return wp[l * 4 + 3] + ((size_t)c * 384 + (r - 68) * 16) * 512;  // down row tile c, 24 slots
+  return wp[l * 4 + 3] + ((size_t)c * 384 + (r - rq - 56) * 16) * 512;  // down row tile c, 24 slots
 }
 
 // LDS words shared by the loader and the consumers
@@ -182,6 +185,13 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 __host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
   return (d >= 0 && d % 7 == 0 && d / 7 < HKV_ * PSE_AU) ? d / 7 : -1;
+}
+// q|k|v units of CU c: an attention CU runs only its q tile (2 units) and hands its k|v half tile
+// to CU c - 1 (4 units): the attention needs k / v only after its cached-key chunks, so the
+// helper's later finish costs nothing, and the attention CU, whose loader pauses through the
+// attention, starts the layer's later ops 4 slots less behind the others.  3 units elsewhere.
+__host__ __device__ inline int pse_nq(int c, int P) {
+  return pse_att_unit(c, P) >= 0 ? 2 : (pse_att_unit(c + 1, P) >= 0 ? 4 : 3);
 }
 
 namespace {
@@ -787,12 +797,13 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
   }
   __syncthreads();
   const uint32_t epoch = (ld32(a.epoch) + 1u) & 0xffffffu;
-  const int total = a.layers * SPL;
+  const int nq = pse_nq(c, P), spl = 4 * nq + 80;  // this CU's q|k|v units, slots per layer
+  const int total = a.layers * spl;
 
   if (wave < LW) {
     // =================== loaders ===================
     if (PSE_LPRIO) __builtin_amdgcn_s_setprio(PSE_LPRIO);  // (A/B: the loader ahead of spinning consumers)
-    auto slot_src = [&](int s) { return pse_slot_src(wp, c, s); };
+    auto slot_src = [&](int s) { return pse_slot_src(wp, c, nq, s); };
     // Register-staged loader: each slot is loaded into one of 3 register buffers (16 x 16 B per
     // lane) and copied into its ring slot once that slot is free, so the 3 slots in flight do not
     // occupy ring slots (8 ready + 3 in flight, against 8 including the in-flight fills of the
@@ -809,9 +820,10 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     const uint32_t ring0 = (uint32_t)(uintptr_t)(lvoid*)(lds + L_RING) + voff;
     auto src_of = [&](int s0) -> const void* {
       const int s = min(s0, total - 1);
-      const int l = s / SPL, r = s - l * SPL;
+      const int l = s / spl, r = s - l * spl;
       if (a.trace && lane == 0 && s0 < total) {
-        const int ev = r == 0 ? 0 : (r == 12 ? 1 : (r == 20 ? 2 : (r == 68 ? 3 : (r == SPL - 1 ? 4 : -1))));
+        const int rq = 4 * nq;
+        const int ev = r == 0 ? 0 : (r == rq ? 1 : (r == rq + 8 ? 2 : (r == rq + 56 ? 3 : (r == spl - 1 ? 4 : -1))));
         if (ev >= 0) ctl->lstamp[l & 1][ev] = __builtin_amdgcn_s_memrealtime();
       }
       if (PSE_APAUSE && s0 < total)  // this CU's attention is gathering its inputs: no new loads
@@ -993,7 +1005,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         if (wave == LW) PSE_STAMP(l, 1);
         const uint32_t tq = tagof(epoch, l, OP_QKV);
         #pragma unroll 1
-        for (int j = 0; j < 3; ++j) {
+        for (int j = 0; j < (ATT ? 2 : nq); ++j) {
           int tile, half;
           pse_qkv_unit(c, j, &tile, &half);
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
