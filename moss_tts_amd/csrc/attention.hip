@@ -399,6 +399,7 @@ int attn_publish_max_splits() {
 }
 
 int attn_decode_splits(int Cmax) { return (Cmax + DEC_KW * decode_waves() - 1) / (DEC_KW * decode_waves()); }
+int attn_decode_keys_per_block_nwv(int nwv) { return DEC_KW * (nwv > 0 ? nwv : decode_waves()); }
 
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax) {
   const size_t cnt = ((size_t)B * Hkv * sizeof(int) + 255) / 256 * 256;
@@ -416,7 +417,9 @@ hipError_t attn_decode(const DecAttnArgs& a0, int B, hipStream_t s) {
   // the self-combining form (B > 16) takes 16 waves = 512 keys per block, which halves the
   // splits to merge (B=32: 5.31 vs 5.62 ms/step; B=1: 8 waves stay faster, 3.29 vs 3.37)
   a.nwv = (!a.publish_only && !getenv("MTTS_ATTN_NWV") && B > 16) ? 16 : decode_waves();
-  if (!a.publish_only && (a.nwv_force == 4 || a.nwv_force == 8 || a.nwv_force == 16)) a.nwv = a.nwv_force;
+  // a forced block size (the depth stack's 4 waves, batch-1 long contexts' 16): a publish-only
+  // caller gives its o_proj the same view (attn_decode_keys_per_block_nwv)
+  if (a.nwv_force == 4 || a.nwv_force == 8 || a.nwv_force == 16) a.nwv = a.nwv_force;
   a.ns = (a.Cmax + DEC_KW * a.nwv - 1) / (DEC_KW * a.nwv);
   static const int probe = getenv("MTTS_ATTN_PROBE") ? atoi(getenv("MTTS_ATTN_PROBE")) : 0;
   a.probe = probe;

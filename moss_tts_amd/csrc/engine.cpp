@@ -150,6 +150,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE")) e->pse = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE_CTX")) e->pse_ctx_max = atoi(v);
+  if (const char* v = getenv("MTTS_ATTN_LONG")) e->attn_long_ctx = atoi(v);
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
   if (const char* v = getenv("MTTS_NW")) sscanf(v, "%d,%d,%d,%d,%d", &e->nw[0], &e->nw[1], &e->nw[2], &e->nw[3], &e->nw[4]);
@@ -493,6 +494,8 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   }
   const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn &&
                          !st.attn_direct;
+  // batch-1 decode at long contexts (e->long_now): 16-wave (512-key) attention blocks
+  const int dec_nwv = st.attn_nwv ? st.attn_nwv : ((S == 1 && B == 1 && e->long_now && st.cos_t) ? 16 : 0);
   // 17-32 row decode: the GEMV inputs (xn, the attention output, the SwiGLU output) travel in
   // the fragment-packed layout, so each x fragment is one 1 KiB load (B=32 per layer: x loads
   // cost ~22 of 129 us row-major)
@@ -521,7 +524,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     da.publish_only = fuse_attn ? 1 : 0;
     da.po_max = attn_publish_max_splits();
     da.out_packed = xpk ? 1 : 0;
-    da.nwv_force = st.attn_nwv;
+    da.nwv_force = dec_nwv;
     da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
     HIPCHK(proj(e, g, EPI_STORE, s));
     if (S == 1) {
@@ -547,7 +550,8 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
     if (fuse_attn) {
       g.attn.part = st.part; g.attn.pos = pos_base; g.attn.Hkv = Hkv; g.attn.G = Hq / Hkv; g.attn.D = D;
-      g.attn.ns = attn_decode_splits(st.Cmax); g.attn.kb = attn_decode_keys_per_block();
+      g.attn.kb = attn_decode_keys_per_block_nwv(dec_nwv);
+      g.attn.ns = (st.Cmax + g.attn.kb - 1) / g.attn.kb;
       g.attn.po_max = attn_publish_max_splits();
     }
     HIPCHK(proj(e, g, EPI_RESADD, s));
@@ -686,6 +690,7 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   hipStream_t s = enter(e, stream);
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
   e->pse_choose(past + S);
+  e->long_now = e->attn_long_ctx > 0 && past + S > e->attn_long_ctx;
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
   if (!rc && S == 1 && B == 1 && e->pse && e->pse_ok && e->pse_now && e->pse_ws) {
     // A persistent streaming launch that gave up waiting (its workgroups were not all resident:
@@ -751,6 +756,7 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   HIPCHK(hipMemsetAsync(e->seen, 0, 2 * e->audio_rows, s));
   HIPCHK(gen_init(e->bufs(), ids, mask, s));
   e->pse_choose(T);  // (a prefill takes the launch only as a one-token prompt)
+  e->long_now = e->attn_long_ctx > 0 && T > e->attn_long_ctx;
   int rc = forward_chunked(e, ids, B, T, 0, e->logits, s);
   if (rc) return rc;
   HIPCHK(sample_step(e->bufs(), B, c.n_vq, TEXT_PARTS, s));
@@ -768,8 +774,8 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   // every step-dependent value is read from device state, so one graph serves all steps --
   // one per path: the persistent streaming launch (pse.hip) while the context stays in its
   // range, the per-op launches beyond (the choice is per step, from the host's step count)
-  auto graph_for = [&](bool pse, hipGraphExec_t* exec) -> int {
-    const int key = e->gen_B * 2 + (pse ? 1 : 0);
+  auto graph_for = [&](bool pse, bool lng, hipGraphExec_t* exec) -> int {
+    const int key = e->gen_B * 4 + (lng ? 2 : 0) + (pse ? 1 : 0);
     auto it = e->graphs.find(key);
     if (it != e->graphs.end() && it->second.forced == e->forced) {
       *exec = it->second.exec;
@@ -780,6 +786,7 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
       e->graphs.erase(it);
     }
     e->pse_now = pse;
+    e->long_now = lng;
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
     int rc = decode_step_launch(e, s);
@@ -793,9 +800,11 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   };
   for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
     // context of this step <= prompt + steps so far + 1
-    const bool pse = e->pse && e->pse_ok && e->gen_B == 1 && e->gen_T + e->steps_issued + 1 <= e->pse_ctx_max;
+    const int ctx = e->gen_T + e->steps_issued + 1;
+    const bool pse = e->pse && e->pse_ok && e->gen_B == 1 && ctx <= e->pse_ctx_max;
+    const bool lng = !pse && e->gen_B == 1 && e->attn_long_ctx > 0 && ctx > e->attn_long_ctx;
     hipGraphExec_t exec = nullptr;
-    if (int rc = graph_for(pse, &exec)) return rc;
+    if (int rc = graph_for(pse, lng, &exec)) return rc;
     HIPCHK(hipGraphLaunch(exec, s));
     ++e->steps_issued;
   }

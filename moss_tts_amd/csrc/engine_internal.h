@@ -100,6 +100,11 @@ struct mtts_engine {
                                  // the per-op split-K attention beyond ~850 cached keys
                                  // (scripts/pse_ctx_sweep.py, round 3: 0.97 at 700, 1.02 at 900)
   bool pse_now = false;          // this forward / captured decode step may take the PSE path
+  // batch-1 per-op decode past this context (TTSD long form): 16-wave decode attention blocks of
+  // 512 keys, half the splits to merge (MTTS_ATTN_LONG; 0: off).  TTSD shape, same box: 8 K keys
+  // 3.74 -> 3.59 ms/step, but 2 K keys 3.33 -> 3.49 (too few blocks), hence the switch
+  int attn_long_ctx = 4096;
+  bool long_now = false;         // this forward / captured decode step takes the long form
   void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
   bool pse_ok = false;           // the shape and the device support it
   int pse_timeouts = 0;          // launches that gave up waiting (each turns `pse` off)
@@ -116,7 +121,7 @@ struct mtts_engine {
   float* part_val = nullptr;
   const int* forced = nullptr;
   int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
-  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };  // key: 2 B + pse
+  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };  // key: 4 B + 2 long + pse
   std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
   std::vector<void*> allocs;      // weights
   std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)

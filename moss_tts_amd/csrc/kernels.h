@@ -234,6 +234,7 @@ hipError_t attention_prefill(const AttnArgs& a, hipStream_t s);
 hipError_t attn_decode(const DecAttnArgs& a, int B, hipStream_t s);
 int attn_decode_splits(int Cmax);
 int attn_decode_keys_per_block();
+int attn_decode_keys_per_block_nwv(int nwv);  // nwv 0: the default waves
 int attn_publish_max_splits();
 // workspace of attn_decode: ticket counters (zero-filled once by the owner) + partials
 size_t attn_decode_ws_bytes(int B, int Hq, int Hkv, int D, int Cmax);

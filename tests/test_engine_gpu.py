@@ -51,6 +51,21 @@ def gpu():
 @pytest.mark.parametrize("name,prefill_cap", [(n, 512) for n in CASES] + [("g_nvq16_bf16", 8), ("g_nvq4_b1_fp32", 8)])
 def test_generate_matches_oracle(gpu, golden, name, prefill_cap):
     """prefill_cap < prompt length exercises the position-chunked prefill (long-form path)."""
+    generate_vs_oracle(golden, name, prefill_cap)
+
+
+def test_generate_long_form_attention_graphs(gpu, golden):
+    """The batch-1 decode graphs past the long-context threshold (16-wave attention blocks;
+    MTTS_ATTN_LONG lowered to 8 so every decode step takes them) follow the oracle's greedy run."""
+    import os
+    os.environ["MTTS_ATTN_LONG"] = "8"
+    try:
+        generate_vs_oracle(golden, "g_nvq4_b1_fp32", 512)
+    finally:
+        os.environ.pop("MTTS_ATTN_LONG")
+
+
+def generate_vs_oracle(golden, name, prefill_cap):
     from moss_tts_amd.engine import sampling_params
     g, c, cfg, W = case(golden, name)
     ids, mask = g[name + "/input_ids"], g[name + "/mask"]
@@ -290,6 +305,46 @@ def test_packed_activations_long_prefill(gpu, golden, rows):
     scale = np.max(np.abs(np.where(fin, want, 0)), axis=-1, keepdims=True)
     tol = 8 * ulp_bf16(np.broadcast_to(scale, want.shape))
     assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), float(np.abs(got[fin] - want[fin]).max())
+
+
+@pytest.mark.parametrize("T", [1290, 2600])
+def test_long_context_16_wave_attention(gpu, golden, T):
+    """Batch-1 decode past the engine's long-context threshold (MTTS_ATTN_LONG, lowered to 1,000
+    here; TTSD's default 4,096) runs 16-wave (512-key) attention blocks: at 1,290 cached keys 3
+    blocks per KV head whose partials o_proj merges, at 2,600 6 that the attention merges itself.
+    Teacher-forced logits vs the oracle, a left-padded prompt."""
+    import os
+    name = "g_nvq4_bf16"
+    g, c, cfg, W = case(golden, name)
+    rng = np.random.default_rng(T)
+    steps = 4
+    ids = np.full((1, T + steps, cfg.n_vq + 1), cfg.audio_pad_code, np.int64)
+    ids[..., 0] = rng.integers(200, 20000, (1, T + steps))
+    ids[:, :, 1:] = rng.integers(0, 1024, (1, T + steps, cfg.n_vq))
+    mask = np.ones((1, T + steps), bool)
+    mask[0, :29] = False
+    ids[0, :29, 0] = cfg.pad_token_id
+    os.environ["MTTS_ATTN_LONG"] = "1000"
+    try:
+        eng = make_engine(cfg, W, max_batch=1, max_ctx=(T + steps + 63) // 64 * 64, max_prefill_tokens=4096)
+    finally:
+        os.environ.pop("MTTS_ATTN_LONG")
+    ctx = O._Ctx("bf16")
+    cache = O.KVCache(cfg.layers)
+    for s in range(steps + 1):
+        p0, p1 = (0, T) if s == 0 else (T + s - 1, T + s)
+        want = O.forward(ctx, W, cfg, ids[:, p0:p1], mask[:, :p1], cache, last_only=True)
+        lg = eng.forward(torch.from_numpy(ids[:, p0:p1].copy()), torch.from_numpy(mask[:, :p1].astype(np.uint8)), p0)
+        got = [x.float().cpu().numpy() for x in eng.split_logits(lg)]
+        for j in range(1, cfg.n_vq + 1):
+            w = want[j][:, -1]
+            fin = np.isfinite(w)
+            assert (np.isfinite(got[j]) == fin).all()
+            scale = np.max(np.abs(np.where(fin, w, 0)), axis=-1, keepdims=True)
+            tol = 8 * ulp_bf16(np.broadcast_to(scale, w.shape))
+            err = np.abs(got[j][fin] - w[fin])
+            assert (err <= tol[fin]).all(), (s, j, float(err.max()))
+    eng.close()
 
 
 def test_long_context_decode_logits(gpu, golden):
