@@ -13,7 +13,7 @@ idx = [i for i, r in enumerate(rows) if "embed_kernel" in r["Kernel_Name"]]
 # decode steps: consecutive embed launches with a single-token grid (prefill embeds are larger)
 steps = []
 for a, b in zip(idx, idx[1:]):
-    if b - a < int(sys.argv[2]) if len(sys.argv) > 2 else 20:
+    if b - a < (int(sys.argv[2]) if len(sys.argv) > 2 else 20):
         steps.append((a, b))
 steps = steps[5:-5]
 inter, intra, busy, big = [], [], [], []
