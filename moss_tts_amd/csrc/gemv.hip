@@ -146,6 +146,20 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
   else norm ? launch_nw<1, RT, EPI, PRO_NORM>(a, n_tiles, s) : launch_nw<1, RT, EPI, PRO_NONE>(a, n_tiles, s);
 }
 
+// Whether an o_proj of B rows x K reading decode-attention partials (EPI_RESADD, attn.part) would
+// load them before its first weight batch (PRO_ATTN_PRE / PRE2: at most two merged elements per
+// thread), mirroring launch_epi.  The generic PRO_ATTN form (loads behind the weight batch) is
+// slower than letting the attention write its rows: MossTTSLocal's B = 8 backbone step 8.52 ->
+// 8.43 ms/frame with the rows written (MTTS_UNFUSED_ATTN=1, profiles/r03_u_ab_local_attn.txt),
+// while Delay B = 4 (PRE2) keeps the merge in o_proj (3.33 vs 3.37 ms/step).
+bool gemv_attn_preload(int B, int K, int N, int force_nw) {
+  static const bool no_pre = getenv("MTTS_NO_PRELOAD") && atoi(getenv("MTTS_NO_PRELOAD"));
+  const int KT = K / 32, rows = (N + 15) / 16 * 16;
+  const int nw = (force_nw == 4 || force_nw == 8 || force_nw == 16) ? force_nw
+                                                                      : (KT < 64 ? 4 : ((rows >= 8192 || KT < 128) ? 8 : 16));
+  return !no_pre && (size_t)B * K / 8 <= (size_t)2 * nw * 64;
+}
+
 hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   if (a0.K % 32 != 0 || a0.B <= 0 || a0.N <= 0) return hipErrorInvalidValue;
   // the packed layout holds 32 token slots and is read by the 2-half (NB = 2) body only

@@ -211,6 +211,8 @@ hipError_t gemv(const bf16_t* wpacked, const bf16_t* x, int ldx, bf16_t* y, int 
 constexpr size_t NORM_LDS_MAX = 48 * 1024;
 size_t norm_lds_bytes(int B, int K);
 hipError_t gemv_ex(const GemvArgs& a, int epi, hipStream_t s);
+// an o_proj (EPI_RESADD) of B rows x K over N outputs would preload decode-attention partials
+bool gemv_attn_preload(int B, int K, int N, int force_nw);
 // gemm.hip: prefill form of gemv_ex (B = tokens, any count; EPI_STORE / RESADD / SWIGLU;
 // no fused norm prologue, no gate)
 hipError_t gemm_ex(const GemvArgs& a, int epi, hipStream_t s);
