@@ -492,10 +492,12 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     HIPCHK(pse_decode(pa, e->pse_ws, s));
     return 0;
   }
-  // small decode batches: o_proj merges the attention's split partials in its prologue -- when it
-  // can preload them (gemv_attn_preload); otherwise the attention writes its rows
+  // decode: o_proj merges the attention's split partials in its prologue when it preloads one
+  // merged element per thread (gemv_attn_preload: batch 1-2 at K 4096) and the context is short
+  // (the long-context graphs' attention merges its many splits itself); otherwise the attention
+  // writes its rows and o_proj is a plain GEMV
   const bool fuse_attn = S == 1 && M <= 16 && (size_t)M * Hq * D * 2 <= NORM_LDS_MAX && !e->unfused_attn &&
-                         !st.attn_direct && gemv_attn_preload(M, Hq * D, H, e->nw[1]);
+                         !st.attn_direct && !e->long_now && gemv_attn_preload(M, Hq * D, H, e->nw[1]);
   // batch-1 decode at long contexts (e->long_now): 16-wave (512-key) attention blocks
   const int dec_nwv = st.attn_nwv ? st.attn_nwv : ((S == 1 && B == 1 && e->long_now && st.cos_t) ? 16 : 0);
   // 17-32 row decode: the GEMV inputs (xn, the attention output, the SwiGLU output) travel in

@@ -147,17 +147,17 @@ static void launch_epi(const GemvArgs& a, int n_tiles, hipStream_t s) {
 }
 
 // Whether an o_proj of B rows x K reading decode-attention partials (EPI_RESADD, attn.part) would
-// load them before its first weight batch (PRO_ATTN_PRE / PRE2: at most two merged elements per
-// thread), mirroring launch_epi.  The generic PRO_ATTN form (loads behind the weight batch) is
-// slower than letting the attention write its rows: MossTTSLocal's B = 8 backbone step 8.52 ->
-// 8.43 ms/frame with the rows written (MTTS_UNFUSED_ATTN=1, profiles/r03_u_ab_local_attn.txt),
-// while Delay B = 4 (PRE2) keeps the merge in o_proj (3.33 vs 3.37 ms/step).
+// load them before its first weight batch with ONE merged element per thread (PRO_ATTN_PRE),
+// mirroring launch_epi.  Only then does the merge in o_proj beat letting the attention write its
+// rows (same box, profiles/r03_u_ab_local_attn.txt): batch-1 per-op decode 3.191 (merge in o_proj)
+// vs 3.223 ms/step; but Delay B = 4 (two elements per thread, PRE2) 3.325 vs 3.262 and
+// MossTTSLocal's B = 8 backbone (four, generic PRO_ATTN) 8.52 vs 8.37 ms/frame with the rows written.
 bool gemv_attn_preload(int B, int K, int N, int force_nw) {
   static const bool no_pre = getenv("MTTS_NO_PRELOAD") && atoi(getenv("MTTS_NO_PRELOAD"));
   const int KT = K / 32, rows = (N + 15) / 16 * 16;
   const int nw = (force_nw == 4 || force_nw == 8 || force_nw == 16) ? force_nw
                                                                       : (KT < 64 ? 4 : ((rows >= 8192 || KT < 128) ? 8 : 16));
-  return !no_pre && (size_t)B * K / 8 <= (size_t)2 * nw * 64;
+  return !no_pre && (size_t)B * K / 8 <= (size_t)nw * 64;
 }
 
 hipError_t gemv_ex(const GemvArgs& a0, int epi, hipStream_t s) {
