@@ -34,6 +34,10 @@ extern "C" {
 
 typedef struct mtts_engine mtts_engine;
 
+/* longest context (prompt + max_new_tokens) an engine reserves: 2.9 hours of 12.5 Hz frames, past
+ * the 60-minute single session of the TTSD model card (docs/moss_ttsd_model_card.md:21) */
+#define MTTS_MAX_CTX 131072
+
 /* Model + capacity configuration.  Model fields restate MossTTSDelayConfig
  * (moss_tts_delay/configuration_moss_tts.py:62-103) and the nested Qwen3Config. */
 typedef struct mtts_config {
@@ -82,6 +86,11 @@ int mtts_engine_reserve(mtts_engine* eng, int max_batch, int max_ctx, int max_pr
  * reference shape, on the host (src_on_device = 0) or the device (1).  The engine
  * repacks matrices into its MFMA-tile layout. */
 int mtts_engine_load_weight(mtts_engine* eng, const char* name, const void* src, size_t bytes, int src_on_device);
+/* The same, ordered after `stream` (a device source may still be being written there): the
+ * repack runs on the engine stream behind an event of `stream`, and `stream`'s later work waits
+ * for it -- no device-wide sync.  mtts_engine_load_weight = this with the legacy default stream. */
+int mtts_engine_load_weight_stream(mtts_engine* eng, const char* name, const void* src, size_t bytes,
+                                   int src_on_device, void* stream);
 /* Fill every weight with the portable splitmix64 init of oracle/prng.py (benchmarks). */
 int mtts_engine_init_random(mtts_engine* eng, uint64_t seed);
 /* Total bytes of weights streamed per decode step (for roofline accounting). */
@@ -115,9 +124,23 @@ int mtts_pse_ctx_max(const mtts_engine* eng);
  * The next check (a teacher-forced batch-1 forward, or mtts_generate_poll) takes the fallback:
  * the launch is turned off for this engine and the work re-runs on the per-op launches. */
 int mtts_pse_inject_timeout(mtts_engine* eng);
+/* A batch-1 mtts_forward through the persistent launch does not synchronise: its error word is
+ * copied asynchronously and checked lazily -- without blocking at the next mtts_forward /
+ * mtts_generate_begin, blocking here.  MTTS_E_PSE_TIMEOUT (reported once): a launch timed out, the
+ * logits of the forwards since the last clean check are invalid, and the engine now runs the
+ * per-op launches (recompute those forwards).  Also reads the word of forwards the caller
+ * captured into its own graph.  0: every forward so far is valid. */
+int mtts_pse_check(mtts_engine* eng);
 /* per-layer event stamps (s_memrealtime, 100 MHz) of the last persistent streaming launch:
  * [layers][20][256 workgroups] (engine created with MTTS_PSE_TRACE=1; see pse.hip) */
 int mtts_pse_trace(mtts_engine* eng, uint64_t* host, size_t n);
+
+/* test hooks: write bf16 K / V rows [n_kv][n][head_dim] (host) at positions pos0.. of batch row
+ * b, layer `layer` (the cache of a long context without prefilling it); fill the whole KV cache
+ * with one bf16 bit pattern (e.g. NaN: rows never written must never reach a result) */
+int mtts_engine_kv_write(mtts_engine* eng, int layer, int b, int pos0, int n, const uint16_t* k_host,
+                         const uint16_t* v_host);
+int mtts_engine_kv_fill(mtts_engine* eng, uint16_t bits);
 
 /* ---- generate (MossTTSDelayModel.generate, modeling_moss_tts.py:392-525) ----
  * begin: state init + prefill + the step-0 sampling.  decode: n more steps (hipGraph).
@@ -151,8 +174,8 @@ int mtts_generate_logits(mtts_engine* eng, uint16_t* out_dev, void* stream);
  * speech_embedding_to_local_mlp.*, local_to_speech_embedding_mlps.{i}.*,
  * layer_norm_before_lm_heads.{i}, lm_heads.{i}).  Poll and fetch are mtts_generate_poll /
  * mtts_generate_fetch.  n_vq_for_inference < 0: all channels.
- * Replaces CustomMixin._sample (moss_tts_local/modeling_moss_tts.py:315-477), greedy
- * (do_samples all False); a positive temperature is rejected with MTTS_E_UNSUPPORTED. */
+ * Replaces CustomMixin._sample (moss_tts_local/modeling_moss_tts.py:315-477): greedy channels
+ * (temperature <= 0) or the HF processor chain with any top_k (<= 0: none), top_p, penalty. */
 int mtts_local_generate_begin(mtts_engine* eng, const int64_t* input_ids_dev, const uint8_t* attention_mask_dev, int B,
                               int T, int max_new_tokens, int n_vq_for_inference, const mtts_sampling* sampling,
                               void* stream);

@@ -78,6 +78,10 @@ _SIGS = {
     "mtts_pse_active": (I, [P]),
     "mtts_pse_ctx_max": (I, [P]),
     "mtts_pse_inject_timeout": (I, [P]),
+    "mtts_pse_check": (I, [P]),
+    "mtts_engine_load_weight_stream": (I, [P, ctypes.c_char_p, P, SZ, I, P]),
+    "mtts_engine_kv_write": (I, [P, I, I, I, I, P, P]),
+    "mtts_engine_kv_fill": (I, [P, ctypes.c_uint16]),
     "mtts_pse_trace": (I, [P, ctypes.POINTER(U64), ctypes.c_size_t]),
     "mtts_generate_begin": (I, [P, P, P, I, I, I, ctypes.POINTER(MttsSampling), P, P]),
     "mtts_generate_decode": (I, [P, I, P]),
@@ -150,12 +154,19 @@ def load():
     return lib
 
 
+class PseTimeout(RuntimeError):
+    """MTTS_E_PSE_TIMEOUT: a batch-1 persistent decode launch timed out; the logits of the
+    forwards since the last check are invalid and the engine now runs the per-op launches."""
+
+
 def check(rc, what=""):
     if rc == MTTS_OK:
         return
     msg = load().mtts_last_error().decode(errors="replace")
     if rc == MTTS_E_INVALID:
         raise ValueError(f"{what}: {msg}")
+    if rc == MTTS_E_PSE_TIMEOUT:
+        raise PseTimeout(f"{what} failed ({rc}): {msg}")
     raise RuntimeError(f"{what} failed ({rc}): {msg}")
 
 

@@ -411,7 +411,6 @@ hipError_t attn_decode(const DecAttnArgs& a0, int B, hipStream_t s) {
   if (a0.Hq % a0.Hkv) return hipErrorInvalidValue;
   if (a0.Cmax % 64) return hipErrorInvalidValue;  // 16-byte V^T fragments, whole 16-key mask words
   if (!a0.part || !a0.cnt) return hipErrorInvalidValue;
-  if (attn_decode_splits(a0.Cmax) > DEC_MAXS) return hipErrorInvalidValue;
   DecAttnArgs a = a0;
   // publish-only blocks must match the o_proj prologue's view (attn_decode_keys_per_block);
   // the self-combining form (B > 16) takes 16 waves = 512 keys per block, which halves the
@@ -421,6 +420,7 @@ hipError_t attn_decode(const DecAttnArgs& a0, int B, hipStream_t s) {
   // caller gives its o_proj the same view (attn_decode_keys_per_block_nwv)
   if (a.nwv_force == 4 || a.nwv_force == 8 || a.nwv_force == 16) a.nwv = a.nwv_force;
   a.ns = (a.Cmax + DEC_KW * a.nwv - 1) / (DEC_KW * a.nwv);
+  if (a.ns > DEC_MAXS) return hipErrorInvalidValue;  // the last arriver's (m, l) table
   static const int probe = getenv("MTTS_ATTN_PROBE") ? atoi(getenv("MTTS_ATTN_PROBE")) : 0;
   a.probe = probe;
   switch (a.D) {

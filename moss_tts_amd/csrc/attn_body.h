@@ -21,7 +21,7 @@
 namespace mtts {
 
 constexpr int DEC_KW = 32;      // keys per wave
-constexpr int DEC_MAXS = 256;  // splits per head
+constexpr int DEC_MAXS = 512;  // splits per head (MTTS_MAX_CTX at 256-key blocks)
 
 template <int G, int D, int NWV>
 __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int sp, const int kvh, const int b) {

@@ -218,17 +218,19 @@ extern "C" int mtts_codec_load_weight(mtts_codec* k, const char* name, const voi
     const int DL = c.stages[c.n_stages - 1].hidden;
     if (bytes != (size_t)c.patch * DL * 2) return fail(MTTS_E_INVALID, "size mismatch for " + n);
     const bf16_t* from = reinterpret_cast<const bf16_t*>(src);
-    if (on_dev) HIPCHK(hipDeviceSynchronize());  // the source may be in flight on the caller's stream
+    // the source may be in flight on the caller's (legacy default) stream: event-ordered, as store_weight
+    hipStream_t ws = enter(&k->W, nullptr);
     if (!on_dev) {
       if (int rc = ensure_staging(&k->W, bytes)) return rc;
-      HIPCHK(hipMemcpyAsync(k->W.staging, src, bytes, hipMemcpyHostToDevice, k->W.stream));
+      HIPCHK(hipMemcpyAsync(k->W.staging, src, bytes, hipMemcpyHostToDevice, ws));
       from = k->W.staging;
     }
     const size_t tot = (size_t)c.patch * DL;
-    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, k->W.stream, from,
+    hipLaunchKernelGGL(transpose_bf16_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, ws, from,
                        k->outw, c.patch, DL);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipStreamSynchronize(k->W.stream));
+    if (!on_dev) HIPCHK(hipStreamSynchronize(ws));
+    leave(&k->W, nullptr);
     return 0;
   } else if (n.rfind(ps, 0) == 0) {
     size_t e;

@@ -53,6 +53,8 @@ extern "C" int mtts_engine_destroy(mtts_engine* e) {
   for (void* p : e->cap_allocs) hipFree(p);
   if (e->staging) hipFree(e->staging);
   if (e->ev_in) hipEventDestroy(e->ev_in);
+  if (e->ev_pse) hipEventDestroy(e->ev_pse);
+  if (e->pse_err_host) hipHostFree(e->pse_err_host);
   if (e->ev_out) hipEventDestroy(e->ev_out);
   if (e->stream) hipStreamDestroy(e->stream);
   delete e;
@@ -85,7 +87,10 @@ static int alloc_capacity(mtts_engine* e) {
     return rc;
   const size_t ns_dec = (c.max_ctx + CH_DECODE - 1) / CH_DECODE;
   const size_t ns_pf = (c.max_ctx + CH_PREFILL - 1) / CH_PREFILL;
-  e->part_floats = std::max((size_t)c.max_batch * ns_dec, M * ns_pf) * Hq * (D + 2);
+  // decode-attention split partials; the per-token split-K prefill attention (MTTS_OLD_PREFILL_ATTN,
+  // A/B only) also keeps M x ns_pf of them -- 17 GB at an 8,192-token chunk and 32 K context,
+  // which the flash prefill attention does not need
+  e->part_floats = std::max((size_t)c.max_batch * ns_dec, e->old_prefill_attn ? M * ns_pf : 0) * Hq * (D + 2);
   if ((rc = e->alloc(&e->part, e->part_floats))) return rc;
   if ((rc = e->alloc(&e->logits, (size_t)c.max_batch * e->heads_ld))) return rc;
   if ((rc = e->alloc(&e->d_pos, 4))) return rc;
@@ -126,7 +131,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (!cfg || !out) return fail(MTTS_E_INVALID, "null argument");
   const mtts_config& c = *cfg;
   if (c.hidden % 32 || c.inter % 32 || c.head_dim % 8 || c.head_dim > 128 || c.n_heads % c.n_kv ||
-      (c.n_heads * c.head_dim) % 32 || c.max_batch <= 0 || c.max_batch > 256 || c.max_ctx <= 0 || c.max_ctx > 32768 || c.n_vq < 1)
+      (c.n_heads * c.head_dim) % 32 || c.max_batch <= 0 || c.max_batch > 256 || c.max_ctx <= 0 || c.max_ctx > MTTS_MAX_CTX || c.n_vq < 1)
     return fail(MTTS_E_UNSUPPORTED, "unsupported model shape");
   const int G = c.n_heads / c.n_kv;
   if (G != 1 && G != 2 && G != 4 && G != 8) return fail(MTTS_E_UNSUPPORTED, "GQA group must be 1/2/4/8");
@@ -150,6 +155,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_OLD_PREFILL_ATTN")) e->old_prefill_attn = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE")) e->pse = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE_CTX")) e->pse_ctx_max = atoi(v);
+  if (const char* v = getenv("MTTS_PSE_COOP")) e->pse_coop = v[0] == '1';
   if (const char* v = getenv("MTTS_ATTN_LONG")) e->attn_long_ctx = atoi(v);
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
@@ -162,6 +168,9 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking) != hipSuccess) return bail(fail(MTTS_E_HIP, "stream"));
   hipEventCreateWithFlags(&e->ev_in, hipEventDisableTiming);
   hipEventCreateWithFlags(&e->ev_out, hipEventDisableTiming);
+  hipEventCreateWithFlags(&e->ev_pse, hipEventDisableTiming);
+  if (hipHostMalloc((void**)&e->pse_err_host, 4, hipHostMallocDefault) != hipSuccess) return bail(fail(MTTS_E_OOM, "pinned word"));
+  *e->pse_err_host = 0;
   const int H = c.hidden, D = c.head_dim, Hq = c.n_heads, Hkv = c.n_kv, I = c.inter;
   e->qkv_rows = (Hq + 2 * Hkv) * D;
   e->audio_rows = c.audio_vocab + 1;
@@ -203,7 +212,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
 }
 
 extern "C" int mtts_engine_reserve(mtts_engine* e, int max_batch, int max_ctx, int max_prefill_tokens) {
-  if (!e || max_batch <= 0 || max_batch > 256 || max_ctx <= 0 || max_ctx > 32768) return fail(MTTS_E_INVALID, "bad capacity");
+  if (!e || max_batch <= 0 || max_batch > 256 || max_ctx <= 0 || max_ctx > MTTS_MAX_CTX) return fail(MTTS_E_INVALID, "bad capacity");
   hipSetDevice(e->device);
   HIPCHK(hipStreamSynchronize(e->stream));
   for (auto& kv : e->graphs) hipGraphExecDestroy(kv.second.exec);
@@ -296,12 +305,12 @@ bool layer_target(const LayerW& w, const std::string& rest, int H, int I, int Hq
 }
 
 int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void* src, size_t bytes, int on_dev) {
-  hipStream_t s = e->stream;
   if (bytes != t.expect * 2) return fail(MTTS_E_INVALID, std::string("size mismatch for ") + name);
-  // a device source may still be in flight on another stream of the caller (e.g. a torch tensor
-  // just produced on torch's stream): the engine stream does not order after it, so wait for the
-  // whole device once per load (one-time cost)
-  if (on_dev) HIPCHK(hipDeviceSynchronize());
+  // a device source may still be in flight on the caller's stream (e.g. a torch tensor just
+  // produced there): the engine stream orders after that stream by an event (enter), and the
+  // caller's later work -- e.g. freeing the source -- after the repack (leave).  No device-wide
+  // sync per tensor (a state_dict is ~400 of them; a device sync also stalls other streams).
+  hipStream_t s = enter(e, e->load_stream);
   if (!t.pack) {
     HIPCHK(hipMemcpyAsync(t.dst, src, bytes, on_dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
   } else {
@@ -314,12 +323,25 @@ int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void*
     }
     HIPCHK(pack_weight(from, t.dst, t.rows, t.K, t.row_off, t.inter, t.which, s));
   }
-  HIPCHK(hipStreamSynchronize(s));
+  // a host source must stay untouched until its copy has landed: wait for those only
+  if (!on_dev) HIPCHK(hipStreamSynchronize(s));
+  leave(e, e->load_stream);
   return 0;
 }
 
-extern "C" int mtts_engine_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev) {
+extern "C" int mtts_engine_load_weight_stream(mtts_engine* e, const char* name, const void* src, size_t bytes,
+                                              int on_dev, void* stream) {
   if (!e || !name || !src) return fail(MTTS_E_INVALID, "null argument");
+  e->load_stream = stream;
+  const int rc = load_weight_impl(e, name, src, bytes, on_dev);
+  e->load_stream = nullptr;
+  return rc;
+}
+// the legacy default stream orders the source (what torch's default stream is)
+extern "C" int mtts_engine_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev) {
+  return mtts_engine_load_weight_stream(e, name, src, bytes, on_dev, nullptr);
+}
+int load_weight_impl(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev) {
   hipSetDevice(e->device);
   if (e->lp) {  // MossTTSLocal names (model.embedding_list.*, local_transformer.*, ...)
     int rc = 0;
@@ -489,7 +511,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     pa.trace = e->pse_trace;
     static const int pse_probe = getenv("MTTS_PSE_PROBE") ? atoi(getenv("MTTS_PSE_PROBE")) : 0;
     pa.probe = pse_probe;
-    HIPCHK(pse_decode(pa, e->pse_ws, s));
+    HIPCHK(pse_decode(pa, e->pse_ws, s, e->pse_coop));
     return 0;
   }
   // decode: o_proj merges the attention's split partials in its prologue when it preloads one
@@ -685,33 +707,106 @@ bool pse_tripped(mtts_engine* e, hipStream_t s) {
   return true;
 }
 
+// A teacher-forced forward through the persistent launch leaves its error word on the way to
+// pinned host memory (an async copy + event): no host sync per step, legal under a caller's
+// stream capture.  The word is checked lazily: without blocking at the start of the next forward
+// / generation (pse_lazy_check(e, false)), blocking in mtts_pse_check.  A tripped launch (a wait
+// timed out: its workgroups were not all resident, other work on the device) turns the launch
+// off for this engine and is reported ONCE as MTTS_E_PSE_TIMEOUT: the logits of the forwards
+// since the last clean check are invalid and must be recomputed (the forward is idempotent: it
+// rewrites the KV rows at past..), which the per-op launches then do.
+static void pse_trip(mtts_engine* e, uint32_t err) {
+  hipMemsetAsync(pse_err_word(e->pse_ws), 0, 4, e->stream);
+  e->pse = false;
+  e->pse_timeouts += 1;
+  fprintf(stderr, "libmtts: persistent streaming decode timed out (code %u; device shared with other work?); "
+                  "this engine continues on the per-op launches\n", err);
+}
+static int pse_lazy_check(mtts_engine* e, bool block) {
+  if (!e->pse_pending) return 0;
+  if (block) {
+    HIPCHK(hipEventSynchronize(e->ev_pse));
+  } else if (hipEventQuery(e->ev_pse) != hipSuccess) {
+    return 0;  // not landed yet: a later call reports it
+  }
+  e->pse_pending = false;
+  const uint32_t err = *(volatile uint32_t*)e->pse_err_host;
+  if (!err) return 0;
+  pse_trip(e, err);
+  return fail(MTTS_E_PSE_TIMEOUT, "persistent streaming decode: a wait timed out; the logits of the forwards since "
+                                  "the last check are invalid (recompute them: the engine now runs the per-op launches)");
+}
+
+extern "C" int mtts_pse_check(mtts_engine* e) {
+  if (!e) return fail(MTTS_E_INVALID, "null engine");
+  hipSetDevice(e->device);
+  if (int rc = pse_lazy_check(e, true)) return rc;
+  // forwards the caller captured into its own graph: read the word itself
+  if (e->pse_ws && pse_tripped(e, e->stream))
+    return fail(MTTS_E_PSE_TIMEOUT, "persistent streaming decode: a wait timed out (results since the last check "
+                                    "are invalid; the engine now runs the per-op launches)");
+  return 0;
+}
+
 extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
                             uint16_t* logits, void* stream) {
   if (!e || !ids || !mask || !logits) return fail(MTTS_E_INVALID, "null argument");
   if (e->lp) return fail(MTTS_E_UNSUPPORTED, "MossTTSLocal engine: use mtts_local_forward");
   const mtts_config& c = e->c;
   if (B <= 0 || B > c.max_batch || S <= 0 || past < 0 || past + S > c.max_ctx) return fail(MTTS_E_INVALID, "bad B/S/past");
+  hipSetDevice(e->device);
+  if (int rc = pse_lazy_check(e, false)) return rc;
   hipStream_t s = enter(e, stream);
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
   e->pse_choose(past + S);
   e->long_now = e->attn_long_ctx > 0 && past + S > e->attn_long_ctx;
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
   if (!rc && S == 1 && B == 1 && e->pse && e->pse_ok && e->pse_now && e->pse_ws) {
-    // A persistent streaming launch that gave up waiting (its workgroups were not all resident:
-    // other work on the device) leaves invalid logits.  Outside a stream capture the step is
-    // checked here and, on a timeout, re-run on the per-op launches, which every later step of
-    // this engine then takes (the forward is idempotent: it rewrites the KV rows at past..).
-    // Inside a caller's capture nothing may synchronise: the check is left to the caller
-    // (mtts_generate_poll reads the same word).
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cs));
-    if (cs == hipStreamCaptureStatusNone && pse_tripped(e, s)) {
-      e->pse_now = false;
-      rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
+    if (cs == hipStreamCaptureStatusNone) {  // (inside a caller's capture: mtts_pse_check reads the word)
+      HIPCHK(hipMemcpyAsync(e->pse_err_host, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipEventRecord(e->ev_pse, s));
+      e->pse_pending = true;
     }
   }
   leave(e, stream);
   return rc;
+}
+
+// ---------------------------------------------------------------------------
+// test hooks: write K / V rows of the cache directly (host bf16 k, v [Hkv][n][D] at positions
+// pos0 .. pos0 + n - 1 of row b, layer l; V is stored transposed), or fill the whole cache with
+// one bf16 pattern (e.g. NaN: rows never written must never reach a result)
+extern "C" int mtts_engine_kv_write(mtts_engine* e, int layer, int b, int pos0, int n, const uint16_t* k,
+                                    const uint16_t* v) {
+  if (!e || !k || !v) return fail(MTTS_E_INVALID, "null argument");
+  const mtts_config& c = e->c;
+  if (e->lp || layer < 0 || layer >= c.layers || b < 0 || b >= c.max_batch || pos0 < 0 || n <= 0 || pos0 + n > c.max_ctx)
+    return fail(MTTS_E_INVALID, "bad kv_write args");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const int D = c.head_dim, Hkv = c.n_kv, Cm = c.max_ctx;
+  bf16_t* kc = e->kc + layer * e->layer_kv + (size_t)b * Hkv * Cm * D;
+  bf16_t* vc = e->vc + layer * e->layer_kv + (size_t)b * Hkv * Cm * D;
+  std::vector<uint16_t> vt((size_t)D * n);
+  for (int g = 0; g < Hkv; ++g) {
+    HIPCHK(hipMemcpy(kc + ((size_t)g * Cm + pos0) * D, k + (size_t)g * n * D, (size_t)n * D * 2, hipMemcpyHostToDevice));
+    for (int i = 0; i < n; ++i)
+      for (int d = 0; d < D; ++d) vt[(size_t)d * n + i] = v[((size_t)g * n + i) * D + d];
+    HIPCHK(hipMemcpy2D(vc + (size_t)g * D * Cm + pos0, (size_t)Cm * 2, vt.data(), (size_t)n * 2, (size_t)n * 2, D,
+                       hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+extern "C" int mtts_engine_kv_fill(mtts_engine* e, uint16_t bits) {
+  if (!e || e->lp) return fail(MTTS_E_INVALID, "bad engine");
+  hipSetDevice(e->device);
+  HIPCHK(hipStreamSynchronize(e->stream));
+  HIPCHK(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(e->kc), bits, e->layer_kv * e->c.layers));
+  HIPCHK(hipMemsetD16(reinterpret_cast<hipDeviceptr_t>(e->vc), bits, e->layer_kv * e->c.layers));
+  HIPCHK(hipDeviceSynchronize());
+  return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -732,6 +827,10 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   const mtts_config& c = e->c;
   if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
     return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
+  hipSetDevice(e->device);
+  // a tripped teacher-forced launch of earlier forwards: switch before this generation (reported
+  // by those forwards' check, not here: this generation is valid)
+  if (pse_lazy_check(e, true)) g_err.clear();
   hipStream_t s = enter(e, stream);
   GenDev& g = e->hst;
   std::memset(&g, 0, sizeof(g));

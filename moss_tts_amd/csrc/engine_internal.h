@@ -110,6 +110,12 @@ struct mtts_engine {
   int pse_timeouts = 0;          // launches that gave up waiting (each turns `pse` off)
   PseLayer* pse_L = nullptr;     // device [layers]
   unsigned char* pse_ws = nullptr;  // pse_ws_bytes(), zero-filled
+  // teacher-forced forwards through the launch: its error word is copied asynchronously into
+  // pinned host memory (no host sync per step) and checked lazily (pse_lazy_check)
+  uint32_t* pse_err_host = nullptr;
+  hipEvent_t ev_pse = nullptr;
+  bool pse_pending = false;
+  bool pse_coop = false;            // MTTS_PSE_COOP=1: cooperative launch (hipLaunchCooperativeKernel)
   uint64_t* pse_trace = nullptr;    // MTTS_PSE_TRACE=1: per-layer event stamps of the last launch
   // generate state
   GenDev* st = nullptr;
@@ -130,6 +136,7 @@ struct mtts_engine {
   int nw[5] = {0, 0, 0, 0, 0};  // waves-per-block overrides (MTTS_NW="qkv,o,gu,down,heads"; 0 = auto)
   int nu[5] = {0, 0, 0, 0, 0};  // load-batch depth overrides (MTTS_U="qkv,o,gu,down,heads"; 0 = auto, 4 / 8)
   bf16_t* staging = nullptr;
+  void* load_stream = nullptr;  // the caller's stream of the weight load in progress (NULL: legacy default)
   size_t staging_bytes = 0;
   uint64_t step_weight_bytes = 0;
 
@@ -164,6 +171,8 @@ struct WTarget {
 // ---- shared engine internals (engine.cpp) ----
 bool layer_target(const LayerW& w, const std::string& rest, int H, int I, int Hq, int Hkv, int D, WTarget* t);
 int store_weight(mtts_engine* e, const WTarget& t, const char* name, const void* src, size_t bytes, int on_dev);
+// mtts_engine_load_weight without the public entry's stream bookkeeping (orders after e->load_stream)
+int load_weight_impl(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev);
 int ensure_staging(mtts_engine* e, size_t bytes);
 bool parse_layer(const char* name, int* layer, std::string* rest);
 int normed_input(mtts_engine* e, const Stack& st, GemvArgs& g, const bf16_t* nw, int M, hipStream_t s,

@@ -279,7 +279,9 @@ size_t pse_lds_bytes();
 int pse_grid(int device);
 bool pse_supported(int device, int B, int layers, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);
 size_t pse_ws_bytes();  // zero-filled once by the owner
-hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s);
+// coop: hipLaunchCooperativeKernel (the runtime checks the grid's co-residency at launch and
+// refuses it with hipErrorCooperativeLaunchTooLarge) instead of a plain launch
+hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s, bool coop = false);
 uint32_t* pse_err_word(void* ws);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
@@ -292,8 +294,9 @@ hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, 
 hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, uint8_t* seen,
                           int B, int C, int n_ch, int eos, int pad, hipStream_t s);
 // channel token: argmax (greedy) or HF penalty/temperature/top-k/top-p + draw (sampled)
+// wide_hist: [B][65536] ints of scratch (the key-bin walk of candidate sets past TOPK_CAP)
 hipError_t local_pick(GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
-                      int C, int B, hipStream_t s);
+                      int C, int B, int* wide_hist, hipStream_t s);
 // init.hip
 hipError_t fill_uniform_bf16(bf16_t* dst, size_t n, unsigned long long seed, unsigned long long tensor_id, float scale,
                              float offset, hipStream_t s);

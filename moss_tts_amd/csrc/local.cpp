@@ -191,7 +191,7 @@ int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t 
   if (channel_index(name, "model.embedding_list.", C, &i, &rest)) {
     if (rest != "weight") return bad("unknown weight");
     const std::string to = i == 0 ? std::string("language_model.embed_tokens.weight") : "emb_ext." + std::to_string(i - 1) + ".weight";
-    *rc = mtts_engine_load_weight(e, to.c_str(), src, bytes, on_dev);
+    *rc = load_weight_impl(e, to.c_str(), src, bytes, on_dev);
     return 1;
   }
   if (!std::strcmp(name, "model.language_model.embed_tokens.weight")) {  // unused: inputs_embeds path (:515-530)
@@ -199,7 +199,7 @@ int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t 
     return 1;
   }
   if (!std::strncmp(name, "model.language_model.", 21)) {
-    *rc = mtts_engine_load_weight(e, name + 6, src, bytes, on_dev);
+    *rc = load_weight_impl(e, name + 6, src, bytes, on_dev);
     return 1;
   }
   // depth stage
@@ -285,7 +285,7 @@ int local_init_random(mtts_engine* e, uint64_t seed) {
     if (s.kind == 0) scale = (float)std::sqrt(3.0 / (double)s.cols);
     else if (s.kind == 1) { scale = 0.25f; offset = 1.0f; }
     HIPCHK(fill_uniform_bf16(e->staging, s.rows * s.cols, seed, tid, scale, offset, e->stream));
-    rc = mtts_engine_load_weight(e, s.name.c_str(), e->staging, s.rows * s.cols * 2, 1);
+    rc = load_weight_impl(e, s.name.c_str(), e->staging, s.rows * s.cols * 2, 1);
     if (rc) return rc;
   }
   return 0;
@@ -387,7 +387,7 @@ static int local_depth(mtts_engine* e, int B, int n_ch, const int64_t* forced, i
     else { g.pad_start = 0; g.pad_period = e->audio_rows; g.pad_off = c.audio_pad_code; }
     HIPCHK(gemv_ex(g, EPI_LOGITS, s));
     if (dump) HIPCHK(argmax_rows(lg, ldl, V, p.next + i, C, B, s));  // teacher forcing: no generate state
-    else HIPCHK(local_pick(e->st, lg, ldl, V, i, p.seen, p.next, C, B, s));
+    else HIPCHK(local_pick(e->st, lg, ldl, V, i, p.seen, p.next, C, B, e->wide_hist, s));
     if (i + 1 < n_ch) {
       const int64_t* tok = forced ? forced + i : p.next + i;
       const bf16_t* table = i == 0 ? e->emb_text : e->emb_audio + (size_t)(i - 1) * e->audio_rows * H;
@@ -453,11 +453,8 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
                      sp->audio_top_p, sp->audio_repetition_penalty, sp->audio_top_k};
     }
     if (c == 0) q.pen = 1.f;  // the reference attaches no repetition penalty to the text channel
-    // keep-all-ties top-k holds <= TOPK_CAP candidates: the text channel needs a cap that leaves
-    // room for ties; the 1,025-code audio rows fit whole
-    if (q.sample && c == 0 && (q.top_k <= 0 || q.top_k > 1024))
-      return fail(MTTS_E_UNSUPPORTED, "sampled text channel needs top_k in [1, 1024]");
-    if (q.sample && q.top_k > 1024) return fail(MTTS_E_UNSUPPORTED, "channel top_k > 1024");
+    // any top_k (<= 0: no TopKLogitsWarper, :365-370): candidate sets past the sorted list take
+    // the key-bin walk (local_pick_kernel)
     if (q.sample && !(q.temp > 0.f)) return fail(MTTS_E_INVALID, "sampled channel needs a positive temperature");
   }
   hipStream_t s = enter(e, stream);
@@ -586,10 +583,9 @@ extern "C" int mtts_k_moss_rmsnorm(const uint16_t* x, const uint16_t* w, uint16_
 extern "C" int mtts_k_local_pick(const uint16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* out, int C,
                                  int B, int audio_rows, float temperature, int top_k, float top_p, float penalty,
                                  uint64_t seed, int step, void* stream) {
-  if (!logits || !out || B <= 0 || V <= 0 || ch < 0 || ch >= C || (ch > 0 && V > audio_rows))
+  // (the per-channel table GenDev::lch holds LOCAL_MAXC channels)
+  if (!logits || !out || B <= 0 || V <= 0 || C <= 0 || C > LOCAL_MAXC || ch < 0 || ch >= C || (ch > 0 && V > audio_rows))
     return fail(MTTS_E_INVALID, "bad local_pick args");
-  if (temperature > 0.f && ((ch == 0 && (top_k <= 0 || top_k > 1024)) || top_k > 1024))
-    return fail(MTTS_E_UNSUPPORTED, "top_k out of range");
   hipStream_t s = (hipStream_t)stream;
   GenDev g;
   std::memset(&g, 0, sizeof(g));
@@ -598,11 +594,12 @@ extern "C" int mtts_k_local_pick(const uint16_t* logits, int ld, int V, int ch, 
   GenDev* d = nullptr;
   HIPCHK(hipMallocAsync((void**)&d, sizeof(GenDev), s));
   HIPCHK(hipMemcpyAsync(d, &g, sizeof(g), hipMemcpyHostToDevice, s));
-  hipError_t err = local_pick(d, reinterpret_cast<const bf16_t*>(logits), ld, V, ch, seen, out, C, B, s);
-  if (err == hipSuccess) err = hipMemcpyAsync(&g, d, sizeof(g), hipMemcpyDeviceToHost, s);
+  int* hist = nullptr;  // key-bin scratch of the wide candidate sets
+  HIPCHK(hipMallocAsync((void**)&hist, (size_t)B * 65536 * sizeof(int), s));
+  hipError_t err = local_pick(d, reinterpret_cast<const bf16_t*>(logits), ld, V, ch, seen, out, C, B, hist, s);
+  HIPCHK(hipFreeAsync(hist, s));
   HIPCHK(hipFreeAsync(d, s));
   HIPCHK(err);
   HIPCHK(hipStreamSynchronize(s));
-  if (g.topk_overflow) return fail(MTTS_E_UNSUPPORTED, "top-k: ties at the k-th score exceed 2048 candidates");
   return 0;
 }

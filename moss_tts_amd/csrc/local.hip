@@ -137,13 +137,14 @@ hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld
 //     the largest always kept
 // The k-th largest is found by a two-pass radix select on the 16-bit order-preserving keys
 // of the (bf16-exact) processed scores (topk.h, TIES_KEEP_ALL), so the whole vocab is never
-// sorted; ties beyond TOPK_CAP candidates are cut in index order and reported by
-// mtts_generate_poll as an error (never an arrival-order choice).  The draw uses
+// sorted; candidate sets past that list (no top_k on the text row, top_k > 1,024, threshold ties
+// beyond TOPK_CAP) run the same processors as a walk over the 65,536 key bins
+// (block_wide_draw_hf), so every reference-valid setting is served.  The draw uses
 // Philox(seed; frame, row, channel): distribution-level parity (torch's RNG stream is not
 // reproduced).
 __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ st, const bf16_t* __restrict__ logits,
                                                           int ld, int V, int ch, const uint8_t* __restrict__ seen,
-                                                          int64_t* __restrict__ next, int C) {
+                                                          int64_t* __restrict__ next, int C, int* __restrict__ wide_hist) {
   __shared__ ArgMax sh[16];
   __shared__ TopkSmem sm;
   __shared__ float ev[TOPK_CAP];
@@ -183,8 +184,22 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ s
     return rbf(v / temp);
   };
   const int K = top_k > 0 ? min(top_k, V) : V;
-  int over = 0;
-  const int n = block_topk_sorted<1024>(val, V, K, TIES_KEEP_ALL, sm, &over);
+  const float u = philox_uniform(st->seed, (uint32_t)st->step, (uint32_t)b, (uint32_t)ch);
+  // the sorted candidate list holds TOPK_CAP entries: K up to half of it leaves room for the
+  // threshold ties (any K on rows that fit whole, e.g. the 1,025-code audio rows); a wider set
+  // (no top_k on the text row, top_k > 1,024) or ties past TOPK_CAP take the key-bin walk
+  bool wide = !(V <= TOPK_CAP || K <= TOPK_CAP / 2);
+  int n = 0;
+  if (!wide) {
+    int over = 0;
+    n = block_topk_sorted<1024>(val, V, K, TIES_KEEP_ALL, sm, &over);
+    wide = over != 0;
+  }
+  if (wide) {
+    const int tok = block_wide_draw_hf<1024>(val, V, top_k > 0 ? K : 0, top_p, u, wide_hist + (size_t)b * WIDE_BINS);
+    if (t == 0) next[(size_t)b * C + ch] = tok < 0 ? 0 : tok;
+    return;
+  }
   if (n <= 0) {
     if (t == 0) next[(size_t)b * C + ch] = 0;
     return;
@@ -193,7 +208,6 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ s
   for (int i = t; i < n; i += 1024) ev[i] = expf(cand_score(sm.cand[i]) - mx);
   __syncthreads();
   if (t == 0) {
-    if (over) st->topk_overflow = 1;  // ties beyond TOPK_CAP: mtts_generate_poll reports it
     float S = 0.f;
     for (int i = 0; i < n; ++i) S += ev[i];
     // HF top-p on the ascending order: cum over candidates from the smallest up
@@ -206,10 +220,23 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ s
         cum += rbf(ev[i] / S);
         if (rbf(cum) > thr_p) { keep = i + 1; break; }
       }
+      // the ascending walk above met equal scores highest index first; torch.sort (the
+      // reference's CPU path, and the oracle's stable argsort) drops the LOWEST indices of the tie
+      // run the cut splits: reverse that run so the kept prefix holds its highest indices
+      const unsigned long long kw = sm.cand[keep - 1] >> 32;
+      if (keep < n && (sm.cand[keep] >> 32) == kw) {
+        int a0 = keep - 1, b0 = keep;
+        while (a0 > 0 && (sm.cand[a0 - 1] >> 32) == kw) --a0;
+        while (b0 < n && (sm.cand[b0] >> 32) == kw) ++b0;
+        for (int i = a0, j = b0 - 1; i < j; ++i, --j) {
+          const unsigned long long x = sm.cand[i];
+          sm.cand[i] = sm.cand[j];
+          sm.cand[j] = x;
+        }
+      }
     }
     float S2 = 0.f;
     for (int i = 0; i < keep; ++i) S2 += ev[i];
-    const float u = philox_uniform(st->seed, (uint32_t)st->step, (uint32_t)b, (uint32_t)ch);
     const float target = u * S2;
     float c = 0.f;
     int pick = cand_index(sm.cand[keep - 1]);
@@ -222,9 +249,9 @@ __global__ __launch_bounds__(1024) void local_pick_kernel(GenDev* __restrict__ s
 }
 
 hipError_t local_pick(GenDev* st, const bf16_t* logits, int ld, int V, int ch, const uint8_t* seen, int64_t* next,
-                      int C, int B, hipStream_t s) {
-  if (B <= 0 || V <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(local_pick_kernel, dim3(B), dim3(1024), 0, s, st, logits, ld, V, ch, seen, next, C);
+                      int C, int B, int* wide_hist, hipStream_t s) {
+  if (B <= 0 || V <= 0 || !wide_hist) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(local_pick_kernel, dim3(B), dim3(1024), 0, s, st, logits, ld, V, ch, seen, next, C, wide_hist);
   return hipGetLastError();
 }
 

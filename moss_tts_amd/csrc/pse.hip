@@ -645,6 +645,19 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
     const int k0 = ch * KW;
+    {
+      // the V^T fragment holding pos also read keys pos .. kb+7: cache rows never written (or
+      // stale after a capacity change).  Their p is 0, but 0 * NaN / Inf in the P.V MFMA is NaN:
+      // zero those 16-bit lanes (as attn_body.h's per-op attention does)
+      const int nv = pos - (k0 + 8 * g4);  // keys of this lane's fragments below pos
+      uint32_t vm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vt[dt][q] &= vm[q];
+    }
     f32x4 sacc[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
@@ -1164,7 +1177,7 @@ size_t pse_ws_bytes() {
   return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 + 64;
 }
 
-hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
+hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   if (a0.layers < 1 || a0.layers > PSE_MAXL || a0.layers * 5 > 256 || a0.Cmax % 64) return hipErrorInvalidValue;
   PseArgs a = a0;
   uint64_t* g = reinterpret_cast<uint64_t*>(ws);
@@ -1178,6 +1191,10 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s) {
   a.g_act = g; g += I_ / 2;
   uint32_t* w = reinterpret_cast<uint32_t*>(g);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
+  if (coop) {
+    void* args[] = {&a};
+    return hipLaunchCooperativeKernel((const void*)pse_kernel, dim3(256), dim3(THREADS), args, (unsigned)pse_lds_bytes(), s);
+  }
   hipLaunchKernelGGL(pse_kernel, dim3(256), dim3(THREADS), pse_lds_bytes(), s, a);
   return hipGetLastError();
 }

@@ -380,4 +380,183 @@ __device__ int block_wide_draw(F val, int V, int K, float top_p, float u, int* h
   return w_tok;
 }
 
+// ---------------------------------------------------------------------------
+// The same bin walk with the HF processor semantics of MossTTSLocal's channel pick
+// (moss_tts_local/modeling_moss_tts.py:360-368, 414-419) for candidate sets past TOPK_CAP
+// (text channel without a top_k, a top_k above 1,024, or threshold ties beyond TOPK_CAP):
+//   TopKLogitsWarper: every score >= the K-th largest (all threshold ties kept)
+//   TopPLogitsWarper: ascending order, p = bf16(softmax), inclusive cumsum; elements with
+//     bf16(cum) <= bf16(1 - top_p) are dropped, the largest always stays.  Inside a bin of
+//     equal scores the ascending walk meets the LOWEST index first (torch.sort's order on the
+//     reference's CPU path, restated by oracle.moss_local.hf_pick_distribution's stable argsort)
+//   multinomial over the survivors' exp(s - s_max) (unnormalised, as the sorted path)
+// Sums in the same fixed chunked order as block_wide_draw (ascending walk: thread t owns the
+// bins [64 t, 64 t + 64)).  Returns the token index (-1: no finite score).
+template <int NT, class F>
+__device__ int block_wide_draw_hf(F val, int V, int K, float top_p, float u, int* hist) {
+  static_assert(NT * 64 == WIDE_BINS, "64 bins per thread");
+  typedef __attribute__((address_space(1))) int gi32;
+  auto hld = [&](int key) { return __hip_atomic_load((gi32*)(hist + key), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  const int t = threadIdx.x;
+  __shared__ float hf_wf[NT];
+  __shared__ int hf_wi[NT];
+  __shared__ int h_thr, h_topkey, h_cut_t, h_cut_key, h_cut_r, h_tok;
+  __shared__ float h_tot;
+  for (int i = t; i < WIDE_BINS; i += NT) __hip_atomic_store((gi32*)(hist + i), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int i = t; i < V; i += NT) {
+    const float v = val(i);
+    if (v > -INFINITY) __hip_atomic_fetch_add((gi32*)(hist + okey16(v)), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // descending ownership (thread t: keys dkey0, dkey0 - 1, ...) for top-k and the draw,
+  // ascending (akey0, akey0 + 1, ...) for the top-p walk
+  const int dkey0 = WIDE_BINS - 1 - 64 * t, akey0 = 64 * t;
+  int mine = 0;
+  for (int j = 0; j < 64; ++j) mine += hld(dkey0 - j);
+  hf_wi[t] = mine;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0, top = -1;
+    for (int w = 0; w < NT; ++w) {
+      const int c = hf_wi[w];
+      hf_wi[w] = run;
+      if (top < 0 && c > 0) top = w;
+      run += c;
+    }
+    h_topkey = -1;
+    if (top >= 0)
+      for (int j = 0; j < 64; ++j)
+        if (hld(WIDE_BINS - 1 - 64 * top - j) > 0) { h_topkey = WIDE_BINS - 1 - 64 * top - j; break; }
+    h_thr = (K > 0 && K < run) ? -2 : -1;  // -2: the top-k threshold key is found below
+    h_tok = -1;
+  }
+  __syncthreads();
+  if (h_topkey < 0) return -1;
+  if (h_thr == -2) {
+    const int before = hf_wi[t];
+    if (before < K && before + mine >= K) {
+      int cum = before;
+      for (int j = 0; j < 64; ++j) {
+        cum += hld(dkey0 - j);
+        if (cum >= K) { h_thr = dkey0 - j; break; }
+      }
+    }
+    __syncthreads();
+  }
+  const int thr = h_thr < 0 ? 0 : h_thr;  // bins below thr are cut (keep-all-ties: thr's bin stays whole)
+  const float mx = okey16_val((uint32_t)h_topkey);
+  // survivors: bins above lim_key whole, bin lim_key without its lim_skip lowest indices
+  auto cnt = [&](int key, int lim_key, int lim_skip) -> int {
+    if (key < thr || key < lim_key) return 0;
+    return key == lim_key ? hld(key) - lim_skip : hld(key);
+  };
+  auto mass = [](int c, float x) { return __fmul_rn((float)c, x); };
+  // fixed-order sum of fp32(c * f(key)) over this thread's 64 bins in direction `asc`; leaves the
+  // exclusive chunk prefixes (in thread order) in hf_wf
+  auto chunk_sums = [&](auto f, bool asc, int lim_key, int lim_skip) -> float {
+    float part = 0.f;
+    for (int j = 0; j < 64; ++j) {
+      const int key = asc ? akey0 + j : dkey0 - j, c = cnt(key, lim_key, lim_skip);
+      if (c) part = __fadd_rn(part, mass(c, f(key)));
+    }
+    hf_wf[t] = part;
+    __syncthreads();
+    if (t == 0) {
+      float run = 0.f;
+      for (int w = 0; w < NT; ++w) { const float x = hf_wf[w]; hf_wf[w] = run; run = __fadd_rn(run, x); }
+      h_tot = run;
+    }
+    __syncthreads();
+    return h_tot;
+  };
+  // the first element (walk direction asc) whose cumulative fp32(P_t + fp32(L + fp32(r * f)))
+  // passes -> (h_cut_key, h_cut_r = its rank r >= 1 inside the bin); h_cut_key -1 when none does
+  auto first_cross = [&](auto f, bool asc, int lim_key, int lim_skip, auto pass) {
+    if (t == 0) { h_cut_t = NT; h_cut_key = -1; h_cut_r = 0; }
+    __syncthreads();
+    const float P = hf_wf[t];
+    float L = 0.f;
+    int ck = -1, cr = 0;
+    for (int j = 0; j < 64 && ck < 0; ++j) {
+      const int key = asc ? akey0 + j : dkey0 - j, c = cnt(key, lim_key, lim_skip);
+      if (!c) continue;
+      const float x = f(key);
+      if (pass(__fadd_rn(P, __fadd_rn(L, mass(c, x))))) {
+        int lo = 1, hi = c;
+        while (lo < hi) {
+          const int mid = (lo + hi) >> 1;
+          if (pass(__fadd_rn(P, __fadd_rn(L, mass(mid, x))))) hi = mid;
+          else lo = mid + 1;
+        }
+        ck = key;
+        cr = lo;
+      }
+      L = __fadd_rn(L, mass(c, x));
+    }
+    if (ck >= 0) atomicMin(&h_cut_t, t);
+    __syncthreads();
+    if (ck >= 0 && h_cut_t == t) { h_cut_key = ck; h_cut_r = cr; }
+    __syncthreads();
+  };
+  auto evf = [&](int key) { return (float)exp((double)(okey16_val((uint32_t)key) - mx)); };
+  int lim_key = -1, lim_skip = 0;
+  if (top_p < 1.0f) {
+    const float thr_p = rbf((float)(1.0 - (double)top_p));
+    const float S = chunk_sums(evf, false, -1, 0);
+    auto pf = [&](int key) { return rbf(evf(key) / S); };
+    chunk_sums(pf, true, -1, 0);  // ascending prefixes
+    first_cross(pf, true, -1, 0, [&](float cum) { return rbf(cum) > thr_p; });
+    lim_key = h_cut_key < 0 ? h_topkey : h_cut_key;
+    // the crossing element and everything above it stay (r - 1 lowest indices of its bin go);
+    // none crossing: the largest alone (the highest index of the top bin) stays
+    lim_skip = h_cut_key < 0 ? hld(h_topkey) - 1 : h_cut_r - 1;
+  }
+  const float S2 = chunk_sums(evf, false, lim_key, lim_skip);
+  const float target = __fmul_rn(u, S2);
+  first_cross(evf, false, lim_key, lim_skip, [&](float cum) { return cum > target; });
+  if (h_cut_key < 0) {  // rounding left the target past the last survivor: take the last one
+    __syncthreads();
+    if (t == 0) {
+      int k = lim_key, r = lim_key >= 0 ? hld(lim_key) - lim_skip : 0;
+      if (lim_key < 0)
+        for (k = thr; k < WIDE_BINS; ++k)
+          if ((r = cnt(k, -1, 0)) > 0) break;
+      h_cut_key = k;
+      h_cut_r = r;
+    }
+    __syncthreads();
+  }
+  const int dk = h_cut_key, dr = h_cut_r + (h_cut_key == lim_key ? lim_skip : 0);
+  // the dr-th (1-based) lowest index of bin dk (the cut bin's survivors are its highest indices)
+  const int chunk = (V + NT - 1) / NT;
+  const int lo_i = min(V, t * chunk), hi_i = min(V, lo_i + chunk);
+  int c = 0;
+  for (int i = lo_i; i < hi_i; ++i) {
+    const float v = val(i);
+    c += (v > -INFINITY && (int)okey16(v) == dk) ? 1 : 0;
+  }
+  hf_wi[t] = c;
+  __syncthreads();
+  if (t == 0) {
+    int run = 0;
+    for (int w = 0; w < NT; ++w) { const int x = hf_wi[w]; hf_wi[w] = run; run += x; }
+  }
+  __syncthreads();
+  int rank = hf_wi[t];
+  if (rank < dr && rank + c >= dr) {
+    for (int i = lo_i; i < hi_i; ++i) {
+      const float v = val(i);
+      if (v > -INFINITY && (int)okey16(v) == dk && ++rank == dr) {
+        h_tok = i;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  return h_tok;
+}
+
 }  // namespace mtts

@@ -113,7 +113,9 @@ class Engine:
         on_dev = 1 if t.is_cuda else 0
         if t.is_cuda and t.device != self.device:
             t = t.to(self.device)
-        N.check(N.load().mtts_engine_load_weight(self._h, name.encode(), _ptr(t), t.numel() * 2, on_dev), name)
+        # ordered after torch's current stream (where a device source was produced): no device sync
+        N.check(N.load().mtts_engine_load_weight_stream(self._h, name.encode(), _ptr(t), t.numel() * 2, on_dev,
+                                                        _stream_ptr(self.device)), name)
 
     def load_state_dict(self, sd: Dict[str, torch.Tensor]):
         for k, v in sd.items():
@@ -138,6 +140,24 @@ class Engine:
     def pse_ctx_max(self) -> int:
         """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
         return int(N.load().mtts_pse_ctx_max(self._h))
+
+    def pse_check(self):
+        """Blocking check of the persistent launch's error word for the teacher-forced forwards so
+        far (`forward` itself does not synchronise).  Raises `PseTimeout` once when a launch timed
+        out: those forwards' logits are invalid, the engine now runs the per-op launches."""
+        N.check(N.load().mtts_pse_check(self._h), "pse_check")
+
+    def kv_write(self, layer: int, row: int, pos0: int, k, v):
+        """test hook: K / V rows (bf16 [n_kv, n, head_dim], host) at positions pos0.. of one row"""
+        k = k.detach().to("cpu", torch.bfloat16).contiguous()
+        v = v.detach().to("cpu", torch.bfloat16).contiguous()
+        assert k.shape == v.shape and k.dim() == 3
+        N.check(N.load().mtts_engine_kv_write(self._h, layer, row, pos0, k.shape[1], ctypes.c_void_p(k.data_ptr()),
+                                              ctypes.c_void_p(v.data_ptr())), "kv_write")
+
+    def kv_fill(self, bits: int):
+        """test hook: the whole KV cache set to one bf16 bit pattern"""
+        N.check(N.load().mtts_engine_kv_fill(self._h, bits), "kv_fill")
 
     def inject_pse_timeout(self):
         """fault injection (tests): the persistent launch's next check sees a timed-out wait"""

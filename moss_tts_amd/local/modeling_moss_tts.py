@@ -8,7 +8,7 @@ local_to_speech_embedding_mlps, layer_norm_before_lm_heads, lm_heads) and the
 generation_config (README `moss_tts_local/README.md:203-220`): `n_vq_for_inference`,
 `do_samples` (per channel), `layers` (per channel dict of repetition_penalty / temperature /
 top_k / top_p), `max_new_tokens` or `max_length`, `eos_token_id`.  Every channel takes its own
-processor set (mtts_local_set_sampling).  A sampled text channel needs a top_k (<= 1,024).
+processor set (mtts_local_set_sampling); any top_k (none, or past the sorted candidate list) is served.
 """
 import copy
 import os

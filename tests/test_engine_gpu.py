@@ -329,6 +329,7 @@ def test_long_context_16_wave_attention(gpu, golden, T):
         eng = make_engine(cfg, W, max_batch=1, max_ctx=(T + steps + 63) // 64 * 64, max_prefill_tokens=4096)
     finally:
         os.environ.pop("MTTS_ATTN_LONG")
+    eng.kv_fill(0x7FC0)  # NaN in every row not yet written: no kernel may read one into a result
     ctx = O._Ctx("bf16")
     cache = O.KVCache(cfg.layers)
     for s in range(steps + 1):
@@ -362,6 +363,7 @@ def test_long_context_decode_logits(gpu, golden):
     mask[1, :37] = False  # left padding of row 1
     ids[1, :37, 0] = cfg.pad_token_id
     eng = make_engine(cfg, W, max_ctx=1408, max_prefill_tokens=4096)
+    eng.kv_fill(0x7FC0)  # NaN in every row not yet written (the prefill flash tiles, the decode splits)
     ctx = O._Ctx("bf16")
     cache = O.KVCache(cfg.layers)
     for s in range(steps + 1):

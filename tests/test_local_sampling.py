@@ -16,6 +16,13 @@ CASES = [
     (3, 1025, 1.0, 50, 0.95, 1.1),
     (1, 1025, 0.7, 25, 0.8, 1.3),
     (2, 1025, 1.2, 1024, 0.9, 1.1),
+    # past the sorted candidate list (round 4): the key-bin walk (topk.h block_wide_draw_hf) on the
+    # text row, any top_k on the audio rows (top_k <= 0: no TopKLogitsWarper)
+    (0, 151936, 1.5, 0, 0.9, None),
+    (0, 151936, 1.0, 5000, 0.95, None),
+    (0, 151936, 0.8, 0, 1.0, None),
+    (2, 1025, 1.2, 0, 0.9, 1.1),
+    (1, 1025, 1.0, 2000, 1.0, 1.3),
 ]
 
 
@@ -37,8 +44,10 @@ def hf_reference(x, hist, ch, temperature, top_k, top_p, penalty):
     if penalty is not None and ch != 0:
         procs.append(RepetitionPenaltyLogitsProcessor(penalty=penalty))
     procs.append(TemperatureLogitsWarper(temperature=temperature))
-    procs.append(TopKLogitsWarper(top_k=top_k))
-    procs.append(TopPLogitsWarper(top_p=top_p))
+    if top_k > 0:  # the reference attaches no TopKLogitsWarper without a top_k (:365-370)
+        procs.append(TopKLogitsWarper(top_k=top_k))
+    if top_p < 1.0:
+        procs.append(TopPLogitsWarper(top_p=top_p))
     ids = torch.from_numpy(np.asarray(hist if len(hist) else [0], np.int64))[None]
     s = procs(ids, torch.from_numpy(x)[None].to(torch.bfloat16))
     return torch.softmax(s.float(), -1)[0].double().numpy()
@@ -50,7 +59,13 @@ def test_oracle_pick_matches_hf_processors(case):
     x, hist = make_row(V, ch, 7 + ch)
     want = hf_reference(x, hist, ch, temperature, top_k, top_p, penalty)
     got = L.hf_pick_distribution(x, hist, ch, temperature, top_k, top_p, penalty)
-    assert np.array_equal(want > 0, got > 0)
+    # the same number kept; the sets may differ only inside the run of equal scores the top-p cut
+    # splits (torch.sort is not stable on the 151,936-entry row: which tied entries HF drops there
+    # is arbitrary -- the oracle drops the lowest indices, as torch does on the short rows)
+    assert (want > 0).sum() == (got > 0).sum()
+    diff = np.nonzero((want > 0) != (got > 0))[0]
+    proc = (torch.from_numpy(x).to(torch.bfloat16) / temperature).to(torch.bfloat16).float().numpy()
+    assert np.unique(proc[diff]).size <= 1, "kept sets differ outside one tie run"
     assert np.allclose(got, want, atol=2e-3)
 
 
@@ -77,9 +92,13 @@ def test_device_pick_distribution(case):
                                        penalty if penalty else 1.0, 1234, 5, None), "local_pick")
     draws = out[:, ch].cpu().numpy()
     kept = np.nonzero(probs > 0)[0]
-    assert np.isin(draws, kept).all(), "draw outside the kept set"
+    # (the top-p cut may fall one element apart in a long tie run: its scores are equal)
+    proc = (torch.from_numpy(x).to(torch.bfloat16) / temperature).to(torch.bfloat16).float().numpy()
+    edge = np.nonzero(proc == proc[kept].min())[0] if kept.size < V else kept
+    assert np.isin(draws, np.union1d(kept, edge)).all(), "draw outside the kept set"
+    draws = draws[np.isin(draws, kept)]
     cnt = np.bincount(draws, minlength=V)[kept].astype(np.float64)
-    exp = probs[kept] * R
+    exp = probs[kept] * draws.size
     big = exp >= 5  # chi-square on the well-populated cells, the rest pooled
     f_obs = np.append(cnt[big], cnt[~big].sum())
     f_exp = np.append(exp[big], exp[~big].sum())
@@ -87,6 +106,41 @@ def test_device_pick_distribution(case):
         f_obs, f_exp = f_obs[:-1], f_exp[:-1]
     f_exp *= f_obs.sum() / f_exp.sum()
     assert chisquare(f_obs, f_exp).pvalue > 1e-3
+
+
+@pytest.mark.gpu
+def test_device_pick_threshold_ties_past_the_list():
+    """top_k = 50 on a text row whose 50th score is shared by 3,000 entries: HF keeps every tie,
+    more than the sorted list holds, so the pick takes the key-bin walk -- draws stay inside the
+    kept set and follow its distribution (round 3 reported MTTS_E_UNSUPPORTED here)"""
+    import ctypes
+    from scipy.stats import chisquare
+    from moss_tts_amd import _native as N
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    V, ch = 151936, 0
+    x, hist = make_row(V, ch, 31)
+    srt = np.sort(x)[::-1]
+    tie = srt[40]
+    rng = np.random.default_rng(5)
+    x[rng.choice(np.nonzero(x < tie)[0], 3000, replace=False)] = tie
+    probs = L.hf_pick_distribution(x, hist, ch, 1.0, 50, 1.0, None)
+    kept = np.nonzero(probs > 0)[0]
+    assert kept.size > 2048
+    R, C, A = 8192, 4, 1025
+    logits = torch.from_numpy(x).to(torch.bfloat16)[None].expand(R, V).contiguous().cuda()
+    seen = torch.zeros(R, C, A, dtype=torch.uint8, device="cuda")
+    out = torch.full((R, C), -1, dtype=torch.int64, device="cuda")
+    P = lambda t: ctypes.c_void_p(t.data_ptr())
+    N.check(N.load().mtts_k_local_pick(P(logits), V, V, ch, P(seen), P(out), C, R, A, 1.0, 50, 1.0, 1.0, 99, 3, None),
+            "local_pick")
+    draws = out[:, ch].cpu().numpy()
+    assert np.isin(draws, kept).all()
+    top = probs[kept] >= 5.0 / R  # the strong candidates one by one, the tie run pooled
+    cnt = np.bincount(draws, minlength=V)[kept].astype(np.float64)
+    f_obs = np.append(cnt[top], cnt[~top].sum())
+    f_exp = np.append(probs[kept][top], probs[kept][~top].sum()) * R
+    assert chisquare(f_obs, f_exp * f_obs.sum() / f_exp.sum()).pvalue > 1e-3
 
 
 @pytest.mark.gpu

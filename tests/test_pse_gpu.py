@@ -194,26 +194,40 @@ def test_pse_generation_crosses_the_context_range(engines):
 
 def test_pse_timeout_falls_back_to_launches(engines):
     """A persistent launch that gives up waiting (its workgroups not all resident: other work on
-    the device) must not surface as an error: a teacher-forced step re-runs on the per-op
-    launches (bit-identical to them), generate() restarts there, and the engine stays on them.
-    The timeout is injected through the error word (mtts_pse_inject_timeout)."""
+    the device) is reported once, lazily (round 4: a teacher-forced forward no longer synchronises
+    the host): mtts_pse_check -- or the next forward once the async copy of the error word has
+    landed -- raises PseTimeout, the engine switches to the per-op launches, and the recomputed
+    steps are bit-identical to them; generate() restarts there by itself.  The timeout is
+    injected through the error word (mtts_pse_inject_timeout)."""
     from moss_tts_amd.engine import sampling_params
+    from moss_tts_amd._native import PseTimeout
     ref, _ = engines
-    e = make(True)
-    try:
-        ids, mask = prompt(120, 3, 17)
-        want = decode_logits(ref, ids, mask, 120, 3)
-        lg = e.forward(torch.from_numpy(ids[:, :120].copy()), torch.from_numpy(mask[:, :120]), 0)
-        got = []
-        e.inject_pse_timeout()  # the first decode step's check trips (the prefill is the GEMM path)
-        for s in range(3):
-            p = 120 + s
-            lg = e.forward(torch.from_numpy(ids[:, p:p + 1].copy()), torch.from_numpy(mask[:, :p + 1]), p)
-            got.append(lg.float().cpu().numpy()[0])
-        assert not e.pse_active()
-        assert all(np.array_equal(w, g) for w, g in zip(want, got))
-    finally:
-        e.close()
+    ids, mask = prompt(120, 3, 17)
+    want = decode_logits(ref, ids, mask, 120, 3)
+    for how in ("pse_check", "next_forward"):
+        e = make(True)
+        try:
+            e.forward(torch.from_numpy(ids[:, :120].copy()), torch.from_numpy(mask[:, :120]), 0)
+            e.pse_check()  # the prefill (GEMM path) is clean
+            e.inject_pse_timeout()  # the first decode step's launch sees the word set
+            e.forward(torch.from_numpy(ids[:, 120:121].copy()), torch.from_numpy(mask[:, :121]), 120)
+            if how == "pse_check":
+                with pytest.raises(PseTimeout):
+                    e.pse_check()
+            else:
+                torch.cuda.synchronize()  # the async copy has landed: the next forward reports it
+                with pytest.raises(PseTimeout):
+                    e.forward(torch.from_numpy(ids[:, 121:122].copy()), torch.from_numpy(mask[:, :122]), 121)
+            assert not e.pse_active()
+            e.pse_check()  # reported once
+            got = []
+            for s in range(3):  # the invalid step recomputed, then on
+                p = 120 + s
+                lg = e.forward(torch.from_numpy(ids[:, p:p + 1].copy()), torch.from_numpy(mask[:, :p + 1]), p)
+                got.append(lg.float().cpu().numpy()[0])
+            assert all(np.array_equal(w, g) for w, g in zip(want, got))
+        finally:
+            e.close()
     e = make(True)
     try:
         ids, mask = prompt(100, 0, 19)

@@ -133,9 +133,14 @@ def band(got, want, what):
         assert int(np.argmax(np.where(fin, got, -np.inf))) == int(np.argmax(np.where(fin, want, -np.inf))), what
 
 
-@pytest.mark.parametrize("T,steps,pad", [(150, 10, 0), (611, 14, 0), (300, 8, 37)])
-def test_pse_decode_logits_vs_oracle(setup, T, steps, pad):
+@pytest.mark.parametrize("T,steps,pad,poison", [(150, 10, 0, False), (611, 14, 0, False), (300, 8, 37, False),
+                                                (201, 9, 5, True)])
+def test_pse_decode_logits_vs_oracle(setup, T, steps, pad, poison):
+    """poison: every KV cache row starts as NaN (kv_fill), so rows past the decode position
+    -- the V^T fragment holding pos reads 8 keys at once -- must never reach a result"""
     eng, M = setup
+    if poison:
+        eng.kv_fill(0x7FC0)
     ids, mask = prompt(T, steps, T + pad, pad)
     ctx = O._Ctx("bf16")
     cache = O.KVCache(LAYERS)
