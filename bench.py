@@ -643,12 +643,16 @@ def main():
                          "frac": round(g_ach / HBM_PEAK_GBS, 4),
                          "kernel": "gemv_kernel gate|up (fused RMSNorm prologue, SwiGLU epilogue), layers rotated",
                          "alg_bytes_per_launch": int(g_nb), "avg_launch_us": round(g_ms * 1e3, 2)}
-            if eng.pse_active() and args.batch == 1 and args.config == "clone":
-                # batch-1 decode runs the whole layer stack as ONE persistent launch (pse.hip):
-                # that launch is the dominant kernel (every layer's weights + the K/V rows read)
+            if args.config == "clone" and ((eng.pse_active() and args.batch == 1) or
+                                           (eng.pse4_active() and args.batch == 4)):
+                # batch-1 / batch-4 decode runs the whole layer stack as ONE persistent launch
+                # (pse.hip / pse4.hip): that launch is the dominant kernel (every layer's weights +
+                # the K/V rows read)
                 ms, nb = time_kernel(5, 20)
-                kname = "pse_kernel (persistent streaming decode: every backbone layer in one launch, batch 1)"
-                traffic, traffic_src = pmc_traffic("pse")
+                kname = ("pse_kernel (persistent streaming decode: every backbone layer in one launch, batch 1)"
+                         if args.batch == 1 else
+                         "pse4_kernel (persistent streaming decode: every backbone layer in one launch, batch 4)")
+                traffic, traffic_src = pmc_traffic("pse" if args.batch == 1 else "pse4")
             else:
                 ms, nb = g_ms, g_nb
                 kname = gemv_roof["kernel"]
@@ -679,9 +683,11 @@ def main():
                        "layers": args.layers, "parallelism": f"dp{world}", "sampling": "greedy, forced text schedule"},
             "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
             "audio_frames_per_utt": frames0,
-            "decode_path": (f"batch 1: the 36-layer stack as one persistent streaming launch (csrc/pse.hip) for steps "
-                            f"with context <= {eng.pse_ctx_max()}, per-op hipGraph launches beyond"
-                            if eng.pse_active() and args.batch == 1 else "per-op hipGraph launches"),
+            "decode_path": (f"batch {args.batch}: the 36-layer stack as one persistent streaming launch (csrc/"
+                            f"{'pse.hip' if args.batch == 1 else 'pse4.hip'}) for steps with context <= "
+                            f"{eng.pse_ctx_max()}, per-op hipGraph launches beyond"
+                            if (eng.pse_active() and args.batch == 1) or (eng.pse4_active() and args.batch == 4)
+                            else "per-op hipGraph launches"),
             "p50_first_chunk_ms": round(p50, 2),
             "first_chunk_def": f"prefill + {13 + n_vq + 1} decode steps (first 1 s of audio codes complete), codec excluded",
             "decode_weight_bytes": wb,

@@ -98,7 +98,7 @@ int mtts_engine_weight_bytes(const mtts_engine* eng, uint64_t* bytes);
 /* Roofline probe: average duration (HIP events, engine stream) of one GEMV of the loaded
  * model -- which: 0 q|k|v, 1 o_proj, 2 gate|up+SwiGLU, 3 down, 4 heads -- and its
  * algorithmic bytes per launch (weights once + activations + outputs); which 5: the
- * persistent streaming decode stack (every layer in one launch, B = 1, at the engine's
+ * persistent streaming decode stack (every layer in one launch, B = 1 or 4, at the engine's
  * current decode position; bytes = all layer weights + the K/V rows read); which 6 / 7
  * (MossTTSLocal): the depth stack's gate|up+SwiGLU / down of depth layer `layer`, launched as
  * the channel loop launches them, walking the depth layers. */
@@ -119,6 +119,8 @@ int mtts_heads_ld(const mtts_engine* eng);
  * forwards) whose context stays within mtts_pse_ctx_max (MTTS_PSE_CTX); later steps of the
  * same generation take the per-op launches. */
 int mtts_pse_active(const mtts_engine* eng);
+/* the same for batch-4 decode steps (configs[2]'s per-GPU share: pse4.hip; MTTS_PSE4=0 turns it off) */
+int mtts_pse4_active(const mtts_engine* eng);
 int mtts_pse_ctx_max(const mtts_engine* eng);
 /* Fault injection (tests): mark the persistent launch's error word as if a wait had timed out.
  * The next check (a teacher-forced batch-1 forward, or mtts_generate_poll) takes the fallback:

@@ -76,6 +76,7 @@ _SIGS = {
     "mtts_forward": (I, [P, P, P, I, I, I, P, P]),
     "mtts_heads_ld": (I, [P]),
     "mtts_pse_active": (I, [P]),
+    "mtts_pse4_active": (I, [P]),
     "mtts_pse_ctx_max": (I, [P]),
     "mtts_pse_inject_timeout": (I, [P]),
     "mtts_pse_check": (I, [P]),

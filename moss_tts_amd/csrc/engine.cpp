@@ -112,6 +112,13 @@ static int alloc_capacity(mtts_engine* e) {
         hipMemset(e->pse_ws, 0, pse_ws_bytes()) != hipSuccess)
       return fail(MTTS_E_HIP, "pse state");
     e->pse_ok = pse_supported(e->device, 1, c.layers, H, Hq, Hkv, D, I, e->qkv_rows, c.max_ctx);
+    e->pse4_ok = c.max_batch >= 4 && pse4_supported(e->device, c.layers, H, Hq, Hkv, D, I, e->qkv_rows, c.max_ctx);
+    if (e->pse4_ok) {
+      if ((rc = e->alloc(&e->pse4_ws, pse4_ws_bytes()))) return rc;
+      if (hipMemset(e->pse4_ws, 0, pse4_ws_bytes()) != hipSuccess) return fail(MTTS_E_HIP, "pse4 state");
+    } else {
+      e->pse4_ws = nullptr;
+    }
     if (getenv("MTTS_PSE_TRACE") && (rc = e->alloc(&e->pse_trace, (size_t)c.layers * PSE_TRACE_EV * 256))) return rc;
   }
   // generate state
@@ -156,6 +163,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_PSE")) e->pse = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE_CTX")) e->pse_ctx_max = atoi(v);
   if (const char* v = getenv("MTTS_PSE_COOP")) e->pse_coop = v[0] == '1';
+  if (const char* v = getenv("MTTS_PSE4")) e->pse4 = v[0] == '1';
   if (const char* v = getenv("MTTS_ATTN_LONG")) e->attn_long_ctx = atoi(v);
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
@@ -237,16 +245,23 @@ extern "C" int mtts_engine_weight_bytes(const mtts_engine* e, uint64_t* bytes) {
   return 0;
 }
 extern "C" int mtts_heads_ld(const mtts_engine* e) { return e ? e->heads_ld : 0; }
+uint32_t* mtts_engine::pse_err(int B) const {
+  return B == 4 ? (pse4_ws ? pse4_err_word(pse4_ws) : nullptr) : (pse_ws ? pse_err_word(pse_ws) : nullptr);
+}
 extern "C" int mtts_pse_active(const mtts_engine* e) { return e && e->pse && e->pse_ok ? 1 : 0; }
+extern "C" int mtts_pse4_active(const mtts_engine* e) { return e && e->pse_takes(4) ? 1 : 0; }
 extern "C" int mtts_pse_inject_timeout(mtts_engine* e) {
   if (!e || !e->pse_ws) return fail(MTTS_E_INVALID, "no persistent launch state");
   hipSetDevice(e->device);
   HIPCHK(hipStreamSynchronize(e->stream));
   const uint32_t code = 0x7e57u;
   HIPCHK(hipMemcpy(pse_err_word(e->pse_ws), &code, 4, hipMemcpyHostToDevice));
+  if (e->pse4_ws) HIPCHK(hipMemcpy(pse4_err_word(e->pse4_ws), &code, 4, hipMemcpyHostToDevice));
   return 0;
 }
-extern "C" int mtts_pse_ctx_max(const mtts_engine* e) { return e && e->pse && e->pse_ok ? e->pse_ctx_max : 0; }
+extern "C" int mtts_pse_ctx_max(const mtts_engine* e) {
+  return e && e->pse && (e->pse_ok || (e->pse4 && e->pse4_ok)) ? e->pse_ctx_max : 0;
+}
 extern "C" int mtts_pse_trace(mtts_engine* e, uint64_t* host, size_t n) {
   if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
   if (!e->pse_trace) return fail(MTTS_E_UNSUPPORTED, "engine created without MTTS_PSE_TRACE=1");
@@ -514,6 +529,15 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     HIPCHK(pse_decode(pa, e->pse_ws, s, e->pse_coop));
     return 0;
   }
+  if (S == 1 && B == 4 && b0 == 0 && e->pse_takes(4) && e->pse_now && st.cos_t && st.L == e->L.data()) {
+    // the batch-4 form (pse4.hip): rows 0-3 of the residual stream, masks and caches
+    PseArgs pa{};
+    pa.L = e->pse_L; pa.layers = st.layers; pa.h = st.h; pa.ss = st.ss; pa.cos_t = st.cos_t; pa.sin_t = st.sin_t;
+    pa.mask = st.mask; pa.pos = pos_base; pa.Cmax = st.Cmax; pa.eps = e->c.rms_eps;
+    pa.scale = 1.0f / std::sqrt((float)D);
+    HIPCHK(pse4_decode(pa, e->pse4_ws, s, e->pse_coop));
+    return 0;
+  }
   // decode: o_proj merges the attention's split partials in its prologue when it preloads one
   // merged element per thread (gemv_attn_preload: batch 1-2 at K 4096) and the context is short
   // (the long-context graphs' attention merges its many splits itself); otherwise the attention
@@ -695,11 +719,14 @@ void leave(mtts_engine* e, void* user) {
 // and report true; synchronises the engine stream.
 bool pse_tripped(mtts_engine* e, hipStream_t s) {
   if (!e->pse_ws) return false;
-  uint32_t err = 0;
-  if (hipStreamSynchronize(s) != hipSuccess ||
-      hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost) != hipSuccess || !err)
+  uint32_t err = 0, err4 = 0;
+  if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost) != hipSuccess)
     return false;
+  if (e->pse4_ws && hipMemcpy(&err4, pse4_err_word(e->pse4_ws), 4, hipMemcpyDeviceToHost) != hipSuccess) return false;
+  if (!err && !err4) return false;
+  err |= err4;
   hipMemset(e->pse_ws, 0, pse_ws_bytes());
+  if (e->pse4_ws) hipMemset(e->pse4_ws, 0, pse4_ws_bytes());
   e->pse = false;
   e->pse_timeouts += 1;
   fprintf(stderr, "libmtts: persistent streaming decode timed out (code %u; device shared with other work?); "
@@ -717,6 +744,7 @@ bool pse_tripped(mtts_engine* e, hipStream_t s) {
 // rewrites the KV rows at past..), which the per-op launches then do.
 static void pse_trip(mtts_engine* e, uint32_t err) {
   hipMemsetAsync(pse_err_word(e->pse_ws), 0, 4, e->stream);
+  if (e->pse4_ws) hipMemsetAsync(pse4_err_word(e->pse4_ws), 0, 4, e->stream);
   e->pse = false;
   e->pse_timeouts += 1;
   fprintf(stderr, "libmtts: persistent streaming decode timed out (code %u; device shared with other work?); "
@@ -761,11 +789,11 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   e->pse_choose(past + S);
   e->long_now = e->attn_long_ctx > 0 && past + S > e->attn_long_ctx;
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
-  if (!rc && S == 1 && B == 1 && e->pse && e->pse_ok && e->pse_now && e->pse_ws) {
+  if (!rc && S == 1 && e->pse_takes(B) && e->pse_now && e->pse_err(B)) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cs));
     if (cs == hipStreamCaptureStatusNone) {  // (inside a caller's capture: mtts_pse_check reads the word)
-      HIPCHK(hipMemcpyAsync(e->pse_err_host, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(e->pse_err_host, e->pse_err(B), 4, hipMemcpyDeviceToHost, s));
       HIPCHK(hipEventRecord(e->ev_pse, s));
       e->pse_pending = true;
     }
@@ -904,7 +932,7 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
     // context of this step <= prompt + steps so far + 1
     const int ctx = e->gen_T + e->steps_issued + 1;
-    const bool pse = e->pse && e->pse_ok && e->gen_B == 1 && ctx <= e->pse_ctx_max;
+    const bool pse = e->pse_takes(e->gen_B) && ctx <= e->pse_ctx_max;
     const bool lng = !pse && e->gen_B == 1 && e->attn_long_ctx > 0 && ctx > e->attn_long_ctx;
     hipGraphExec_t exec = nullptr;
     if (int rc = graph_for(pse, lng, &exec)) return rc;
@@ -1071,7 +1099,7 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
   if (which == 5) {
     // the persistent streaming decode stack (pse.hip): ONE launch streams every layer, at the
     // engine's current decode position `layer` ignored; the cached keys up to pos are read
-    if (e->lp || !(e->pse && e->pse_ok) || B != 1) return fail(MTTS_E_UNSUPPORTED, "persistent streaming decode inactive");
+    if (e->lp || (B != 1 && B != 4) || !e->pse_takes(B)) return fail(MTTS_E_UNSUPPORTED, "persistent streaming decode inactive");
     hipStream_t s = e->stream;
     const Stack st = backbone_stack(e);
     int pos = 0;
@@ -1083,10 +1111,10 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
     e->pse_now = true;
-    if (int rc = run_layers(e, st, 0, 1, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
+    if (int rc = run_layers(e, st, 0, B, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
     HIPCHK(hipEventRecord(a, s));
     for (int i = 0; i < iters; ++i)
-      if (int rc = run_layers(e, st, 0, 1, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
+      if (int rc = run_layers(e, st, 0, B, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
     HIPCHK(hipEventRecord(b, s));
     HIPCHK(hipEventSynchronize(b));
     float ms = 0.f;
@@ -1094,15 +1122,15 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
     hipEventDestroy(a);
     hipEventDestroy(b);
     uint32_t err = 0;
-    HIPCHK(hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(&err, e->pse_err(B), 4, hipMemcpyDeviceToHost));
     if (err) {
-      hipMemset(pse_err_word(e->pse_ws), 0, 4);
+      hipMemset(e->pse_err(B), 0, 4);
       return fail(MTTS_E_HIP, "persistent streaming decode: a wait timed out (timing invalid)");
     }
     *avg_ms = ms / iters;
     // every layer's weights once + its K / V rows 0..pos read and row pos written
     const uint64_t wl = 2ull * ((uint64_t)e->qkv_rows * H + (uint64_t)H * Hq * D + 3ull * I * H);
-    const uint64_t kv = 2ull * 2 * c.n_kv * D * (uint64_t)(pos + 1);
+    const uint64_t kv = 2ull * 2 * c.n_kv * D * (uint64_t)(pos + 1) * B;
     *alg_bytes = (uint64_t)st.layers * (wl + kv);
     return 0;
   }

@@ -107,6 +107,13 @@ struct mtts_engine {
   bool long_now = false;         // this forward / captured decode step takes the long form
   void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
   bool pse_ok = false;           // the shape and the device support it
+  // batch-4 form (pse4.hip, configs[2]'s per-GPU share): MTTS_PSE4=0 turns it off (A/B)
+  bool pse4 = true;
+  bool pse4_ok = false;
+  unsigned char* pse4_ws = nullptr;  // pse4_ws_bytes(), zero-filled
+  // the persistent launch a decode of B rows takes (when its context is in range)
+  bool pse_takes(int B) const { return pse && ((B == 1 && pse_ok) || (B == 4 && pse4 && pse4_ok)); }
+  uint32_t* pse_err(int B) const;
   int pse_timeouts = 0;          // launches that gave up waiting (each turns `pse` off)
   PseLayer* pse_L = nullptr;     // device [layers]
   unsigned char* pse_ws = nullptr;  // pse_ws_bytes(), zero-filled

@@ -283,6 +283,13 @@ size_t pse_ws_bytes();  // zero-filled once by the owner
 // refuses it with hipErrorCooperativeLaunchTooLarge) instead of a plain launch
 hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s, bool coop = false);
 uint32_t* pse_err_word(void* ws);
+// pse4.hip: the same for a decode batch of exactly 4 rows (configs[2]'s per-GPU share); PseArgs as
+// above with h [4][H], ss [4][H/16], mask [4][Cmax] (rows 0-3), the caches' rows 0-3
+size_t pse4_lds_bytes();
+bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I, int qkv_rows, int Cmax);
+size_t pse4_ws_bytes();  // zero-filled once by the owner
+hipError_t pse4_decode(const PseArgs& a, void* ws, hipStream_t s, bool coop = false);
+uint32_t* pse4_err_word(void* ws);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);

@@ -137,6 +137,10 @@ class Engine:
         """Whether batch-1 decode steps run the decoder stack as one persistent launch (pse.hip)."""
         return bool(N.load().mtts_pse_active(self._h))
 
+    def pse4_active(self) -> bool:
+        """Whether batch-4 decode steps run the decoder stack as one persistent launch (pse4.hip)."""
+        return bool(N.load().mtts_pse4_active(self._h))
+
     def pse_ctx_max(self) -> int:
         """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
         return int(N.load().mtts_pse_ctx_max(self._h))

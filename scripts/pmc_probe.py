@@ -2,7 +2,8 @@
 """Launch the bench's dominant kernel on its own (the decode step's gate|up GEMV instance, via
 mtts_engine_time_gemv: layers rotated, so no launch re-reads a matrix the previous one left in
 the 256 MB MALL; --config local: the depth stack's gate|up at B=8, its 4 layers walked as the
-frame walks them; --config pse: the batch-1 persistent streaming decode launch, every layer) for
+frame walks them; --config pse / pse4: the batch-1 / batch-4 persistent streaming decode launch, every
+layer) for
 rocprofv3 PMC passes:
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D -o f --output-format csv -- python3 scripts/pmc_probe.py --config clone
@@ -33,13 +34,13 @@ def run(cfg_name, iters):
                            local_mlp_ffn=2048)
         B = 8
     else:
-        cfg = EngineConfig(max_batch=1, max_ctx=512)
-        B = 1
+        B = 4 if cfg_name == "pse4" else 1
+        cfg = EngineConfig(max_batch=B, max_ctx=512)
     eng = Engine(cfg, 0)
     eng.init_random(0)
     which = 6 if cfg_name == "local" else 2  # local: the depth stack's gate|up (the frame's dominant launch)
-    if cfg_name == "pse":  # the batch-1 decode stack as one persistent launch (pse.hip)
-        if not eng.pse_active():
+    if cfg_name in ("pse", "pse4"):  # the decode stack as one persistent launch (pse.hip / pse4.hip)
+        if not (eng.pse_active() if cfg_name == "pse" else eng.pse4_active()):
             raise SystemExit("persistent streaming decode inactive")
         which = 5
     ms, nb = ctypes.c_float(), ctypes.c_uint64()
@@ -53,7 +54,8 @@ def summarize(d, cfg_name):
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if ("pse_kernel" if cfg_name == "pse" else "gemv_kernel") not in r["Kernel_Name"]:
+            want = {"pse": "pse_kernel", "pse4": "pse4_kernel"}.get(cfg_name, "gemv_kernel")
+            if want not in r["Kernel_Name"]:
                 continue
             vals.setdefault(r["Counter_Name"], {}).setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     out = {"config": cfg_name, "unit_raw": "KiB (rocprofv3 FETCH_SIZE / WRITE_SIZE)"}
@@ -71,7 +73,7 @@ def summarize(d, cfg_name):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["clone", "local", "pse"], default="clone")
+    ap.add_argument("--config", choices=["clone", "local", "pse", "pse4"], default="clone")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--summarize", default=None)
     a = ap.parse_args()

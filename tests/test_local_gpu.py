@@ -284,10 +284,13 @@ def test_local_per_channel_processors(gpu, gl):
     greedy = run([False] * C, [{}] * C)
     # (power-of-two temperatures: bf16(s / T) keeps every order.  HF's top-k keeps every score tied
     # with the k-th -- random bf16 logits often tie at the top of 1,025 codes -- and top_p 0.3 then
-    # drops all but one of a tie, the lowest index in the engine's order: the argmax)
+    # drops all but one of a tie: the HIGHEST index, torch.sort's ascending order dropping the lower
+    # ones first (test_local_sampling.py::test_device_pick_greedy_and_top1), where argmax takes the
+    # first -- so the top-1 channels are deterministic, and equal the greedy run where no tie occurs)
     top1 = [{"temperature": 2.0 ** (i % 3 - 1), "top_k": 1, "top_p": 0.3, "repetition_penalty": 1.0} for i in range(C)]
     mixed = run([i % 2 == 1 for i in range(C)], top1)
-    assert all(torch.equal(a, b) for a, b in zip(greedy, mixed))
+    assert all(torch.equal(a, b) for a, b in zip(mixed, run([i % 2 == 1 for i in range(C)], top1, seed=7)))
+    assert all(a.shape == b.shape for a, b in zip(greedy, mixed))
     j0 = 3
     layers = [{}] * C
     layers[j0] = {"temperature": 2.0, "top_k": 1000, "top_p": 1.0}

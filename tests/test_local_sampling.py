@@ -163,6 +163,13 @@ def test_device_pick_greedy_and_top1():
     N.check(N.load().mtts_k_local_pick(P(logits), 1025, 1025, 2, P(seen), P(out), C, R, A, 1.0, 1, 1.0, 1.0, 1, 0,
                                        None), "pick")
     assert np.isin(out[:, 2].cpu().numpy(), [100, 200]).all()  # TopKLogitsWarper keeps ties
+    # top_p 0.3 over the tie (p = 0.5 each): the ascending walk drops the lower index (cum 0.5 <= 0.7)
+    # and keeps the higher -- the oracle's stable-argsort order, torch.sort's on these rows
+    want = L.hf_pick_distribution(x, hist, 2, 1.0, 1, 0.3, 1.0)
+    assert np.nonzero(want)[0].tolist() == [200]
+    N.check(N.load().mtts_k_local_pick(P(logits), 1025, 1025, 2, P(seen), P(out), C, R, A, 1.0, 1, 0.3, 1.0, 1, 0,
+                                       None), "pick")
+    assert (out[:, 2].cpu() == 200).all()
 
 
 @pytest.mark.gpu
