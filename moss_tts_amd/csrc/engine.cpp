@@ -535,6 +535,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     pa.L = e->pse_L; pa.layers = st.layers; pa.h = st.h; pa.ss = st.ss; pa.cos_t = st.cos_t; pa.sin_t = st.sin_t;
     pa.mask = st.mask; pa.pos = pos_base; pa.Cmax = st.Cmax; pa.eps = e->c.rms_eps;
     pa.scale = 1.0f / std::sqrt((float)D);
+    pa.trace = e->pse_trace;
     HIPCHK(pse4_decode(pa, e->pse4_ws, s, e->pse_coop));
     return 0;
   }

@@ -33,7 +33,7 @@ constexpr int THREADS = (LW + CW) * 64;
 #define PSE4_NS 5
 #endif
 #ifndef PSE4_RC
-#define PSE4_RC 0  // ring slots a plain CU's consumer waves drain into registers during the attention wait
+#define PSE4_RC 2  // ring slots a plain CU's consumer waves drain into registers during the attention wait
 #endif
 constexpr int NS = PSE4_NS;
 constexpr int SLOT_KB = 16;
@@ -53,6 +53,14 @@ __device__ __forceinline__ uint32_t ld32(const void* p) {
 __device__ __forceinline__ void st32(void* p, uint32_t v) {
   __hip_atomic_store((g32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// trace (MTTS_PSE_TRACE=1, scripts/pse4_trace.py): consumer wave 1 per layer -- 0 start, 1 q|k|v input
+// normed, 2 q|k|v done, 3 attention done (attention CUs), 4 o input, 5 o done, 6 gate|up input normed,
+// 7 gate|up rounds 0-1 done, 8 act round 0 in (+ round 2), 9 round 1 in (+ down 0-7), 10 round 2 in
+// (+ down 8-15), 11 down done; loader 12-15 first q|k|v / o / gate|up / down slot issued
+#define P4_STAMP(l, ev)                                                                         \
+  do {                                                                                          \
+    if (a.trace && lane == 0) a.trace[((size_t)(l) * PSE_TRACE_EV + (ev)) * 256 + c] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 __device__ __forceinline__ uint64_t gran(uint32_t payload, uint32_t tag) { return (uint64_t)tag << 32 | payload; }
 __device__ __forceinline__ uint32_t tagof(uint32_t epoch, int l, int op) { return epoch << 8 | (uint32_t)(l * 5 + op); }
 
@@ -190,22 +198,25 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   __builtin_amdgcn_s_setprio(3);
   bool ok = true;
   uint32_t lo[MAXP], hi[MAXP];
+  // one lane offset (tid * 8) for every granule i: i's 2 KiB stride rides in the SGPR offset, so a
+  // gather site keeps no per-granule offset registers live across the layer loop (MAXP = 36 of
+  // them spilled the consumers' registers)
+  const uint32_t vo = (uint32_t)x.tid * 8u;
   auto issue = [&]() {
 #pragma unroll
     for (int i = 0; i < MAXP; ++i) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (pend >> i & 1ull) ? (uint32_t)(x.tid + i * CW * 64) * 8u : OOB,
-                                                          0, 16 /* sc1 */);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (pend >> i & 1ull) ? vo : OOB, i * CW * 64 * 8, 16 /* sc1 */);
       lo[i] = v[0];
       hi[i] = v[1];
     }
   };
+  // (n0 % 256 == 0: granule i of every thread goes to the same destination)
   auto take = [&]() {
 #pragma unroll
     for (int i = 0; i < MAXP; ++i)
       if ((pend >> i & 1ull) && hi[i] == t) {
-        const int j = x.tid + i * CW * 64;
-        if (j < n0) dst0[j] = lo[i];
-        else dst1[j - n0] = lo[i];
+        if (i * CW * 64 < n0) dst0[x.tid + i * CW * 64] = lo[i];
+        else dst1[x.tid + i * CW * 64 - n0] = lo[i];
         pend &= ~(1ull << i);
       }
   };
@@ -254,7 +265,7 @@ __device__ __forceinline__ NormW norm_w(const Ctx& x, const bf16_t* w) {
   const u32x4* wv = reinterpret_cast<const u32x4*>(w);
   return NormW{wv[x.tid], wv[x.tid + 256]};
 }
-__device__ void norm_stage(Ctx& x, NormW nw) {
+__device__ __forceinline__ void norm_stage(Ctx& x, NormW nw) {
   const float* ss = reinterpret_cast<const float*>(p4_lds + L_MISC);
   float r[NB];
 #pragma unroll
@@ -647,6 +658,11 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
     const uint32_t ring0 = (uint32_t)(uintptr_t)(lvoid*)(lds + L_RING) + voff;
     auto src_of = [&](int s0) -> const void* {
       const int s = min(s0, total - 1);
+      if (a.trace && lane == 0 && s0 < total) {
+        const int l = s / spl, r = s - l * spl, rq = 4 * nq;
+        const int ev = r == 0 ? 12 : (r == rq ? 13 : (r == rq + 8 ? 14 : (r == rq + 56 ? 15 : -1)));
+        if (ev >= 0) a.trace[((size_t)l * PSE_TRACE_EV + ev) * 256 + c] = __builtin_amdgcn_s_memrealtime();
+      }
       if (s0 < total)  // this CU's attention is gathering its inputs: no new loads
         for (uint32_t spins = 0; __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
                                  !__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
@@ -787,6 +803,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         const PseLayer& Lw = a.L[l];
         constexpr int RC = ATT ? 0 : PSE4_RC;
         NormW nw;
+        if (wave == LW) P4_STAMP(l, 0);
         // ---------------- q|k|v (input RMSNorm fused) ----------------
         if (l == 0) {  // the embedding rows and their sums of squares (previous launch)
           nw = norm_w(x, Lw.in_norm);
@@ -801,6 +818,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           break;
         }
         norm_stage(x, nw);
+        if (wave == LW) P4_STAMP(l, 1);
         const uint32_t tq = tagof(epoch, l, OP_QKV);
 #pragma unroll 1
         for (int j = 0; j < (ATT ? 2 : nq); ++j) {
@@ -818,6 +836,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
         }
+        if (wave == LW) P4_STAMP(l, 2);
         // ---------------- attention (32 units: one per row and KV head) ----------------
         if constexpr (ATT) {
           const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.err, a.eps, a.scale,
@@ -826,12 +845,14 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           if (att_ok) x.bar_gen = bg;
           if (x.tid == 0) __hip_atomic_store(&P4_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (!att_ok) break;
+          if (wave == LW) P4_STAMP(l, 3);
         }
         // ---------------- o_proj (+ residual) ----------------
         SlotCache<RC> co;
         if (!gather<32>(x, a.g_att, NG_ATT, tagof(epoch, l, OP_ATT), xa32, NG_ATT, nullptr, NoHook(),
                         [&]() { co.drain(x, seq); }))
           break;
+        if (wave == LW) P4_STAMP(l, 4);
         {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -845,11 +866,13 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
         }
+        if (wave == LW) P4_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
         if (!gather<36>(x, a.g_h[0], NG_H + NG_SS, tagof(epoch, l, OP_O), xa32, NG_H, ss32,
                         [&]() { nw = norm_w(x, Lw.post_norm); }))
           break;
         norm_stage(x, nw);
+        if (wave == LW) P4_STAMP(l, 6);
         const uint32_t tg = tagof(epoch, l, OP_GU);
         auto gu_round = [&](int j) {
           f32x4 ag = (f32x4){0.f, 0.f, 0.f, 0.f}, au = ag;
@@ -873,6 +896,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         };
         gu_round(0);
         gu_round(1);
+        if (wave == LW) P4_STAMP(l, 7);
         // round 0's columns -> region B while round 2 runs on region A's normed input
         if (!gather<32>(x, a.g_act, NG_ACT_ROUND, tg, xb32, NG_ACT_ROUND, nullptr, [&]() {
               __builtin_amdgcn_s_setprio(0);
@@ -880,6 +904,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
               __builtin_amdgcn_s_setprio(3);
             }))
           break;
+        if (wave == LW) P4_STAMP(l, 8);
         // ---------------- down (+ residual) ----------------
         {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -894,9 +919,11 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           if (!gather<32>(x, a.g_act + NG_ACT_ROUND, NG_ACT_ROUND, tg, xa32, NG_ACT_ROUND, nullptr,
                           [&]() { slots(0, L_XB); }))
             break;
+          if (wave == LW) P4_STAMP(l, 9);
           if (!gather<32>(x, a.g_act + 2 * NG_ACT_ROUND, NG_ACT_ROUND, tg, xb32, NG_ACT_ROUND, nullptr,
                           [&]() { slots(8, L_XA); }))
             break;
+          if (wave == LW) P4_STAMP(l, 10);
 #pragma unroll 1
           for (int k = 16; k < 24; ++k) consume_slot(x, seq++, L_XB, (k - 16) * 16, acc);
           __builtin_amdgcn_s_setprio(3);
@@ -906,6 +933,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
         }
+        if (wave == LW) P4_STAMP(l, 11);
       }
       // the final residual rows and their sums of squares for the heads (plain stores: the next launch)
       if (wave == LW) a.h[(size_t)ecol * H_ + c * 16 + erow] = f2bf(hres);
