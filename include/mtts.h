@@ -121,6 +121,9 @@ int mtts_heads_ld(const mtts_engine* eng);
 int mtts_pse_active(const mtts_engine* eng);
 /* the same for batch-4 decode steps (configs[2]'s per-GPU share: pse4.hip; MTTS_PSE4=0 turns it off) */
 int mtts_pse4_active(const mtts_engine* eng);
+/* 1 when batch-1 steps past mtts_pse_ctx_max take the launch's long-context form (every CU scores a
+ * slice of each KV head's cached keys, merge units combine them; MTTS_PSE_LONG=0: per-op launches) */
+int mtts_pse_long_active(const mtts_engine* eng);
 int mtts_pse_ctx_max(const mtts_engine* eng);
 /* Fault injection (tests): mark the persistent launch's error word as if a wait had timed out.
  * The next check (a teacher-forced batch-1 forward, or mtts_generate_poll) takes the fallback:

@@ -77,6 +77,7 @@ _SIGS = {
     "mtts_heads_ld": (I, [P]),
     "mtts_pse_active": (I, [P]),
     "mtts_pse4_active": (I, [P]),
+    "mtts_pse_long_active": (I, [P]),
     "mtts_pse_ctx_max": (I, [P]),
     "mtts_pse_inject_timeout": (I, [P]),
     "mtts_pse_check": (I, [P]),

@@ -164,6 +164,7 @@ extern "C" int mtts_engine_create(const mtts_config* cfg, int device, mtts_engin
   if (const char* v = getenv("MTTS_PSE_CTX")) e->pse_ctx_max = atoi(v);
   if (const char* v = getenv("MTTS_PSE_COOP")) e->pse_coop = v[0] == '1';
   if (const char* v = getenv("MTTS_PSE4")) e->pse4 = v[0] == '1';
+  if (const char* v = getenv("MTTS_PSE_LONG")) e->pse_long = v[0] == '1';
   if (const char* v = getenv("MTTS_ATTN_LONG")) e->attn_long_ctx = atoi(v);
   if (const char* v = getenv("MTTS_XPACK")) e->xpack = v[0] == '1';
   if (const char* v = getenv("MTTS_SPLITK")) e->splitk = v[0] == '1';
@@ -250,6 +251,7 @@ uint32_t* mtts_engine::pse_err(int B) const {
 }
 extern "C" int mtts_pse_active(const mtts_engine* e) { return e && e->pse && e->pse_ok ? 1 : 0; }
 extern "C" int mtts_pse4_active(const mtts_engine* e) { return e && e->pse_takes(4) ? 1 : 0; }
+extern "C" int mtts_pse_long_active(const mtts_engine* e) { return e && e->pse_takes(1) && e->pse_long ? 1 : 0; }
 extern "C" int mtts_pse_inject_timeout(mtts_engine* e) {
   if (!e || !e->pse_ws) return fail(MTTS_E_INVALID, "no persistent launch state");
   hipSetDevice(e->device);
@@ -517,7 +519,8 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   const int M = B * S;
   const int NT = H / 16;  // per-row sum-of-squares partials (one per 16-column tile)
   const float eps = e->c.rms_eps;
-  if (S == 1 && B == 1 && b0 == 0 && e->pse && e->pse_ok && e->pse_now && st.cos_t && st.L == e->L.data()) {
+  if (S == 1 && B == 1 && b0 == 0 && e->pse && e->pse_ok && (e->pse_now || e->pse_long_now) && st.cos_t &&
+      st.L == e->L.data()) {
     // the whole stack as one persistent launch with run-ahead weight streaming (pse.hip)
     PseArgs pa{};
     pa.L = e->pse_L; pa.layers = st.layers; pa.h = st.h; pa.ss = st.ss; pa.cos_t = st.cos_t; pa.sin_t = st.sin_t;
@@ -526,7 +529,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     pa.trace = e->pse_trace;
     static const int pse_probe = getenv("MTTS_PSE_PROBE") ? atoi(getenv("MTTS_PSE_PROBE")) : 0;
     pa.probe = pse_probe;
-    HIPCHK(pse_decode(pa, e->pse_ws, s, e->pse_coop));
+    HIPCHK(pse_decode(pa, e->pse_ws, s, e->pse_coop, !e->pse_now));
     return 0;
   }
   if (S == 1 && B == 4 && b0 == 0 && e->pse_takes(4) && e->pse_now && st.cos_t && st.L == e->L.data()) {
@@ -790,7 +793,7 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   e->pse_choose(past + S);
   e->long_now = e->attn_long_ctx > 0 && past + S > e->attn_long_ctx;
   int rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
-  if (!rc && S == 1 && e->pse_takes(B) && e->pse_now && e->pse_err(B)) {
+  if (!rc && S == 1 && e->pse_takes(B) && (e->pse_now || (B == 1 && e->pse_long_now)) && e->pse_err(B)) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cs));
     if (cs == hipStreamCaptureStatusNone) {  // (inside a caller's capture: mtts_pse_check reads the word)
@@ -906,8 +909,8 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
   // every step-dependent value is read from device state, so one graph serves all steps --
   // one per path: the persistent streaming launch (pse.hip) while the context stays in its
   // range, the per-op launches beyond (the choice is per step, from the host's step count)
-  auto graph_for = [&](bool pse, bool lng, hipGraphExec_t* exec) -> int {
-    const int key = e->gen_B * 4 + (lng ? 2 : 0) + (pse ? 1 : 0);
+  auto graph_for = [&](bool pse, bool lng, bool plong, hipGraphExec_t* exec) -> int {
+    const int key = e->gen_B * 8 + (plong ? 4 : 0) + (lng ? 2 : 0) + (pse ? 1 : 0);
     auto it = e->graphs.find(key);
     if (it != e->graphs.end() && it->second.forced == e->forced) {
       *exec = it->second.exec;
@@ -918,6 +921,7 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
       e->graphs.erase(it);
     }
     e->pse_now = pse;
+    e->pse_long_now = plong;
     e->long_now = lng;
     hipGraph_t graph;
     HIPCHK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
@@ -927,16 +931,18 @@ extern "C" int mtts_generate_decode(mtts_engine* e, int n_steps, void* stream) {
     if (ce != hipSuccess) return fail(MTTS_E_HIP, std::string("capture: ") + hipGetErrorString(ce));
     HIPCHK(hipGraphInstantiate(exec, graph, nullptr, nullptr, 0));
     hipGraphDestroy(graph);
-    e->graphs[key] = mtts_engine::Graph{*exec, e->forced, pse};
+    e->graphs[key] = mtts_engine::Graph{*exec, e->forced, pse || plong};
     return 0;
   };
   for (int i = 0; i < n_steps && e->steps_issued < e->gen_max_new; ++i) {
     // context of this step <= prompt + steps so far + 1
     const int ctx = e->gen_T + e->steps_issued + 1;
     const bool pse = e->pse_takes(e->gen_B) && ctx <= e->pse_ctx_max;
-    const bool lng = !pse && e->gen_B == 1 && e->attn_long_ctx > 0 && ctx > e->attn_long_ctx;
+    // batch 1 past the short form's range: the launch's all-CU attention form
+    const bool plong = !pse && e->gen_B == 1 && e->pse_takes(1) && e->pse_long;
+    const bool lng = !pse && !plong && e->gen_B == 1 && e->attn_long_ctx > 0 && ctx > e->attn_long_ctx;
     hipGraphExec_t exec = nullptr;
-    if (int rc = graph_for(pse, lng, &exec)) return rc;
+    if (int rc = graph_for(pse, lng, plong, &exec)) return rc;
     HIPCHK(hipGraphLaunch(exec, s));
     ++e->steps_issued;
   }
@@ -1111,7 +1117,9 @@ extern "C" int mtts_engine_time_gemv(mtts_engine* e, int which, int layer, int B
     hipEvent_t a, b;
     HIPCHK(hipEventCreate(&a));
     HIPCHK(hipEventCreate(&b));
-    e->pse_now = true;
+    e->pse_choose(pos + 1);  // the form a decode step at this context takes (batch 1: short or long)
+    if (B == 4) e->pse_now = true;
+    if (B == 1 && !e->pse_now && !e->pse_long_now) return fail(MTTS_E_UNSUPPORTED, "no persistent form at this context");
     if (int rc = run_layers(e, st, 0, B, 1, e->d_pos, CH_DECODE, n_split, s)) return rc;
     HIPCHK(hipEventRecord(a, s));
     for (int i = 0; i < iters; ++i)

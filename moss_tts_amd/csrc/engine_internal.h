@@ -105,7 +105,14 @@ struct mtts_engine {
   // 3.74 -> 3.59 ms/step, but 2 K keys 3.33 -> 3.49 (too few blocks), hence the switch
   int attn_long_ctx = 4096;
   bool long_now = false;         // this forward / captured decode step takes the long form
-  void pse_choose(int ctx) { pse_now = ctx <= pse_ctx_max; }
+  // batch-1 contexts past pse_ctx_max: the launch's all-CU attention form (pse.hip, round 4;
+  // MTTS_PSE_LONG=0: the per-op launches there, as before)
+  bool pse_long = true;
+  bool pse_long_now = false;
+  void pse_choose(int ctx) {
+    pse_now = ctx <= pse_ctx_max;
+    pse_long_now = !pse_now && pse_long;
+  }
   bool pse_ok = false;           // the shape and the device support it
   // batch-4 form (pse4.hip, configs[2]'s per-GPU share): MTTS_PSE4=0 turns it off (A/B)
   bool pse4 = true;
@@ -134,7 +141,7 @@ struct mtts_engine {
   float* part_val = nullptr;
   const int* forced = nullptr;
   int gen_B = 0, gen_T = 0, gen_max_new = 0, steps_issued = 0;
-  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };  // key: 4 B + 2 long + pse
+  struct Graph { hipGraphExec_t exec; const int* forced; bool pse; };  // key: 8 B + 4 pse-long + 2 long + pse
   std::unordered_map<int, Graph> graphs;  // decode-step graph per batch size
   std::vector<void*> allocs;      // weights
   std::vector<void*> cap_allocs;  // capacity buffers (see alloc_capacity)

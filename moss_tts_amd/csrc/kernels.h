@@ -269,6 +269,7 @@ struct PseArgs {
   float eps, scale;
   // workspace (set by pse_decode): granules and words
   uint64_t *g_qkv, *g_att, *g_h[2], *g_ss[2], *g_act;
+  uint64_t* g_part;   // long-context form: per-slice attention partials [q head][half][slice][66]
   uint32_t *err, *epoch, *exit_cnt;
   uint64_t* trace;  // nullptr, or [layers][PSE_TRACE_EV][256] s_memrealtime stamps
   int probe;        // timing probe (MTTS_PSE_PROBE; results invalid): 1 loader issues no DMA,
@@ -281,7 +282,9 @@ bool pse_supported(int device, int B, int layers, int H, int Hq, int Hkv, int D,
 size_t pse_ws_bytes();  // zero-filled once by the owner
 // coop: hipLaunchCooperativeKernel (the runtime checks the grid's co-residency at launch and
 // refuses it with hipErrorCooperativeLaunchTooLarge) instead of a plain launch
-hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s, bool coop = false);
+// long_ctx: the all-CU attention form (every CU scores 1/32 of a KV head's cached keys, 64 merge
+// units combine the slices) for contexts past the 2-CU-per-head form's range
+hipError_t pse_decode(const PseArgs& a, void* ws, hipStream_t s, bool coop = false, bool long_ctx = false);
 uint32_t* pse_err_word(void* ws);
 // pse4.hip: the same for a decode batch of exactly 4 rows (configs[2]'s per-GPU share); PseArgs as
 // above with h [4][H], ss [4][H/16], mask [4][Cmax] (rows 0-3), the caches' rows 0-3

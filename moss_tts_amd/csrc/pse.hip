@@ -172,6 +172,8 @@ constexpr int L_ATT = L_GRAW + 1536 * 4;
 static_assert(L_ATT + 16 * D_ * 2 + 2 * D_ * 4 + CW * 16 * 32 * 2 + CW * G_ * 2 * 4 + CW * G_ * D_ * 4 <= L_RED,
               "attention scratch fits the op input region");
 static_assert(L_END <= 160 * 1024, "LDS");
+// (long form) the merge unit's 32 slice partials (2,112 words) over the slice's p_s / ml_s / acc_s
+static_assert(L_ATT + 16 * D_ * 2 + 2 * D_ * 4 + 2112 * 4 <= L_RED, "merge partials fit the op input region");
 
 }  // namespace
 
@@ -791,10 +793,353 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   return x.bar_gen;
 }
 
+
+// ---------------------------------------------------------------------------
+// Long-context form (pse_kernel_t<true>, contexts past the 2-CU-per-head form's range; round 4).
+// The short form's attention units each read EVERY cached key of their head, so the chain grows
+// with the context (the launch lost to the per-op split attention past ~800 keys).  Here every CU
+// takes a slice: CU c scores the cached keys of KV head g = c % 8 in its 1/32 share (s = c / 8) of
+// the 32-key chunks, all 4 q heads of the group at once, and publishes its (m, l, o) partials;
+// 64 merge units (q head, half of the dims) combine the 32 slices with the new key (score q . k,
+// p = 1) and append k / v.  The chain: q gather -> the slice's K / V (1/256 of the layer's cache
+// per CU, every CU's loader paused so the reads do not queue behind the weight stream) -> partial
+// hop -> merge -> the o gather: about the short form's length at any context.
+constexpr int LS = 32;                               // slices per KV head
+constexpr int PART_W = 2 + D_ / 2;                   // granules per (q head, half, slice): m, l, 64 dims
+constexpr int NG_PART = HQ_ * 2 * LS * PART_W;       // 135,168
+constexpr int L_STASH = L_MISC;                      // merge inputs kept by the slice: k norm w, cos, sin, mask
+// merge unit u (q head u / 2, dim half u % 2) on the CU whose slice is slice 24 + u % 8 of KV head
+// u / 8: the unit reuses the q rows and k / v partials its own slice gathered; -1: none
+__host__ __device__ inline int pse_merge_unit(int c) {
+  const int sl = c / HKV_;
+  return sl >= LS - 8 ? (c % HKV_) * 8 + (sl - (LS - 8)) : -1;
+}
+
+// The slice of CU c = blockIdx.x: q rows of the group's 4 q heads (q|k|v granules grouped by KV head,
+// qkv_gran), then per-wave online softmax over the slice's chunks (pse.hip attention()'s chunk
+// math, HU = 4), the 4 wave partials merged, (m, l, o) published unnormalised.  A merge unit also
+// gathers the new token's k / v partials (behind its chunks) and stashes its merge inputs.
+__device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, const int* pos_p, const uint8_t* mask,
+                                                         const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
+                                                         uint64_t* g_part, uint32_t* err, float eps, float scale,
+                                                         int Cmax, uint32_t epoch, int bar_gen, int l, int merge,
+                                                         uint32_t tq) {
+  const int c = blockIdx.x;
+  Ctx x{err, eps, 0, c, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64, epoch, bar_gen};
+  constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = G_;
+  const int g = c % HKV_, sl = c / HKV_;
+  const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
+  uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
+  const PseLayer& Lw = *Lp;
+  const int pos = *pos_p;
+  const int lane = x.lane, w = x.wave - LW, g4 = lane >> 4, c16 = lane & 15;
+  const bf16_t* kcache = Lw.kc + (size_t)g * Cmax * D;
+  const bf16_t* vcache = Lw.vc + (size_t)g * D * Cmax;
+  bf16_t* q_s = reinterpret_cast<bf16_t*>(pse_lds + L_ATT);
+  float* k_s = reinterpret_cast<float*>(q_s + 16 * D);
+  float* v_s = k_s + D;
+  bf16_t* p_s = reinterpret_cast<bf16_t*>(v_s + D);
+  float* ml_s = reinterpret_cast<float*>(p_s + CW * 16 * KW);
+  float* acc_s = ml_s + CW * G * 2;
+  uint32_t* stash = reinterpret_cast<uint32_t*>(pse_lds + L_STASH);
+  constexpr uint32_t OOBA = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(kcache), 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(vcache), 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mask), 0, Cmax, 0x00020000);
+  // this slice's chunks of the cached keys 0 .. pos-1
+  const int nct = (pos + KW - 1) / KW, cb = sl * nct / LS, ce = (sl + 1) * nct / LS;
+  auto load_chunk = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
+    const int k0 = ch * KW;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = k0 + t * 16 + c16;
+#pragma unroll
+      for (int s2 = 0; s2 < QS; ++s2)
+        kt[t][s2] = __builtin_amdgcn_raw_buffer_load_b128(
+            krs, (key < pos && ch < ce) ? (uint32_t)(key * D + s2 * 32 + 8 * g4) * 2u : OOBA, 0, 0);
+      mk[t] = __builtin_amdgcn_raw_buffer_load_b32(
+          mrs, (k0 + t * 16 <= pos && ch < ce) ? (uint32_t)(k0 + t * 16 + g4 * 4) : OOBA, 0, 0);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int kb = k0 + 8 * g4;
+      vt[dt] = __builtin_amdgcn_raw_buffer_load_b128(
+          vrs, (kb < pos && ch < ce) ? (uint32_t)((dt * 16 + c16) * Cmax + kb) * 2u : OOBA, 0, 0);
+    }
+  };
+  u32x4 ktA[2][QS], vtA[DT];
+  uint32_t mkA[2];
+  const int ch0 = cb + w;
+  uint32_t qnw = 0, knw = 0, pcs = 0, psn = 0, mnew = 0;
+  auto prefetch = [&]() {
+    load_chunk(ch0, ktA, vtA, mkA);
+    qnw = reinterpret_cast<const uint32_t*>(Lw.q_norm)[lane];
+    pcs = reinterpret_cast<const uint32_t*>(cos_t + (size_t)pos * D)[lane];
+    psn = reinterpret_cast<const uint32_t*>(sin_t + (size_t)pos * D)[lane];
+    if (merge) {
+      knw = reinterpret_cast<const uint32_t*>(Lw.k_norm)[lane];
+      mnew = mask[pos];
+    }
+  };
+  auto val = [&](int base_tile, int i) {
+    const float* p = graw + (base_tile + i / 16) * 32 + i % 16;
+    return rbf(p[0] + p[16]);
+  };
+  auto norm_rope = [&](float x0, float x1, uint32_t nw, float& o0, float& o1) {
+    const float ss = wave_sum(x0 * x0 + x1 * x1);
+    const float r = 1.0f / sqrtf(ss / (float)D + eps);
+    const float n0 = rbf(__uint_as_float(nw << 16) * rbf(x0 * r)), n1 = rbf(__uint_as_float(nw & 0xffff0000u) * rbf(x1 * r));
+    constexpr int q4 = D / 4;
+    const bool lo = 2 * lane < D / 2;
+    const int partner = lo ? lane + q4 : lane - q4;
+    const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
+    const float sg = lo ? -1.f : 1.f;
+    const float c0 = __uint_as_float(pcs << 16), c1 = __uint_as_float(pcs & 0xffff0000u);
+    const float s0 = __uint_as_float(psn << 16), s1 = __uint_as_float(psn & 0xffff0000u);
+    o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
+    o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+  };
+  if (x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  constexpr int NG = (G_ + 2) * (D_ / 16) * 32;
+  constexpr int NQ = HU * (D_ / 16) * 32, NKV = 2 * (D_ / 16) * 32;
+  if (!gather<(NQ + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG, NQ, tq, graw32, NQ, nullptr, prefetch))
+    return -1;
+  if (merge && w == 0) {  // the merge's inputs, read back after this slice's scratch is reused
+    stash[lane] = knw;
+    stash[64 + lane] = pcs;
+    stash[128 + lane] = psn;
+    if (lane == 0) stash[192] = mnew;
+  }
+  {
+    const int bt = w * (D / 16);
+    float o0, o1;
+    norm_rope(val(bt, 2 * lane), val(bt, 2 * lane + 1), qnw, o0, o1);
+    q_s[w * D + 2 * lane] = f2bf(o0);
+    q_s[w * D + 2 * lane + 1] = f2bf(o1);
+  }
+  for (int i = x.tid; i < 16 * D; i += CW * 64)
+    if (i / D >= HU) q_s[i] = 0;
+  cbar(x);
+  float m_run = -INFINITY, l_run = 0.f;
+  float o_run[DT][HU];
+#pragma unroll
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
+  auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
+    const int k0 = ch * KW;
+    {
+      const int nv = pos - (k0 + 8 * g4);  // V^T lanes of keys >= pos: zeroed (pse.hip attention())
+      uint32_t vm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vt[dt][q] &= vm[q];
+    }
+    f32x4 sacc[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int s2 = 0; s2 < QS; ++s2)
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][s2]),
+                                                         *reinterpret_cast<const bf16x8*>(&q_s[c16 * D + s2 * 32 + 8 * g4]),
+                                                         sacc[t], 0, 0, 0);
+    }
+    float sv[2][4], mc = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + t * 16 + g4 * 4 + r;
+        const bool valid = key < pos && ((mk[t] >> (8 * r)) & 0xffu);
+        sv[t][r] = valid ? sacc[t][r] * scale : -INFINITY;
+        mc = fmaxf(mc, sv[t][r]);
+      }
+    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
+    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    float lc = 0.f;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      float pr4[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
+        lc += p;
+        pr4[r] = p;
+      }
+      uint2 pk;
+      pk.x = pack2(pr4[0], pr4[1]);
+      pk.y = pack2(pr4[2], pr4[3]);
+      *reinterpret_cast<uint2*>(&p_s[(w * 16 + c16) * KW + t * 16 + g4 * 4]) = pk;
+    }
+    lc += __shfl_xor(lc, 16, 64);
+    lc += __shfl_xor(lc, 32, 64);
+    const float mn = fmaxf(m_run, mc);
+    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
+    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
+    l_run = l_run * alpha + lc * beta;
+    m_run = mn;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
+    float al[HU], be[HU];
+#pragma unroll
+    for (int r = 0; r < HU; ++r) {
+      al[r] = __shfl(alpha, r, 64);
+      be[r] = __shfl(beta, r, 64);
+    }
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
+                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < HU; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  };
+  auto chunks = [&]() {
+    for (int ch = ch0; ch < ce; ch += CW) {
+      if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
+      compute(ch, ktA, vtA, mkA);
+    }
+  };
+  if (merge) {  // the new token's k / v partials, gathered behind this slice's chunks
+    if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + NQ, NKV, tq, graw32 + NQ, NKV, nullptr,
+                                                 chunks))
+      return -1;
+  } else {
+    chunks();
+  }
+  if (lane < HU) {
+    ml_s[(w * HU + lane) * 2] = m_run;
+    ml_s[(w * HU + lane) * 2 + 1] = l_run;
+  }
+  if (g4 == 0)
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < HU; ++r) acc_s[(w * HU + r) * D + dt * 16 + c16] = o_run[dt][r];
+  cbar(x);
+  // the 4 wave partials -> the slice's (m, l, o) of q head h (thread: 2 dims)
+  {
+    const int e = 2 * x.tid, h = e / D, d = e % D;
+    float M = -INFINITY;
+#pragma unroll
+    for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
+    float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < CW; ++ww) {
+      const float mw = ml_s[(ww * HU + h) * 2];
+      const float f = (mw == -INFINITY) ? 0.f : expf(mw - M);
+      L += f * ml_s[(ww * HU + h) * 2 + 1];
+      o0 += f * acc_s[(ww * HU + h) * D + d];
+      o1 += f * acc_s[(ww * HU + h) * D + d + 1];
+    }
+    const uint32_t tg = tagof(x.epoch, l, OP_ATT);
+    uint64_t* pp = g_part + ((size_t)((g * G + h) * 2 + d / (D / 2)) * LS + sl) * PART_W;
+    st64(pp + 2 + d % (D / 2), gran(__float_as_uint(o0), tg));
+    st64(pp + 3 + d % (D / 2), gran(__float_as_uint(o1), tg));
+    if (d % (D / 2) == 0) {
+      st64(pp, gran(__float_as_uint(M), tg));
+      st64(pp + 1, gran(__float_as_uint(L), tg));
+    }
+  }
+  cbar(x);
+  return x.bar_gen;
+}
+
+// Merge unit u: q head hq = u / 2, dims [64 (u % 2), +64): the 32 slices' partials plus the new key
+// (score q . k, p = 1: TF/integrations/sdpa_attention.py:79-166 over keys 0..pos), k RMSNorm + RoPE,
+// k / v appended by the group's first unit (TF/cache_utils.py:127-145), the output published as
+// the o_proj input granules.  q_s / graw / the stash still hold this CU's slice inputs.
+__device__ __attribute__((noinline)) int attention_merge(const PseLayer* Lp, const int* pos_p, uint64_t* g_part,
+                                                         uint64_t* g_att, uint32_t* err, float eps, float scale,
+                                                         int Cmax, uint32_t epoch, int bar_gen, int l, int u) {
+  const int c = blockIdx.x;
+  Ctx x{err, eps, 0, c, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64, epoch, bar_gen};
+  constexpr int D = D_, G = G_;
+  const int hq = u / 2, half = u % 2, g = hq / G, hl = hq % G;
+  const int lane = x.lane, w = x.wave - LW;
+  const int pos = *pos_p;
+  const PseLayer& Lw = *Lp;
+  const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
+  const bf16_t* q_s = reinterpret_cast<const bf16_t*>(pse_lds + L_ATT);
+  float* k_s = reinterpret_cast<float*>(pse_lds + L_ATT + 16 * D * 2);
+  float* v_s = k_s + D;
+  uint32_t* pb32 = reinterpret_cast<uint32_t*>(v_s + D);  // the slices' partials (over the slice's p_s / acc_s)
+  const float* pb = reinterpret_cast<const float*>(pb32);
+  const uint32_t* stash = reinterpret_cast<const uint32_t*>(pse_lds + L_STASH);
+  auto val = [&](int base_tile, int i) {
+    const float* p = graw + (base_tile + i / 16) * 32 + i % 16;
+    return rbf(p[0] + p[16]);
+  };
+  const bool app = hl == 0 && half == 0;
+  if (w == 0) {  // k: RMSNorm + RoPE (pse.hip attention() step 3)
+    const uint32_t knw = stash[lane], pcs = stash[64 + lane], psn = stash[128 + lane];
+    const float x0 = val(G * (D / 16), 2 * lane), x1 = val(G * (D / 16), 2 * lane + 1);
+    const float ss = wave_sum(x0 * x0 + x1 * x1);
+    const float r = 1.0f / sqrtf(ss / (float)D + eps);
+    const float n0 = rbf(__uint_as_float(knw << 16) * rbf(x0 * r)), n1 = rbf(__uint_as_float(knw & 0xffff0000u) * rbf(x1 * r));
+    constexpr int q4 = D / 4;
+    const bool lo = 2 * lane < D / 2;
+    const int partner = lo ? lane + q4 : lane - q4;
+    const float p0 = __shfl(n0, partner, 64), p1 = __shfl(n1, partner, 64);
+    const float sg = lo ? -1.f : 1.f;
+    const float c0 = __uint_as_float(pcs << 16), c1 = __uint_as_float(pcs & 0xffff0000u);
+    const float s0 = __uint_as_float(psn << 16), s1 = __uint_as_float(psn & 0xffff0000u);
+    const float o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0)), o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
+    k_s[2 * lane] = o0;
+    k_s[2 * lane + 1] = o1;
+    if (app) *reinterpret_cast<uint32_t*>(Lw.kc + (size_t)g * Cmax * D + (size_t)pos * D + 2 * lane) = pack2(o0, o1);
+  } else if (w == 1) {
+    const float x0 = val((G + 1) * (D / 16), 2 * lane), x1 = val((G + 1) * (D / 16), 2 * lane + 1);
+    v_s[2 * lane] = x0;
+    v_s[2 * lane + 1] = x1;
+    if (app) {
+      bf16_t* vcache = Lw.vc + (size_t)g * D * Cmax;
+      vcache[(size_t)(2 * lane) * Cmax + pos] = f2bf(x0);
+      vcache[(size_t)(2 * lane + 1) * Cmax + pos] = f2bf(x1);
+    }
+  }
+  constexpr int NP = LS * PART_W;  // 2,112
+  if (!gather<(NP + CW * 64 - 1) / (CW * 64)>(x, g_part + (size_t)(hq * 2 + half) * NP, NP, tagof(epoch, l, OP_ATT), pb32, NP))
+    return -1;
+  // the new key's score q . k (every wave alike), then thread j < 32: dims 64 half + 2 j, +1
+  const float sn = wave_sum(bf2f(q_s[hl * D + 2 * lane]) * k_s[2 * lane] + bf2f(q_s[hl * D + 2 * lane + 1]) * k_s[2 * lane + 1]) * scale;
+  if (x.tid < D / 4) {
+    const int j = x.tid, d = half * (D / 2) + 2 * j;
+    const bool nv = stash[192] != 0u;
+    float M = nv ? sn : -INFINITY;
+    for (int s2 = 0; s2 < LS; ++s2) M = fmaxf(M, pb[s2 * PART_W]);
+    float L = 0.f, o0 = 0.f, o1 = 0.f;
+    for (int s2 = 0; s2 < LS; ++s2) {
+      const float ms = pb[s2 * PART_W];
+      const float f = (ms == -INFINITY) ? 0.f : expf(ms - M);
+      L += f * pb[s2 * PART_W + 1];
+      o0 += f * pb[s2 * PART_W + 2 + 2 * j];
+      o1 += f * pb[s2 * PART_W + 3 + 2 * j];
+    }
+    if (nv) {
+      const float f = expf(sn - M);
+      L += f;
+      o0 += f * v_s[d];
+      o1 += f * v_s[d + 1];
+    }
+    st64(g_att + (hq * D + d) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+  }
+  cbar(x);
+  return x.bar_gen;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
+template <bool LONG>
+__global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
   unsigned char* const lds = pse_lds;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int c = blockIdx.x, P = gridDim.x;
@@ -810,7 +1155,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
   }
   __syncthreads();
   const uint32_t epoch = (ld32(a.epoch) + 1u) & 0xffffffu;
-  const int nq = pse_nq(c, P), spl = 4 * nq + 80;  // this CU's q|k|v units, slots per layer
+  const int nq = LONG ? 3 : pse_nq(c, P), spl = 4 * nq + 80;  // this CU's q|k|v units, slots per layer
   const int total = a.layers * spl;
 
   if (wave < LW) {
@@ -957,14 +1302,16 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
     bf16_t* xs = reinterpret_cast<bf16_t*>(lds + L_XS);
     float* ssl = reinterpret_cast<float*>(lds + L_MISC);  // [256] gathered sums of squares
     constexpr int NT = H_ / 16;
-    const int att_u = pse_att_unit(c, P);
+    const int att_u = LONG ? -1 : pse_att_unit(c, P);
+    const int mrg_u = LONG ? pse_merge_unit(c) : -1;
     // The layer loop, instantiated twice: with the attention inlined (the 16 attention CUs) and
     // without it (the rest).  Each instance gets its own register allocation, so the attention's
     // chunk state neither spills the plain CUs' loop nor costs a call: as a noinline callee its
     // ~96 callee-saved VGPRs went to scratch and back every layer (98 KiB each way per CU, 2.8 us
     // of prologue on the attention chain, profiles/r03_n_pse_trace_t2.txt).
-    auto run = [&](auto att_c) __attribute__((always_inline)) {
+    auto run = [&](auto att_c, auto mrg_c) __attribute__((always_inline)) {
       constexpr bool ATT = decltype(att_c)::value;
+      constexpr bool MRG = decltype(mrg_c)::value;  // long form: this CU is a merge unit
       // residual columns 16c .. 16c+15 owned by this CU: lanes 0..15 of wave 1 (bf16 values)
       float hres = (wave == LW && lane < 16) ? bf2f(a.h[c * 16 + lane]) : 0.f;
       float hsq = 0.f;
@@ -995,7 +1342,8 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
         // loader run RC slots further ahead through the attention (the longest wait of the layer);
         // o_proj then runs those slots from registers.  (At the h gathers the same drain spilled
         // 44+ VGPRs even at 2 slots: not used there.)
-        constexpr int RC = ATT ? 0 : (PSE_RC < 8 ? PSE_RC : 8);
+        // (long form: 0 -- live across the slice call, the drained slots spill: 33 VGPRs at 2 slots)
+        constexpr int RC = (ATT || MRG || LONG) ? 0 : (PSE_RC < 8 ? PSE_RC : 8);
         NormW nw;
         auto load_nw = [&]() { nw = norm_w(x, Lw.in_norm); };
         if (l == 0) {  // the embedding row and its sums of squares (previous launch)
@@ -1043,6 +1391,20 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
           if (PSE_APAUSE == 2 && x.tid == 0)  // (PSE_APAUSE 2: the loader waits out the whole attention)
             __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
           if (!att_ok) break;
+          if (wave == LW) PSE_STAMP(l, 3);
+        }
+        if constexpr (LONG) {
+          // every CU: its slice of the KV head's cached keys; merge units then combine the slices
+          int bg = attention_slice(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_part, a.err, a.eps, a.scale,
+                                   a.Cmax, epoch, x.bar_gen, l, MRG ? 1 : 0, tq);
+          if (bg >= 0) x.bar_gen = bg;
+          if (MRG && bg >= 0) {
+            bg = attention_merge(a.L + l, a.pos, a.g_part, a.g_att, a.err, a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l,
+                                 mrg_u);
+            if (bg >= 0) x.bar_gen = bg;
+          }
+          if (x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (bg < 0) break;
           if (wave == LW) PSE_STAMP(l, 3);
         }
         // ---------------- o_proj (+ residual) ----------------
@@ -1136,8 +1498,13 @@ __global__ __launch_bounds__(THREADS) void pse_kernel(PseArgs a) {
       if (wave == LW && lane < 16) a.h[c * 16 + lane] = f2bf(hres);
       if (wave == LW && lane == 0) a.ss[c] = hsq;
     };
-    if (att_u >= 0) run(BoolC<true>{});
-    else run(BoolC<false>{});
+    if constexpr (LONG) {
+      if (mrg_u >= 0) run(BoolC<false>{}, BoolC<true>{});
+      else run(BoolC<false>{}, BoolC<false>{});
+    } else {
+      if (att_u >= 0) run(BoolC<true>{}, BoolC<false>{});
+      else run(BoolC<false>{}, BoolC<false>{});
+    }
   }
   // exit: the last workgroup out advances the epoch for the next launch
   __syncthreads();
@@ -1161,23 +1528,22 @@ bool pse_supported(int device, int B, int layers, int H, int Hq, int Hkv, int D,
 int pse_grid(int device) {
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, device) != hipSuccess) return 0;
-  if (hipFuncSetAttribute((const void*)pse_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pse_lds_bytes()) !=
-      hipSuccess)
-    return 0;
-  int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)pse_kernel, THREADS, pse_lds_bytes()) !=
-      hipSuccess || per_cu < 1)
-    return 0;
+  for (const void* k : {(const void*)pse_kernel_t<false>, (const void*)pse_kernel_t<true>}) {
+    if (hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)pse_lds_bytes()) != hipSuccess) return 0;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, THREADS, pse_lds_bytes()) != hipSuccess || per_cu < 1)
+      return 0;
+  }
   return p.multiProcessorCount;
 }
 
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2) * 8 + 64;
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + 64;
 }
 
-hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
+hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, bool long_ctx) {
   if (a0.layers < 1 || a0.layers > PSE_MAXL || a0.layers * 5 > 256 || a0.Cmax % 64) return hipErrorInvalidValue;
   PseArgs a = a0;
   uint64_t* g = reinterpret_cast<uint64_t*>(ws);
@@ -1189,13 +1555,16 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   a.g_h[1] = g; g += H_ / 2;
   a.g_ss[1] = g; g += H_ / 16;
   a.g_act = g; g += I_ / 2;
+  a.g_part = g; g += NG_PART;
   uint32_t* w = reinterpret_cast<uint32_t*>(g);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
+  const void* k = long_ctx ? (const void*)pse_kernel_t<true> : (const void*)pse_kernel_t<false>;
   if (coop) {
     void* args[] = {&a};
-    return hipLaunchCooperativeKernel((const void*)pse_kernel, dim3(256), dim3(THREADS), args, (unsigned)pse_lds_bytes(), s);
+    return hipLaunchCooperativeKernel(k, dim3(256), dim3(THREADS), args, (unsigned)pse_lds_bytes(), s);
   }
-  hipLaunchKernelGGL(pse_kernel, dim3(256), dim3(THREADS), pse_lds_bytes(), s, a);
+  if (long_ctx) hipLaunchKernelGGL(pse_kernel_t<true>, dim3(256), dim3(THREADS), pse_lds_bytes(), s, a);
+  else hipLaunchKernelGGL(pse_kernel_t<false>, dim3(256), dim3(THREADS), pse_lds_bytes(), s, a);
   return hipGetLastError();
 }
 

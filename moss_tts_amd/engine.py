@@ -141,6 +141,10 @@ class Engine:
         """Whether batch-4 decode steps run the decoder stack as one persistent launch (pse4.hip)."""
         return bool(N.load().mtts_pse4_active(self._h))
 
+    def pse_long_active(self) -> bool:
+        """Whether batch-1 steps past pse_ctx_max() run the launch's long-context (all-CU attention) form."""
+        return bool(N.load().mtts_pse_long_active(self._h))
+
     def pse_ctx_max(self) -> int:
         """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
         return int(N.load().mtts_pse_ctx_max(self._h))

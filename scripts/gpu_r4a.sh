@@ -1,0 +1,26 @@
+#!/bin/bash
+# Round 4 session A: the batch-4 launch (trace, same-box A/B of variants), the long-context form of
+# the batch-1 launch (parity tests, TTSD bench with the form on / off).  Writes gpurun_out/r4a/.
+set -u
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/r4a
+mkdir -p $O
+export TMPDIR=/tmp
+timeout -k 10 400 python -u -m pytest tests/test_ttsd_shape_gpu.py tests/test_pse_gpu.py tests/test_pse_oracle_gpu.py \
+    -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR|SKIPPED" $O/pytest.log | tail -30; tail -3 $O/pytest.log
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+timeout -k 10 300 python -u scripts/pse4_trace.py 8 181 > $O/pse4_trace.txt 2>&1
+rc=$?; echo "trace rc=$rc"; grep -v Warn $O/pse4_trace.txt; if [ $rc -ne 0 ]; then exit $rc; fi
+for lib in moss_tts_amd/lib/libmtts.so moss_tts_amd/lib/var/libmtts_rc0.so moss_tts_amd/lib/var/libmtts_ns4.so; do
+  MTTS_LIB=$lib timeout -k 10 300 python3 bench.py --batch 4 --steps 2 --warmup 1 --no-cpu-baseline --no-codec --no-dp-leg \
+      --no-roofline --extra-batches "" > $O/b4.json 2> $O/b4.err
+  rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -5 $O/b4.err; exit $rc; }
+  python3 -c "import json,sys; d=json.load(open('$O/b4.json')); print('$lib'.split('/')[-1], {k: d[k] for k in ('value','ms_per_decode_step','decode_step_hbm_frac')})"
+done
+for flag in 1 0; do
+  MTTS_PSE_LONG=$flag timeout -k 10 400 python3 bench.py --config ttsd --steps 1 --warmup 0 --no-cpu-baseline \
+      > $O/ttsd_long$flag.json 2> $O/ttsd_long$flag.err
+  rc=$?; [ $rc -eq 0 ] || { echo "ttsd long=$flag rc=$rc"; tail -5 $O/ttsd_long$flag.err; exit $rc; }
+  python3 -c "import json; d=json.load(open('$O/ttsd_long$flag.json')); print('ttsd pse_long=$flag', {k: d[k] for k in ('value','ms_per_decode_step','prefill_ms','decode_step_hbm_frac')}, d['roofline'] and {k: d['roofline'][k] for k in ('frac','avg_launch_us','kernel')})"
+done

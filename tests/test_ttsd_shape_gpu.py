@@ -4,8 +4,10 @@ cached keys, n_vq 16, the MossTTSDelay-8B layer shape, against the oracle.
 configs[4] decodes from 2,117 to 9,636 cached keys (`bench.py --config ttsd`); past 4,096 keys the
 engine's batch-1 decode takes 16-wave (512-key) attention blocks (MTTS_ATTN_LONG), i.e. ~19 blocks
 per KV head at 9,600 keys, whose (m, l, o) partials the last arriving block merges
-(attn_body.h).  The decode graphs of a TTSD generation capture exactly these launches; here they
-run as teacher-forced forwards so every step's logits can be compared.
+(attn_body.h) -- or, by default since round 4, the persistent launch's long-context form
+(pse.hip: every CU scores 1/32 of a KV head's cached keys, 64 merge units combine the slices).
+Both are pinned here (MTTS_PSE_LONG 1 / 0).  The decode graphs of a TTSD generation capture exactly
+these launches; here they run as teacher-forced forwards so every step's logits can be compared.
 
 The cache of the long context is written directly (`mtts_engine_kv_write`, the same bf16 K / V
 rows handed to the oracle's cache): the attention sees the same function of the past as after a
@@ -47,15 +49,12 @@ class DeviceRows:
 def setup():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from moss_tts_amd.engine import Engine, EngineConfig
     assert int(os.environ.get("MTTS_ATTN_LONG", "4096")) < T
-    eng = Engine(EngineConfig(layers=LAYERS, n_vq=NVQ, max_batch=1, max_ctx=T + 64, max_prefill_tokens=1024), 0)
     g = torch.Generator(device="cuda").manual_seed(16)
     Wd = {}
     for name, shape, kind in O.weight_specs(CFG):
         sc, off = O.scale_for(kind, shape)
         Wd[name] = (off + sc * (2 * torch.rand(shape, generator=g, device="cuda") - 1)).to(torch.bfloat16)
-    eng.load_state_dict(Wd)
     rng = np.random.default_rng(16)
     tile_lo = (min(CFG.im_end_token_id, CFG.audio_assistant_gen_slot_token_id,
                    CFG.audio_assistant_delay_slot_token_id) // 16) * 16
@@ -68,14 +67,30 @@ def setup():
             text_rows = t[torch.from_numpy(sel).cuda()].float().cpu().numpy()
         else:
             W[name] = t.float().cpu().numpy()
-    del Wd
-    torch.cuda.empty_cache()
-    yield eng, W, sel, text_rows
-    eng.close()
+    yield Wd, W, sel, text_rows
 
 
-def test_ttsd_long_context_decode_vs_oracle(setup):
-    eng, W, sel, text_rows = setup
+@pytest.mark.parametrize("pse_long", ["1", "0"])
+def test_ttsd_long_context_decode_vs_oracle(setup, pse_long):
+    from moss_tts_amd.engine import Engine, EngineConfig
+    Wd, W, sel, text_rows = setup
+    os.environ["MTTS_PSE_LONG"] = pse_long
+    try:
+        eng = Engine(EngineConfig(layers=LAYERS, n_vq=NVQ, max_batch=1, max_ctx=T + 64, max_prefill_tokens=1024), 0)
+    finally:
+        os.environ.pop("MTTS_PSE_LONG")
+    try:
+        eng.load_state_dict(Wd)
+        if pse_long == "1" and not eng.pse_long_active():
+            pytest.skip("persistent launch unsupported on this device")
+        assert pse_long == "1" or not eng.pse_long_active()
+        run_ttsd(eng, W, sel, text_rows)
+        eng.pse_check()
+    finally:
+        eng.close()
+
+
+def run_ttsd(eng, W, sel, text_rows):
     rng = np.random.default_rng(9600)
     ctx = O._Ctx("bf16")
     cache = O.KVCache(LAYERS)
@@ -115,4 +130,3 @@ def test_ttsd_long_context_decode_vs_oracle(setup):
             assert err <= 8 * ulp_bf16(scale), (s, j, float(err), float(scale))
             if margin_top2(wr) > 16 * float(ulp_bf16(scale)):
                 assert int(np.argmax(np.where(fin, gr, -np.inf))) == int(np.argmax(np.where(fin, wr, -np.inf))), (s, j)
-    assert not eng.pse_active() or eng.pse_ctx_max() < T  # the per-op long-context launches ran
