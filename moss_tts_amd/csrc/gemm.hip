@@ -332,6 +332,183 @@ static int gemm_splits(const GemvArgs& a, int nx, int ny) {
   return S;
 }
 
+
+// ---------------------------------------------------------------------------
+// LDS-staged form for packed activations (round 4): a 512-thread block (8 waves, 2 x 4) owns
+// 32 WR weight rows x 64 WN tokens; per 64-deep k-step the block's weight tiles (2 WR row tiles x
+// 2 k tiles) and activation fragments (4 WN token tiles x 2) -- 1 KiB each, contiguous in both
+// packed layouts -- go global -> LDS by LDS-DMA (buffer_load ... lds: no registers), double
+// buffered, while the waves run the previous stage's MFMAs from LDS.  Every A / B fragment a wave
+// reads from LDS feeds WN / WR MFMAs (gemm2_kernel re-read them from L1/L2 per wave, ~0.3 MFMA busy
+// at M = 5,792: profiles/r03_b_pmc_mfma.json).  SPLIT: blockIdx.z takes a K range and writes fp32
+// partials for gemm_splitk_reduce (few row blocks: o_proj / down at N 4,096).
+template <int WR, int WN, int EPI, bool SPLIT = false>
+__global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
+  typedef __attribute__((address_space(3))) void lvoid;
+  constexpr int BR = 2 * WR, BT = 4 * WN;          // row tiles / token tiles per block
+  constexpr int STAGE = (BR + BT) * 2 * 1024;      // bytes per k-step stage
+  constexpr int TILES = (BR + BT) * 2;             // 1 KiB tiles per stage
+  static_assert(TILES % 8 == 0, "tiles per stage split over the 8 waves");
+  extern __shared__ __attribute__((aligned(16))) unsigned char g3_lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int wr = wave & 1, wn = wave >> 1;
+  const int KT = a.KT, T = a.pk_tiles, n_rt = a.n_row_tiles;
+  const int rb0 = blockIdx.x * BR, tb0 = blockIdx.y * BT;
+  if (rb0 >= n_rt || tb0 >= T) return;
+  int kbeg = 0, kend = KT;
+  if constexpr (SPLIT) {
+    const int KS = KT / gridDim.z;
+    kbeg = blockIdx.z * KS;
+    kend = kbeg + KS;
+  }
+  const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.w), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0, 0x7fffffff, 0x00020000);
+  // stage loads: tile q = wave * (TILES / 8) + i; q < 2 BR: weights (row tile q / 2, k tile q % 2),
+  // else activations (token tile, k tile); rows / tokens past the matrix re-read the last one
+  auto issue = [&](int kt, int buf) {
+#pragma unroll
+    for (int i = 0; i < TILES / 8; ++i) {
+      const int q = wave * (TILES / 8) + i;
+      unsigned char* dst = g3_lds + buf * STAGE + q * 1024;
+      if (q < 2 * BR) {
+        const int rt = min(rb0 + q / 2, n_rt - 1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lvoid*)dst, 16, (uint32_t)(((size_t)rt * KT + kt + (q & 1)) * 1024 + lane * 16),
+                                                 0, 0, 0);
+      } else {
+        const int tt = min(tb0 + (q - 2 * BR) / 2, T - 1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lvoid*)dst, 16,
+                                                 (uint32_t)(((size_t)(kt + (q & 1)) * T + tt) * 1024 + lane * 16), 0, 0, 0);
+      }
+    }
+  };
+  f32x4 acc[WR][WN];
+#pragma unroll
+  for (int r = 0; r < WR; ++r)
+#pragma unroll
+    for (int j = 0; j < WN; ++j) acc[r][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  issue(kbeg, 0);
+  int buf = 0;
+  for (int kt = kbeg; kt < kend; kt += 2) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();  // stage `buf` landed for every wave; the other buffer's readers are done
+    if (kt + 2 < kend) issue(kt + 2, buf ^ 1);
+    const u32x4* A = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE);
+    const u32x4* Bx = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE + 2 * BR * 1024);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 af[WR], bf[WN];
+#pragma unroll
+      for (int r = 0; r < WR; ++r) af[r] = A[((wr * WR + r) * 2 + kk) * 64 + lane];
+#pragma unroll
+      for (int j = 0; j < WN; ++j) bf[j] = Bx[((wn * WN + j) * 2 + kk) * 64 + lane];
+#pragma unroll
+      for (int r = 0; r < WR; ++r)
+#pragma unroll
+        for (int j = 0; j < WN; ++j)
+          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[r]),
+                                                             __builtin_bit_cast(bf16x8, bf[j]), acc[r][j], 0, 0, 0);
+    }
+    buf ^= 1;
+  }
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int rt0 = rb0 + wr * WR, tt0 = tb0 + wn * WN;
+  if constexpr (SPLIT) {
+    const size_t ld = (size_t)n_rt * 16;
+    float* wsz = a.ws + (size_t)blockIdx.z * a.B * ld;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      if (rt0 + r >= n_rt) continue;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int m = (tt0 + j) * 16 + c16;
+        if (m < a.B) *reinterpret_cast<f32x4*>(wsz + (size_t)m * ld + (rt0 + r) * 16 + g4 * 4) = acc[r][j];
+      }
+    }
+    return;
+  }
+  // epilogue (gemm2_kernel's): lane -> token (tt0 + j) * 16 + c16, output columns n0 .. n0 + 3
+  constexpr int OT = EPI == EPI_SWIGLU ? WR / 2 : WR;
+#pragma unroll
+  for (int q = 0; q < OT; ++q) {
+    const int ot = EPI == EPI_SWIGLU ? rt0 / 2 + q : rt0 + q;
+    const int n0 = ot * 16 + g4 * 4;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int m = (tt0 + j) * 16 + c16;
+      const bool mok = m < a.B && n0 < a.N;
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + i;
+        if constexpr (EPI == EPI_STORE) {
+          o[i] = rbf(acc[q][j][i]);
+        } else if constexpr (EPI == EPI_RESADD) {
+          o[i] = (mok && n < a.N) ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(acc[q][j][i])) : 0.f;
+        } else {
+          const float g = rbf(acc[2 * q][j][i]);
+          const float u = rbf(acc[2 * q + 1][j][i]);
+          o[i] = rbf(rbf(g / (1.0f + expf(-g))) * u);
+        }
+      }
+      if (mok && a.y_packed) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (n0 + i < a.N) a.y[xpkT_index(m, n0 + i, a.pk_tiles)] = f2bf(o[i]);
+      } else if (mok) {
+        bf16_t* yr = a.y + (size_t)m * a.ldy;
+        if (n0 + 3 < a.N && (a.ldy % 4) == 0) {
+          uint2 pk;
+          pk.x = pack2(o[0], o[1]);
+          pk.y = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(yr + n0) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n0 + i < a.N) yr[n0 + i] = f2bf(o[i]);
+        }
+      }
+      if constexpr (EPI == EPI_RESADD) {
+        float ss = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (a.ss_out && mok && g4 == 0) a.ss_out[(size_t)m * a.ld_ss_out + ot] = ss;
+      }
+    }
+  }
+}
+
+// gemm3 tile shape by row count: 256-row blocks for the wide matrices, 128 for N 4,096 (o_proj /
+// down), split K until the grid covers the CUs (its partials through gemm_splitk_reduce)
+template <int WR, int WN, int EPI>
+static hipError_t gemm3_launch(GemvArgs a, hipStream_t s) {
+  constexpr int BR = 2 * WR, BT = 4 * WN;
+  const size_t lds = (size_t)2 * (BR + BT) * 2 * 1024;
+  const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
+  static const int force = getenv("MTTS_GEMM3_SPLIT") ? atoi(getenv("MTTS_GEMM3_SPLIT")) : -1;
+  int S = 1;
+  if (!a.y_packed && a.ws) {
+    if (force > 0) S = force;
+    else if (force < 0)
+      while (grid.x * grid.y * S < 128 && a.KT / (2 * S) >= 16) S *= 2;  // (a grid of half the CUs and up runs whole)
+    while (S > 1 && (a.KT % (2 * S) || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
+  }
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)gemm3_kernel<WR, WN, EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm3_kernel<WR, WN, EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr = true;
+  }
+  if (S > 1) {
+    hipLaunchKernelGGL((gemm3_kernel<WR, WN, EPI, true>), dim3(grid.x, grid.y, S), dim3(512), lds, s, a);
+    const int n = a.B * ((a.N + 15) / 16);
+    hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
+  } else {
+    hipLaunchKernelGGL((gemm3_kernel<WR, WN, EPI, false>), grid, dim3(512), lds, s, a);
+  }
+  return hipGetLastError();
+}
+
 template <int WR, int WN, int EPI>
 static void gemm2_launch(GemvArgs a, hipStream_t s) {
   a.n_row_tiles = (EPI == EPI_SWIGLU ? 2 : 1) * ((a.N + 15) / 16);
@@ -360,6 +537,18 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   static const int big = getenv("MTTS_GEMM_SMALL") && getenv("MTTS_GEMM_SMALL")[0] == '1' ? 1 << 30 : 128;
   // the packed layout is read / written by the 128 x 128 form only
   if ((a0.x_packed || a0.y_packed) && (a0.B < big || a0.K % 64 || a0.pk_tiles * 16 < a0.B)) return hipErrorInvalidValue;
+  // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged form (0: off, A/B)
+  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 512;
+  if (g3min > 0 && a.x_packed && a.pk_tiles > 2 && a.B >= g3min && a.K % 64 == 0) {
+    a.n_row_tiles = (epi == EPI_SWIGLU ? 2 : 1) * n_tiles;
+    const bool wide = a.n_row_tiles >= 1024;  // 256-row blocks for q|k|v / gate|up, 128 for N 4,096
+    switch (epi) {
+      case EPI_STORE: return wide ? gemm3_launch<8, 4, EPI_STORE>(a, s) : gemm3_launch<4, 4, EPI_STORE>(a, s);
+      case EPI_RESADD: return wide ? gemm3_launch<8, 4, EPI_RESADD>(a, s) : gemm3_launch<4, 4, EPI_RESADD>(a, s);
+      case EPI_SWIGLU: return wide ? gemm3_launch<8, 4, EPI_SWIGLU>(a, s) : gemm3_launch<4, 4, EPI_SWIGLU>(a, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (a.B >= big && a.K % 64 == 0) {  // 128 x 128 block tiles
     switch (epi) {
       case EPI_STORE: gemm2_launch<4, 4, EPI_STORE>(a, s); break;

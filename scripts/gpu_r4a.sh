@@ -7,6 +7,7 @@ O=gpurun_out/r4a
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_ttsd_shape_gpu.py tests/test_pse_gpu.py tests/test_pse_oracle_gpu.py \
+    "tests/test_engine_gpu.py::test_packed_activations_long_prefill" tests/test_b4_oracle_gpu.py \
     -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread > $O/pytest.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "PASSED|FAILED|ERROR|SKIPPED" $O/pytest.log | tail -30; tail -3 $O/pytest.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
@@ -23,4 +24,10 @@ for flag in 1 0; do
       > $O/ttsd_long$flag.json 2> $O/ttsd_long$flag.err
   rc=$?; [ $rc -eq 0 ] || { echo "ttsd long=$flag rc=$rc"; tail -5 $O/ttsd_long$flag.err; exit $rc; }
   python3 -c "import json; d=json.load(open('$O/ttsd_long$flag.json')); print('ttsd pse_long=$flag', {k: d[k] for k in ('value','ms_per_decode_step','prefill_ms','decode_step_hbm_frac')}, d['roofline'] and {k: d['roofline'][k] for k in ('frac','avg_launch_us','kernel')})"
+done
+for g3 in 512 0; do
+  MTTS_GEMM3_MIN=$g3 timeout -k 10 300 python3 bench.py --batch 32 --steps 1 --warmup 1 --no-cpu-baseline --no-codec --no-dp-leg \
+      --no-roofline --extra-batches "" > $O/b32_g3_$g3.json 2> $O/b32_g3_$g3.err
+  rc=$?; [ $rc -eq 0 ] || { echo "b32 g3=$g3 rc=$rc"; tail -5 $O/b32_g3_$g3.err; exit $rc; }
+  python3 -c "import json; d=json.load(open('$O/b32_g3_$g3.json')); print('B=32 gemm3_min=$g3', {k: d[k] for k in ('value','prefill_ms','ms_per_decode_step')})"
 done
