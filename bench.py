@@ -663,6 +663,14 @@ def main():
                     "kernel": kname, "alg_bytes_per_launch": int(nb), "avg_launch_us": round(ms * 1e3, 2)}
             if kname != gemv_roof["kernel"]:
                 roof["gemv_gate_up"] = gemv_roof
+            if args.config == "ttsd" and eng.pse_long_active():
+                # the TTSD step's dominant launch: the persistent launch's long-context form at the
+                # end-of-generation context (the line's roofline itself is the whole step, below)
+                ms, nb = time_kernel(5, 10)
+                ach = nb / (ms * 1e-3) / 1e9
+                roof["pse_long_launch"] = {"kernel": "pse_kernel_t<true> (batch 1, long-context attention form)",
+                                           "achieved": round(ach, 1), "frac": round(ach / HBM_PEAK_GBS, 4),
+                                           "alg_bytes_per_launch": int(nb), "avg_launch_us": round(ms * 1e3, 2)}
         # whole decode step against the weight-stream roofline
         per_utt_ms = dt_max / args.steps * 1e3
         res = {
@@ -707,6 +715,22 @@ def main():
         res["text_head_steps"] = text_steps
         res["decode_alg_bytes_per_step"] = int(step_bytes)
         res["decode_step_hbm_frac"] = round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+        if args.config == "ttsd" and roof is not None:
+            # TTSD: the roofline is the WHOLE decode step (every kernel of the captured step), its
+            # algorithmic bytes averaged over the generation's contexts, against the PMC bytes of
+            # whole steps at the mean context (scripts/pmc_probe.py --config ttsd)
+            traffic, traffic_src = pmc_traffic("ttsd")
+            ach = step_bytes / (step_ms * 1e-3) / 1e9
+            parts = {k: roof[k] for k in ("pse_long_launch", "gemv_gate_up") if k in roof}
+            if "gemv_gate_up" not in parts and roof["kernel"].startswith("gemv_kernel"):
+                parts["gemv_gate_up"] = {k: roof[k] for k in ("kernel", "achieved", "frac", "alg_bytes_per_launch",
+                                                              "avg_launch_us")}
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_src": traffic_src,
+                    "kernel": "whole decode step (hipGraph replay: embedding, the 36-layer stack, final norm, heads, "
+                              "samplers)", "alg_bytes_per_launch": int(step_bytes),
+                    "avg_launch_us": round(step_ms * 1e3, 2), **parts}
+            res["roofline"] = roof
         if sweep:
             res["batch_sweep"] = sweep
         if dp_leg:

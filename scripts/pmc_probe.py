@@ -3,8 +3,8 @@
 mtts_engine_time_gemv: layers rotated, so no launch re-reads a matrix the previous one left in
 the 256 MB MALL; --config local: the depth stack's gate|up at B=8, its 4 layers walked as the
 frame walks them; --config pse / pse4: the batch-1 / batch-4 persistent streaming decode launch, every
-layer) for
-rocprofv3 PMC passes:
+layer; --config ttsd: WHOLE decode steps of the TTSD long form at its mean context, i.e. every
+kernel of the captured decode graph) for rocprofv3 PMC passes:
 
     rocprofv3 --pmc FETCH_SIZE --kernel-trace -d D -o f --output-format csv -- python3 scripts/pmc_probe.py --config clone
     rocprofv3 --pmc WRITE_SIZE --kernel-trace -d D -o w --output-format csv -- python3 scripts/pmc_probe.py --config clone
@@ -23,11 +23,73 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+TTSD_TEXT, TTSD_A, TTSD_B = 5750, 24, 56  # prompt 5,867 rows = the bench's mean TTSD context (2,117 + 7,519 / 2)
+
+
+def run_ttsd():
+    """Two greedy generations from one ~5.9 K-token TTSD-shaped prompt (n_vq 16), the same forced
+    schedule, max_new TTSD_A then TTSD_B: identical prefills and first TTSD_A steps, so the
+    counters of the second minus the first are TTSD_B - TTSD_A whole decode steps (hipGraph replays:
+    the batch-1 persistent launch's long form + embedding, final norm, heads, samplers)."""
+    import numpy as np
+    import torch
+    from bench import synthetic_prompt, forced_schedule
+    from moss_tts_amd.engine import Engine, EngineConfig, sampling_params
+    n_vq = 16
+    ids = synthetic_prompt(dict(n_vq=n_vq), np.random.default_rng(1), text_tokens=TTSD_TEXT)
+    T = ids.shape[1]
+    eng = Engine(EngineConfig(n_vq=n_vq, max_batch=1, max_ctx=T + TTSD_B + 64, max_prefill_tokens=1024), 0)
+    eng.init_random(0)
+    ids_d = torch.from_numpy(ids[None]).cuda()
+    mask_d = torch.ones((1, T), dtype=torch.uint8, device="cuda")
+    forced = torch.from_numpy(forced_schedule(TTSD_B, n_vq, TTSD_B - (n_vq + 3))).cuda()
+    sp = sampling_params(text_temperature=0, audio_temperature=0)
+    for n in (TTSD_A, TTSD_B):
+        eng.generate_ids(ids_d, mask_d, n, sp, forced_text=forced, chunk=16)
+        torch.cuda.synchronize()
+    wl = eng.weight_bytes() - (min(151645, 151656, 151662) // 16) * 16 * 4096 * 2  # text head gated off
+    kv = 36 * 2 * 8 * 128 * 2 * (T + (TTSD_A + TTSD_B) / 2 + 1)
+    print(json.dumps({"T": T, "steps": [TTSD_A, TTSD_B], "pse_long": eng.pse_long_active(),
+                      "alg_bytes_per_step": int(wl + kv)}))
+    eng.close()
+
+
+def summarize_ttsd(d):
+    """per-step bytes = (second generation - first) / (TTSD_B - TTSD_A); a generation starts at
+    the first prefill GEMM after a decode-step kernel"""
+    rows = []
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(rows))
+            rows.append((int(key), r["Kernel_Name"], r["Counter_Name"], float(r["Counter_Value"])))
+    out = {"config": "ttsd", "unit_raw": "KiB (rocprofv3 FETCH_SIZE / WRITE_SIZE)",
+           "what": f"whole decode steps at the mean TTSD context: generation of {TTSD_B} steps minus one of {TTSD_A}"}
+    for cname in sorted({r[2] for r in rows}):
+        seq = sorted((r for r in rows if r[2] == cname), key=lambda r: r[0])
+        seg, dec_seen, tot = -1, True, [0.0, 0.0]
+        for _, kname, _, v in seq:
+            if "gemm" in kname and dec_seen:
+                seg, dec_seen = seg + 1, False
+            if "pse_kernel" in kname or "finalize" in kname or "attn_decode" in kname:
+                dec_seen = True
+            if 0 <= seg < 2:
+                tot[seg] += v
+        out[cname] = {"segments": seg + 1, "gen_kib": tot, "per_step_kib": (tot[1] - tot[0]) / (TTSD_B - TTSD_A)}
+    fetch = out.get("FETCH_SIZE", {}).get("per_step_kib")
+    write = out.get("WRITE_SIZE", {}).get("per_step_kib")
+    if fetch is not None and write is not None:
+        out["traffic_bytes_per_launch"] = int((2 * fetch + write) * 1024)
+        out["traffic_unit"] = "bytes per decode step (hipGraph replay, every kernel)"
+    print(json.dumps(out, indent=1))
+
+
 def run(cfg_name, iters):
     import ctypes
     import torch
     from moss_tts_amd.engine import Engine, EngineConfig
     from moss_tts_amd import _native as N
+    if cfg_name == "ttsd":
+        return run_ttsd()
     if cfg_name == "local":
         cfg = EngineConfig(hidden=2048, layers=28, n_heads=16, n_kv=8, head_dim=128, inter=6144, n_vq=32, max_batch=8,
                            max_ctx=512, model_kind=1, local_hidden=1536, local_layers=4, local_inter=8960,
@@ -51,6 +113,8 @@ def run(cfg_name, iters):
 
 
 def summarize(d, cfg_name):
+    if cfg_name == "ttsd":
+        return summarize_ttsd(d)
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -73,7 +137,7 @@ def summarize(d, cfg_name):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["clone", "local", "pse", "pse4"], default="clone")
+    ap.add_argument("--config", choices=["clone", "local", "pse", "pse4", "ttsd"], default="clone")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--summarize", default=None)
     a = ap.parse_args()
