@@ -125,9 +125,17 @@ int mtts_pse4_active(const mtts_engine* eng);
  * slice of each KV head's cached keys, merge units combine them; MTTS_PSE_LONG=0: per-op launches) */
 int mtts_pse_long_active(const mtts_engine* eng);
 int mtts_pse_ctx_max(const mtts_engine* eng);
+/* MossTTSLocal engines: 1 when each channel of a frame's depth stage (adapter in, the depth layers,
+ * local_transformer.norm, adapter out) runs as one persistent launch (lpse.hip; the 1.7B depth
+ * shape, <= 8 rows, 256 CUs; MTTS_LPSE=0 at creation turns it off), else 0.  A timed-out launch
+ * is handled like the Delay launch's: mtts_generate_poll reports MTTS_E_PSE_TIMEOUT and the engine
+ * continues on the per-op launches (mtts_local_generate restarts once); mtts_local_forward checks
+ * its own launches and recomputes the frame. */
+int mtts_local_lpse_active(const mtts_engine* eng);
 /* Fault injection (tests): mark the persistent launch's error word as if a wait had timed out.
  * The next check (a teacher-forced batch-1 forward, or mtts_generate_poll) takes the fallback:
- * the launch is turned off for this engine and the work re-runs on the per-op launches. */
+ * the launch is turned off for this engine and the work re-runs on the per-op launches.
+ * (MossTTSLocal engines: the persistent channel launch's word.) */
 int mtts_pse_inject_timeout(mtts_engine* eng);
 /* A batch-1 mtts_forward through the persistent launch does not synchronise: its error word is
  * copied asynchronously and checked lazily -- without blocking at the next mtts_forward /

@@ -78,6 +78,7 @@ _SIGS = {
     "mtts_pse_active": (I, [P]),
     "mtts_pse4_active": (I, [P]),
     "mtts_pse_long_active": (I, [P]),
+    "mtts_local_lpse_active": (I, [P]),
     "mtts_pse_ctx_max": (I, [P]),
     "mtts_pse_inject_timeout": (I, [P]),
     "mtts_pse_check": (I, [P]),

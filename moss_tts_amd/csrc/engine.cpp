@@ -253,6 +253,10 @@ extern "C" int mtts_pse_active(const mtts_engine* e) { return e && e->pse && e->
 extern "C" int mtts_pse4_active(const mtts_engine* e) { return e && e->pse_takes(4) ? 1 : 0; }
 extern "C" int mtts_pse_long_active(const mtts_engine* e) { return e && e->pse_takes(1) && e->pse_long ? 1 : 0; }
 extern "C" int mtts_pse_inject_timeout(mtts_engine* e) {
+  if (e && e->lp) {
+    hipSetDevice(e->device);
+    return local_lpse_inject(e);
+  }
   if (!e || !e->pse_ws) return fail(MTTS_E_INVALID, "no persistent launch state");
   hipSetDevice(e->device);
   HIPCHK(hipStreamSynchronize(e->stream));
@@ -722,6 +726,7 @@ void leave(mtts_engine* e, void* user) {
 // clear it, turn the launch off for this engine (every later step takes the per-op launches)
 // and report true; synchronises the engine stream.
 bool pse_tripped(mtts_engine* e, hipStream_t s) {
+  if (e->lp) return local_lpse_tripped(e, s);
   if (!e->pse_ws) return false;
   uint32_t err = 0, err4 = 0;
   if (hipStreamSynchronize(s) != hipSuccess || hipMemcpy(&err, pse_err_word(e->pse_ws), 4, hipMemcpyDeviceToHost) != hipSuccess)

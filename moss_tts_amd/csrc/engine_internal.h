@@ -215,3 +215,8 @@ int local_init_random(mtts_engine* e, uint64_t seed);
 int local_load_weight(mtts_engine* e, const char* name, const void* src, size_t bytes, int on_dev, int* rc);
 // mtts_engine_time_gemv's depth-stack cases: proj 2 = gate|up, 3 = down of depth layer `layer`
 int local_time_proj(mtts_engine* e, int proj_kind, int layer, int B, int iters, float* avg_ms, uint64_t* alg_bytes);
+// the persistent channel launch (lpse.hip): taken for B rows; its error word (clears it, turns the
+// launch off and drops the captured frames when set); the fault-injection hook
+bool local_lpse_takes(const mtts_engine* e, int B);
+bool local_lpse_tripped(mtts_engine* e, hipStream_t s);
+int local_lpse_inject(mtts_engine* e);

@@ -293,6 +293,38 @@ bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I
 size_t pse4_ws_bytes();  // zero-filled once by the owner
 hipError_t pse4_decode(const PseArgs& a, void* ws, hipStream_t s, bool coop = false);
 uint32_t* pse4_err_word(void* ws);
+// lpse.hip: one MossTTSLocal channel's depth stage as one persistent launch -- the adapter into
+// the depth stack, its layers, local_transformer.norm and the adapter out (the 1.7B depth shape:
+// LH 1536, 16 / 8 heads x 128, I 8960, adapters F 2048 to H 2048; B <= 8 rows, 256 CUs)
+constexpr int LPSE_MAXL = 6;
+constexpr int LPSE_MAXB = 8;
+struct LpseLayer {
+  const bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
+};
+struct LpseArgs {
+  LpseLayer L[LPSE_MAXL];
+  int layers;
+  // the channel's input rows x_b = tok ? table + tok[b * ld_tok] * H : in + b * H (H = 2048)
+  const bf16_t* in;
+  const int64_t* tok;
+  int ld_tok;
+  const bf16_t *mi_gu, *mi_down, *norm, *mo_gu, *mo_down;  // packed adapters, local_transformer.norm
+  // activations: h [B][LH] + ss [B][LH / 16] (the depth residual stream), qkvb [B][4096],
+  // attnb [B][2048], act [B][I], actF [B][F], z [B][H] (the channel output)
+  bf16_t *h, *qkvb, *attnb, *act, *actF, *z;
+  float* ss;
+  bf16_t *kc, *vc;   // depth KV caches [layer][Bmax][Hkv][64][D], V transposed [..][D][64]
+  size_t layer_kv;   // elements per layer
+  int B, pos;        // rows; the channel position (the new key's slot)
+  float eps, scale;
+  int* cnt;          // workspace: hand-off counters (zero between launches), error word
+  uint32_t* err;
+};
+size_t lpse_lds_bytes();
+bool lpse_supported(int device, int B, int layers, int LH, int Hq, int Hkv, int D, int LI, int F, int H, int Cmax);
+size_t lpse_ws_bytes();  // zero-filled once by the owner
+hipError_t lpse_channel(const LpseArgs& a, void* ws, hipStream_t s);
+uint32_t* lpse_err_word(void* ws);
 // sample.hip
 hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);

@@ -44,6 +44,10 @@ struct LocalParts {
   std::vector<ChSampling> ch_table;  // mtts_local_set_sampling: per-channel processors (empty: from mtts_sampling)
   bool no_graph = false;
   std::unordered_map<long long, hipGraphExec_t> graphs;
+  // one channel's depth stage as one persistent launch (lpse.hip); MTTS_LPSE=0: per-op launches
+  bool lpse = true, lpse_ok = false;
+  void* lpse_ws = nullptr;  // lpse_ws_bytes(), zero-filled
+  int lpse_timeouts = 0;
 };
 
 static Stack local_stack(mtts_engine* e) {
@@ -76,6 +80,7 @@ int local_create(mtts_engine* e) {
   p.LH = c.local_hidden; p.LL = c.local_layers; p.LI = c.local_inter; p.F = c.local_mlp_ffn; p.C = c.n_vq + 1;
   p.qkv_rows = (Hq + 2 * Hkv) * D;
   if (const char* v = getenv("MTTS_LOCAL_NO_GRAPH")) p.no_graph = v[0] == '1';
+  if (const char* v = getenv("MTTS_LPSE")) p.lpse = v[0] == '1';
   const int LH = p.LH, LI = p.LI, F = p.F, C = p.C;
   int rc = 0;
   p.L.resize(p.LL);
@@ -106,6 +111,12 @@ int local_create(mtts_engine* e) {
   hipMemset(p.mi_down, 0, packed_bytes(LH, F));
   // weight bytes one frame streams: backbone once, then per channel the depth stack, its norm,
   // both adapters, the channel norm and the channel head
+  p.lpse_ok = lpse_supported(e->device, 1, p.LL, LH, Hq, Hkv, D, LI, F, H, LOCAL_CMAX) &&
+              p.qkv_rows == (Hq + 2 * Hkv) * D;
+  if (p.lpse_ok) {
+    if ((rc = e->alloc(reinterpret_cast<unsigned char**>(&p.lpse_ws), lpse_ws_bytes()))) return rc;
+    HIPCHK(hipMemset(p.lpse_ws, 0, lpse_ws_bytes()));
+  }
   p.backbone_bytes = e->step_weight_bytes;
   p.channel_bytes = lb + 2ull * LH + 2ull * (2ull * F * H + (uint64_t)LH * F) + 2ull * (2ull * F * LH + (uint64_t)H * F) + 2ull * H;
   p.text_head_bytes = 2ull * c.vocab * H;
@@ -145,6 +156,34 @@ int local_alloc_capacity(mtts_engine* e) {
   HIPCHK(hipMemset(p.zero, 0, (size_t)B * LH * 2));
   HIPCHK(hipMemset(p.next, 0, (size_t)B * C * 8));
   HIPCHK(hipMemset(p.seen, 0, (size_t)B * C * e->audio_rows));
+  return 0;
+}
+
+// The persistent channel launch's error word (lpse.hip: a bounded wait timed out).  When set:
+// clear it, turn the launch off for this engine (the captured frames are re-captured on the
+// per-op launches) and report true; synchronises the stream.
+bool local_lpse_tripped(mtts_engine* e, hipStream_t s) {
+  LocalParts* p = e->lp;
+  if (!p || !p->lpse_ws) return false;
+  uint32_t err = 0;
+  if (hipStreamSynchronize(s) != hipSuccess ||
+      hipMemcpy(&err, lpse_err_word(p->lpse_ws), 4, hipMemcpyDeviceToHost) != hipSuccess || !err)
+    return false;
+  hipMemset(p->lpse_ws, 0, lpse_ws_bytes());
+  p->lpse = false;
+  p->lpse_timeouts += 1;
+  local_clear_graphs(e);
+  fprintf(stderr, "libmtts: persistent channel launch timed out (code %u; device shared with other work?); "
+                  "this engine continues on the per-op launches\n", err);
+  return true;
+}
+
+int local_lpse_inject(mtts_engine* e) {
+  LocalParts* p = e->lp;
+  if (!p || !p->lpse_ws) return fail(MTTS_E_INVALID, "no persistent channel launch state");
+  HIPCHK(hipStreamSynchronize(e->stream));
+  const uint32_t code = 0x7e57u;
+  HIPCHK(hipMemcpy(lpse_err_word(p->lpse_ws), &code, 4, hipMemcpyHostToDevice));
   return 0;
 }
 
@@ -364,31 +403,70 @@ static bool local_sep_embed() {
 // The depth loop of one frame from the backbone state p.hid [B, H].  Greedy tokens go to
 // p.next[b][i]; forced != nullptr feeds forced[b * ld_forced + i] to channel i+1 instead
 // (teacher forcing); dump != nullptr receives channel i's logits at dump + i*B*ld_dump.
+bool local_lpse_takes(const mtts_engine* e, int B) {
+  const LocalParts* p = e->lp;
+  return p && p->lpse && p->lpse_ok && B >= 1 && B <= LPSE_MAXB;
+}
+
+// channel i's depth stage (adapter in, the depth layers, local_transformer.norm, adapter out -> p.z)
+// as one persistent launch; its input rows: the backbone state (i == 0) or the embedding rows of
+// channel i - 1's tokens tok[b * ld_tok]
+static int lpse_launch(mtts_engine* e, int B, int i, const int64_t* tok, int ld_tok, hipStream_t s) {
+  LocalParts& p = *e->lp;
+  const mtts_config& c = e->c;
+  LpseArgs a{};
+  for (int l = 0; l < p.LL; ++l) {
+    const LayerW& w = p.L[l];
+    a.L[l] = LpseLayer{w.qkv, w.o, w.gu, w.down, w.in_norm, w.post_norm, w.q_norm, w.k_norm};
+  }
+  a.layers = p.LL;
+  if (i == 0) {
+    a.in = p.hid;
+  } else {
+    a.in = i - 1 == 0 ? e->emb_text : e->emb_audio + (size_t)(i - 2) * e->audio_rows * c.hidden;
+    a.tok = tok;
+    a.ld_tok = ld_tok;
+  }
+  a.mi_gu = p.mi_gu; a.mi_down = p.mi_down; a.norm = p.norm; a.mo_gu = p.mo_gu[i]; a.mo_down = p.mo_down[i];
+  a.h = p.h; a.qkvb = p.qkvb; a.attnb = p.attnb; a.act = p.act; a.actF = p.actF; a.z = p.z; a.ss = p.ss;
+  a.kc = p.kc; a.vc = p.vc; a.layer_kv = p.layer_kv;
+  a.B = B; a.pos = i; a.eps = c.rms_eps; a.scale = 1.0f / std::sqrt((float)c.head_dim);
+  HIPCHK(lpse_channel(a, p.lpse_ws, s));
+  return 0;
+}
+
 static int local_depth(mtts_engine* e, int B, int n_ch, const int64_t* forced, int ld_forced, bf16_t* dump, int ld_dump,
                        hipStream_t s) {
   LocalParts& p = *e->lp;
   const mtts_config& c = e->c;
   const int H = c.hidden, LH = p.LH, F = p.F, C = p.C;
   const Stack st = local_stack(e);
-  if (int rc = mlp_in(e, st, p.hid, B, s)) return rc;
+  const bool lp = local_lpse_takes(e, B);
+  if (!lp)
+    if (int rc = mlp_in(e, st, p.hid, B, s)) return rc;
   for (int i = 0; i < n_ch; ++i) {
-    if (int rc = run_layers(e, st, 0, B, 1, p.lpos + i, CH_DECODE, 1, s)) return rc;
-    GemvArgs g = gemv_args(p.mo_gu[i], st.xn, LH, p.actF, F, B, F, LH);
-    if (int rc = normed_input(e, st, g, p.norm, B, s)) return rc;  // local_transformer.norm (Qwen3RMSNorm)
-    HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
-    g = gemv_args(p.mo_down[i], p.actF, F, p.z, H, B, H, F);
-    HIPCHK(gemv_ex(g, EPI_STORE, s));
+    if (lp) {
+      const int64_t* tok = i == 0 ? nullptr : (forced ? forced + (i - 1) : p.next + (i - 1));
+      if (int rc = lpse_launch(e, B, i, tok, forced ? ld_forced : C, s)) return rc;
+    } else {
+      if (int rc = run_layers(e, st, 0, B, 1, p.lpos + i, CH_DECODE, 1, s)) return rc;
+      GemvArgs g = gemv_args(p.mo_gu[i], st.xn, LH, p.actF, F, B, F, LH);
+      if (int rc = normed_input(e, st, g, p.norm, B, s)) return rc;  // local_transformer.norm (Qwen3RMSNorm)
+      HIPCHK(gemv_ex(g, EPI_SWIGLU, s));
+      g = gemv_args(p.mo_down[i], p.actF, F, p.z, H, B, H, F);
+      HIPCHK(gemv_ex(g, EPI_STORE, s));
+    }
     HIPCHK(moss_rmsnorm(p.z, p.ln[i], p.zn, B, H, c.rms_eps, s));
     const int V = i == 0 ? c.vocab : e->audio_rows;
     bf16_t* lg = dump ? dump + (size_t)i * B * ld_dump : p.logits;
     const int ldl = dump ? ld_dump : p.ld_logits;
-    g = gemv_args(p.head[i], p.zn, H, lg, ldl, B, V, H);
+    GemvArgs g = gemv_args(p.head[i], p.zn, H, lg, ldl, B, V, H);
     if (i == 0) { g.pad_start = V; }
     else { g.pad_start = 0; g.pad_period = e->audio_rows; g.pad_off = c.audio_pad_code; }
     HIPCHK(gemv_ex(g, EPI_LOGITS, s));
     if (dump) HIPCHK(argmax_rows(lg, ldl, V, p.next + i, C, B, s));  // teacher forcing: no generate state
     else HIPCHK(local_pick(e->st, lg, ldl, V, i, p.seen, p.next, C, B, e->wide_hist, s));
-    if (i + 1 < n_ch) {
+    if (i + 1 < n_ch && !lp) {
       const int64_t* tok = forced ? forced + i : p.next + i;
       const bf16_t* table = i == 0 ? e->emb_text : e->emb_audio + (size_t)(i - 1) * e->audio_rows * H;
       const int ld_tok = forced ? ld_forced : C;
@@ -531,19 +609,25 @@ extern "C" int mtts_local_generate_decode(mtts_engine* e, int n_steps, void* str
 
 extern "C" int mtts_local_generate(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T, int max_new,
                                    int n_vq_for_inference, const mtts_sampling* sp, int chunk, int* n_rows, void* stream) {
-  int rc = mtts_local_generate_begin(e, ids, mask, B, T, max_new, n_vq_for_inference, sp, stream);
-  if (rc) return rc;
   if (chunk <= 0) chunk = 16;
-  int steps = 1, done = -1;
-  while (true) {
-    rc = mtts_generate_poll(e, &steps, &done, stream);
+  // a persistent-launch timeout (MTTS_E_PSE_TIMEOUT) turned that launch off: the generation
+  // restarts once from the prompt on the per-op launches
+  for (int attempt = 0;; ++attempt) {
+    int rc = mtts_local_generate_begin(e, ids, mask, B, T, max_new, n_vq_for_inference, sp, stream);
     if (rc) return rc;
-    if (done >= 0 || steps >= max_new) break;
-    rc = mtts_local_generate_decode(e, std::min(chunk, max_new - steps), stream);
+    int steps = 1, done = -1;
+    while (true) {
+      rc = mtts_generate_poll(e, &steps, &done, stream);
+      if (rc) break;
+      if (done >= 0 || steps >= max_new) break;
+      rc = mtts_local_generate_decode(e, std::min(chunk, max_new - steps), stream);
+      if (rc) break;
+    }
+    if (rc == MTTS_E_PSE_TIMEOUT && attempt == 0) continue;
     if (rc) return rc;
+    if (n_rows) *n_rows = done >= 0 ? done + 1 : steps;
+    return 0;
   }
-  if (n_rows) *n_rows = done >= 0 ? done + 1 : steps;
-  return 0;
 }
 
 extern "C" int mtts_local_forward(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int S, int past,
@@ -560,9 +644,21 @@ extern "C" int mtts_local_forward(mtts_engine* e, const int64_t* ids, const uint
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
   int rc = forward_chunked(e, ids, B, S, past, nullptr, s, p.hid, n_ch);
   if (!rc) rc = local_depth(e, B, n_ch, forced, p.C, reinterpret_cast<bf16_t*>(logits), ld_logits, s);
+  if (!rc && local_lpse_takes(e, B)) {
+    // (a teacher-forced frame is the parity entry: checked here, and on a timed-out launch the
+    // frame is recomputed on the per-op launches -- it rewrites the same cache rows)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(s, &cs));
+    if (cs == hipStreamCaptureStatusNone && local_lpse_tripped(e, s)) {
+      rc = forward_chunked(e, ids, B, S, past, nullptr, s, p.hid, n_ch);
+      if (!rc) rc = local_depth(e, B, n_ch, forced, p.C, reinterpret_cast<bf16_t*>(logits), ld_logits, s);
+    }
+  }
   leave(e, stream);
   return rc;
 }
+
+extern "C" int mtts_local_lpse_active(const mtts_engine* e) { return e && local_lpse_takes(e, 1) ? 1 : 0; }
 
 extern "C" int mtts_local_frame_bytes(const mtts_engine* e, int n_vq_for_inference, uint64_t* bytes) {
   if (!e || !bytes) return fail(MTTS_E_INVALID, "null argument");

@@ -145,6 +145,10 @@ class Engine:
         """Whether batch-1 steps past pse_ctx_max() run the launch's long-context (all-CU attention) form."""
         return bool(N.load().mtts_pse_long_active(self._h))
 
+    def lpse_active(self) -> bool:
+        """MossTTSLocal: each channel's depth stage runs as one persistent launch (lpse.hip)"""
+        return bool(N.load().mtts_local_lpse_active(self._h))
+
     def pse_ctx_max(self) -> int:
         """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
         return int(N.load().mtts_pse_ctx_max(self._h))
