@@ -136,7 +136,7 @@ def count_audio_frames(gen_row, start, n_vq):
 
 
 def _torch_cpu_layer(W, h, cos, sin, kc, vc, pos0, n_heads, n_kv, D, eps=1e-6):
-    """One Qwen3 decoder layer in fp32 torch-CPU ops (the oracle's decoder_layer restated on
+    """One Qwen3 decoder layer in torch-CPU ops (the oracle's decoder_layer restated on
     torch matmuls: `TF/models/qwen3/modeling_qwen3.py:294-323`), appending to the caches."""
     import torch
     import torch.nn.functional as F
@@ -165,41 +165,46 @@ def _torch_cpu_layer(W, h, cos, sin, kc, vc, pos0, n_heads, n_kv, D, eps=1e-6):
 
 
 def cpu_baseline(args, T, n_steps, frames):
-    """A CPU restatement of the decode path at the full 8B shape in fp32 torch-CPU ops (the
-    oracle's layer math on torch matmuls) on this host's cores, on a bounded sample: one prefill
-    layer over T tokens, 6 decode layer-steps at the prompt's context and one pass of the 1+32
-    heads; composed into one utterance (36 layers x (prefill + n_steps decode) + heads per step).
-    SURVEY.md §6 measured the reference's own torch-CPU path at 0.44 s per decode step (0.18
-    audio-s/s) on the 8-core build container."""
+    """A CPU restatement of the decode path at the full 8B shape in bf16 torch-CPU ops (the
+    oracle's layer math on torch matmuls, in the reference deployment's dtype: `torch_dtype=bf16`,
+    clis/moss_tts_app.py:95-107) on this host's cores, on a bounded sample: one prefill layer over
+    T tokens, 6 decode layer-steps at the prompt's context and one pass of the 1+32 heads; composed
+    into one utterance (36 layers x (prefill + n_steps decode) + heads per step).  SURVEY.md §6
+    measured the reference's own torch-CPU path at 0.44 s per decode step (0.18 audio-s/s) on the
+    8-core build container; round 3's fp32 form of this port ran 2.7x slower than that (bf16 halves
+    the bytes a CPU GEMV streams: 40 vs 52 GB/s, 5.0 vs 7.8 ms per gate+down pair on the build
+    container's 8 cores)."""
     import torch
     cores = torch.get_num_threads()
     H, I, D, nh, nkv = 4096, 12288, 128, 32, 8
     g = torch.Generator().manual_seed(0)
 
-    def rnd(*shape):
-        return torch.randn(*shape, generator=g) * shape[-1] ** -0.5
+    bf = torch.bfloat16
 
+    def rnd(*shape):
+        return (torch.randn(*shape, generator=g) * shape[-1] ** -0.5).to(bf)
+
+    one = lambda n: torch.ones(n, dtype=bf)  # noqa: E731
     W = {"q": rnd(nh * D, H), "k": rnd(nkv * D, H), "v": rnd(nkv * D, H), "o": rnd(H, nh * D), "g": rnd(I, H),
-         "u": rnd(I, H), "d": rnd(H, I), "in": torch.ones(H), "post": torch.ones(H), "qn": torch.ones(D),
-         "kn": torch.ones(D)}
+         "u": rnd(I, H), "d": rnd(H, I), "in": one(H), "post": one(H), "qn": one(D), "kn": one(D)}
     inv = 1.0 / (1e6 ** (torch.arange(0, D, 2, dtype=torch.float32) / D))
     f = torch.arange(T + 16, dtype=torch.float32)[:, None] * inv[None]
-    cos, sin = torch.cat([f, f], -1).cos(), torch.cat([f, f], -1).sin()
-    kc, vc = torch.zeros(1, nkv, T + 16, D), torch.zeros(1, nkv, T + 16, D)
+    cos, sin = torch.cat([f, f], -1).cos().to(bf), torch.cat([f, f], -1).sin().to(bf)
+    kc, vc = torch.zeros(1, nkv, T + 16, D, dtype=bf), torch.zeros(1, nkv, T + 16, D, dtype=bf)
     with torch.inference_mode():
         t0 = time.perf_counter()
-        _torch_cpu_layer(W, torch.randn(1, T, H, generator=g), cos[:T], sin[:T], kc, vc, 0, nh, nkv, D)
+        _torch_cpu_layer(W, torch.randn(1, T, H, generator=g).to(bf), cos[:T], sin[:T], kc, vc, 0, nh, nkv, D)
         t_prefill_layer = time.perf_counter() - t0
         nd = 6
         for s in range(nd + 1):  # the first decode step warms the kernels up (untimed)
             if s == 1:
                 t0 = time.perf_counter()
-            _torch_cpu_layer(W, torch.randn(1, 1, H, generator=g), cos[T + s:T + s + 1], sin[T + s:T + s + 1], kc, vc,
-                             T + s, nh, nkv, D)
+            _torch_cpu_layer(W, torch.randn(1, 1, H, generator=g).to(bf), cos[T + s:T + s + 1], sin[T + s:T + s + 1],
+                             kc, vc, T + s, nh, nkv, D)
         t_dec_layer = (time.perf_counter() - t0) / nd
         del W
         heads = rnd(151936 + 32 * 1025, H)
-        x = torch.randn(1, H, generator=g)
+        x = torch.randn(1, H, generator=g).to(bf)
         t0 = time.perf_counter()
         for _ in range(2):
             _ = x @ heads.T
@@ -207,7 +212,7 @@ def cpu_baseline(args, T, n_steps, frames):
         del heads
     utt = 36 * (t_prefill_layer + n_steps * t_dec_layer) + (n_steps + 1) * t_heads
     return {"value": round(frames / FRAME_RATE / utt, 5), "unit": "audio-s/s", "cores": int(cores), "kind": "port",
-            "sample": (f"fp32 torch-CPU restatement of the layer math at the 8B shape, batch 1: 1 prefill layer "
+            "sample": (f"bf16 torch-CPU restatement of the layer math at the 8B shape, batch 1: 1 prefill layer "
                        f"(T={T}, {t_prefill_layer:.2f}s) + {nd} decode layer-steps ({t_dec_layer * 1e3:.1f}ms each) "
                        f"+ the 1+32 heads ({t_heads * 1e3:.0f}ms), composed to one utterance of {n_steps} steps = "
                        f"{utt:.1f}s"),
