@@ -44,7 +44,12 @@ namespace {
 
 constexpr int CW = 4;                   // consumer waves
 constexpr int THREADS = (1 + CW) * 64;  // + the loader wave
+#ifndef LPSE_INF
+#define LPSE_INF 3  // ring slots in flight per loader (48 KiB: the batch-1 launch's measured optimum)
+#endif
 constexpr int NS = 7;                   // ring slots of 16 KiB
+constexpr int INF = LPSE_INF;
+static_assert(INF >= 1 && INF <= 3 && INF < NS, "vmcnt counts at most 63 loads");
 constexpr int SLOT = 16 * 1024;
 constexpr int NB = LPSE_MAXB;           // rows
 constexpr int LH = 1536, H = 2048, F = 2048, LI = 8960, HQ = 16, HKV = 8, D = 128, QKVR = (HQ + 2 * HKV) * D;
@@ -449,7 +454,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
   if (wave == 0) {
     // =================== loader ===================
     // This CU's slots in consumption order; slot k of a segment = 16 weight tiles from its base.
-    // Each slot goes global -> ring slot by LDS-DMA (16 wave-instructions of 1 KiB); the 2 most
+    // Each slot goes global -> ring slot by LDS-DMA (16 wave-instructions of 1 KiB); the INF most
     // recent slots stay in flight, older ones are published in FULL.  `valid`: bytes of the matrix
     // from the segment base (a slot past it reads zeros: down_proj's half last slot of row tile 95)
     int issued = 0, pub = 0;
@@ -496,8 +501,9 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
         for (int i = 0; i < 16; ++i)
           __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (lvoid*)(dst + i * 1024), 16, voff + (uint32_t)i * 1024u, 0, 0, 0);
         issued = s + 1;
-        asm volatile("s_waitcnt vmcnt(32)" ::: "memory");  // all but the 2 newest slots have landed
-        publish(issued - 2);
+        // all but the INF - 1 newest slots have landed
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(16 * (INF - 1)) : "memory");
+        publish(issued - (INF - 1));
       }
     };
     // the adapter into the stack: gate|up pairs on CUs NR .. NR + 127, down on the residual CUs
