@@ -16,17 +16,21 @@ torch = pytest.importorskip("torch")
 LAYERS = 3
 
 
-def make(pse, max_ctx=1024, max_prefill=1024, ctx_limit=1 << 20):
-    """ctx_limit: the PSE context range (MTTS_PSE_CTX; unlimited here to test the kernel itself)"""
+def make(pse, max_ctx=1024, max_prefill=1024, ctx_limit=1 << 20, long_form=None):
+    """ctx_limit: the PSE context range (MTTS_PSE_CTX; unlimited here to test the kernel itself);
+    long_form: MTTS_PSE_LONG (None: the default, on)"""
     from moss_tts_amd.engine import Engine, EngineConfig
     os.environ["MTTS_PSE"] = "1" if pse else "0"
     if ctx_limit is not None:
         os.environ["MTTS_PSE_CTX"] = str(ctx_limit)
+    if long_form is not None:
+        os.environ["MTTS_PSE_LONG"] = "1" if long_form else "0"
     try:
         e = Engine(EngineConfig(layers=LAYERS, max_batch=1, max_ctx=max_ctx, max_prefill_tokens=max_prefill), 0)
     finally:
         os.environ.pop("MTTS_PSE")
         os.environ.pop("MTTS_PSE_CTX", None)
+        os.environ.pop("MTTS_PSE_LONG", None)
     e.init_random(seed=3)
     return e
 
@@ -140,20 +144,27 @@ def test_pse_generate_matches_launches(engines):
 
 
 def test_pse_context_gate(engines):
-    """The default engine takes the PSE path only within its context range: beyond it a decode
-    forward is the per-op launches' (bit-identical), within it the PSE one (within the band)"""
+    """The short form runs only within its context range.  Beyond it an engine without the
+    long-context form (MTTS_PSE_LONG=0) decodes through the per-op launches (bit-identical), the
+    default engine through the long-context form (within the band); within it both take the
+    short form (within the band)"""
     ref, _ = engines
+    short = make(True, ctx_limit=None, long_form=False)
     dflt = make(True, ctx_limit=None)
     try:
-        lim = dflt.pse_ctx_max()
+        lim = short.pse_ctx_max()
         assert 0 < lim <= 1000  # lim + 20 cached keys must fit max_ctx
+        assert dflt.pse_long_active() and not short.pse_long_active()
         ids, mask = prompt(lim + 20, 2, 9)
         want = decode_logits(ref, ids, mask, lim + 20, 2)
-        got = decode_logits(dflt, ids, mask, lim + 20, 2)
-        assert all(np.array_equal(w, g) for w, g in zip(want, got))
+        assert all(np.array_equal(w, g) for w, g in zip(want, decode_logits(short, ids, mask, lim + 20, 2)))
+        check_logits(ref, want, decode_logits(dflt, ids, mask, lim + 20, 2))
         ids, mask = prompt(lim - 40, 2, 9)
-        check_logits(ref, decode_logits(ref, ids, mask, lim - 40, 2), decode_logits(dflt, ids, mask, lim - 40, 2))
+        want = decode_logits(ref, ids, mask, lim - 40, 2)
+        check_logits(ref, want, decode_logits(short, ids, mask, lim - 40, 2))
+        check_logits(ref, want, decode_logits(dflt, ids, mask, lim - 40, 2))
     finally:
+        short.close()
         dflt.close()
 
 
