@@ -35,6 +35,13 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE4_RC
 #define PSE4_RC 2  // ring slots a plain CU's consumer waves drain into registers during the attention wait
 #endif
+// PSE4_HCNT: the residual hand-offs (h after o_proj / down, 9,216 tagged granules per consumer CU)
+// as counter + bulk load -- producers store the bf16 rows write-through and bump a per-layer counter,
+// consumers poll it and then load the 32 KiB of rows + sums of squares in one round of 16-byte sc1
+// loads (lpse.hip's hand-off form; half the bytes and a quarter of the load instructions of a sweep)
+#ifndef PSE4_HCNT
+#define PSE4_HCNT 0
+#endif
 constexpr int NS = PSE4_NS;
 constexpr int SLOT_KB = 16;
 constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
@@ -239,6 +246,46 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   cbar(x);
   return ok && !failed(x);
 }
+
+// PSE4_HCNT: wait for the 256 producers of hand-off `k` (counter hcnt[k]), then bulk-load the 4
+// residual rows (bf16 [4][H] at hb) into region A as [k tile][row][16 words] and their sums of
+// squares (fp32 [4][256] at hs) into ss32; `hook` runs before the poll (loads independent of it)
+template <typename Hook>
+__device__ __forceinline__ bool hgather(Ctx& x, const int* hcnt, int k, const bf16_t* hb, const float* hs,
+                                        uint32_t* xa32, uint32_t* ss32, const Hook& hook) {
+  hook();
+  __builtin_amdgcn_s_setprio(3);
+  for (uint32_t spins = 0; (int)ld32(hcnt + k) < 256; ++spins) {
+    if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
+      give_up(x, 2);
+      __builtin_amdgcn_s_setprio(0);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (every read below is an sc1 load)
+  constexpr int CPR = H_ / 8;  // 16-byte chunks per row
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(hb), 0, NB * H_ * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hs), 0, NB * (H_ / 16) * 4, 0x00020000);
+  u32x4 v[NB * CPR / (CW * 64)];
+#pragma unroll
+  for (int j = 0; j < NB * CPR / (CW * 64); ++j) {
+    const int b = j / (CPR / (CW * 64)), c8 = x.tid + (CW * 64) * (j % (CPR / (CW * 64)));
+    v[j] = __builtin_amdgcn_raw_buffer_load_b128(hrs, (uint32_t)(b * H_ + c8 * 8) * 2u, 0, 16 /* sc1 */);
+  }
+  const u32x4 sv = __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)x.tid * 16u, 0, 16);
+  u32x4* xa = reinterpret_cast<u32x4*>(xa32);
+#pragma unroll
+  for (int j = 0; j < NB * CPR / (CW * 64); ++j) {
+    const int b = j / (CPR / (CW * 64)), c8 = x.tid + (CW * 64) * (j % (CPR / (CW * 64)));
+    xa[((c8 >> 2) * NB + b) * 4 + (c8 & 3)] = v[j];
+  }
+  reinterpret_cast<u32x4*>(ss32)[x.tid] = sv;
+  __builtin_amdgcn_s_setprio(0);
+  cbar(x);
+  return !failed(x);
+}
+static_assert(NB * (H_ / 16) == 4 * CW * 64, "one 16-byte sums-of-squares chunk per consumer thread");
 
 // q|k|v partial granules of row b, grouped by KV head (pse.hip qkv_gran) -- unit (b, g) gathers
 // one contiguous range
@@ -786,7 +833,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
       int seq = 0;
       // hidden = residual + bf16(o) (TF/.../modeling_qwen3.py:311,322), published with each row's
       // sum of squares over the 16 columns in column order
-      auto emit_h = [&](uint64_t* gh, uint32_t t, float o) {
+      auto emit_h = [&](uint64_t* gh, uint32_t t, float o, int k) {
         if (wave != LW) return;
         const float hv = rbf(hres + rbf(o));
         hres = hv;
@@ -796,8 +843,20 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         for (int i = 0; i < 16; ++i) s16 += __shfl(sq, (lane & 48) + i, 64);
         hsq = s16;
         const float hn = __shfl_down(hv, 1, 64);
-        if ((erow & 1) == 0) st64(gh + xword(ecol, c * 16 + erow), gran(pack2(hv, hn), t));
-        if (erow == 0) st64(gh + NG_H + ecol * NT + c, gran(__float_as_uint(s16), t));
+        if constexpr (PSE4_HCNT) {
+          // rows bf16 [4][H] over the granule region's first 32 KiB, sums of squares fp32 [4][256] behind
+          // them; drained, then one arrival
+          bf16_t* hb = reinterpret_cast<bf16_t*>(gh);
+          float* hs = reinterpret_cast<float*>(gh + NG_H);
+          if ((erow & 1) == 0) st32(hb + (size_t)ecol * H_ + c * 16 + erow, pack2(hv, hn));
+          if (erow == 0) st32(hs + ecol * NT + c, __float_as_uint(s16));
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0) __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + k), 1, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          if ((erow & 1) == 0) st64(gh + xword(ecol, c * 16 + erow), gran(pack2(hv, hn), t));
+          if (erow == 0) st64(gh + NG_H + ecol * NT + c, gran(__float_as_uint(s16), t));
+        }
       };
       for (int l = 0; l < a.layers && !failed(x); ++l) {
         const PseLayer& Lw = a.L[l];
@@ -813,6 +872,10 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           }
           for (int i = x.tid; i < NB * NT; i += CW * 64) ss32[i] = __float_as_uint(a.ss[i]);
           cbar(x);
+        } else if (PSE4_HCNT) {
+          if (!hgather(x, a.hcnt, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
+                       reinterpret_cast<const float*>(a.g_h[1] + NG_H), xa32, ss32, [&]() { nw = norm_w(x, Lw.in_norm); }))
+            break;
         } else if (!gather<36>(x, a.g_h[1], NG_H + NG_SS, tagof(epoch, l - 1, OP_DOWN), xa32, NG_H, ss32,
                                [&]() { nw = norm_w(x, Lw.in_norm); })) {
           break;
@@ -862,15 +925,20 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           __builtin_amdgcn_s_setprio(3);
           red_put(x, 0, acc);
           cbar(x);
-          emit_h(a.g_h[0], tagof(epoch, l, OP_O), red_get(0, ecol, erow));
+          emit_h(a.g_h[0], tagof(epoch, l, OP_O), red_get(0, ecol, erow), l * 2);
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
         }
         if (wave == LW) P4_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
-        if (!gather<36>(x, a.g_h[0], NG_H + NG_SS, tagof(epoch, l, OP_O), xa32, NG_H, ss32,
-                        [&]() { nw = norm_w(x, Lw.post_norm); }))
+        if (PSE4_HCNT) {
+          if (!hgather(x, a.hcnt, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
+                       reinterpret_cast<const float*>(a.g_h[0] + NG_H), xa32, ss32, [&]() { nw = norm_w(x, Lw.post_norm); }))
+            break;
+        } else if (!gather<36>(x, a.g_h[0], NG_H + NG_SS, tagof(epoch, l, OP_O), xa32, NG_H, ss32,
+                               [&]() { nw = norm_w(x, Lw.post_norm); })) {
           break;
+        }
         norm_stage(x, nw);
         if (wave == LW) P4_STAMP(l, 6);
         const uint32_t tg = tagof(epoch, l, OP_GU);
@@ -929,7 +997,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           __builtin_amdgcn_s_setprio(3);
           red_put(x, 0, acc);
           cbar(x);
-          emit_h(a.g_h[1], tagof(epoch, l, OP_DOWN), red_get(0, ecol, erow));
+          emit_h(a.g_h[1], tagof(epoch, l, OP_DOWN), red_get(0, ecol, erow), l * 2 + 1);
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
         }
@@ -946,6 +1014,8 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add((g32*)a.exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (uint32_t)P - 1) {
+      if (PSE4_HCNT)
+        for (int k = 0; k < 2 * a.layers; ++k) st32(a.hcnt + k, 0u);
       st32(a.exit_cnt, 0u);
       st32(a.epoch, epoch);
     }
@@ -970,7 +1040,7 @@ bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I
 }
 
 size_t pse4_ws_bytes() {
-  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 64;
+  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 2 * PSE_MAXL * 4 + 64;
 }
 
 hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
@@ -984,7 +1054,8 @@ hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   a.g_h[1] = g; g += NG_H + NG_SS;
   a.g_ss[1] = a.g_h[1] + NG_H;
   a.g_act = g; g += NG_ACT;
-  uint32_t* w = reinterpret_cast<uint32_t*>(g);
+  a.hcnt = reinterpret_cast<int*>(g);
+  uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse4_ws_bytes() - 64);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
   if (coop) {
     void* args[] = {&a};

@@ -9,7 +9,10 @@ export TMPDIR=/tmp
 timeout -k 10 200 python -u -m pytest "tests/test_pse_gpu.py::test_pse_context_gate" -m gpu -q -p no:cacheprovider \
     --timeout 150 --timeout-method thread > $O/pytest_gate.log 2>&1
 rc=$?; echo "gate test rc=$rc"; tail -2 $O/pytest_gate.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-for lib in moss_tts_amd/lib/libmtts.so moss_tts_amd/lib/var/libmtts_rc0.so moss_tts_amd/lib/var/libmtts_ns4.so; do
+MTTS_LIB=moss_tts_amd/lib/var/libmtts_hcnt.so timeout -k 10 300 python -u -m pytest tests/test_b4_oracle_gpu.py -m gpu -q \
+    -p no:cacheprovider --timeout 250 --timeout-method thread > $O/pytest_b4_hcnt.log 2>&1
+rc=$?; echo "b4 tests (hcnt lib) rc=$rc"; tail -2 $O/pytest_b4_hcnt.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+for lib in moss_tts_amd/lib/libmtts.so moss_tts_amd/lib/var/libmtts_hcnt.so moss_tts_amd/lib/var/libmtts_rc0.so moss_tts_amd/lib/var/libmtts_ns4.so; do
   MTTS_LIB=$lib timeout -k 10 300 python3 bench.py --batch 4 --steps 2 --warmup 1 --no-cpu-baseline --no-codec --no-dp-leg \
       --no-roofline --extra-batches "" > $O/b4.json 2> $O/b4.err
   rc=$?; [ $rc -eq 0 ] || { echo "$lib rc=$rc"; tail -5 $O/b4.err; exit $rc; }
