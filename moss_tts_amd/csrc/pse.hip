@@ -75,6 +75,13 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_TRACE2
 #define PSE_TRACE2 0  // (diagnostic: the input-norm h gather's own stamps replace the loader's)
 #endif
+#ifndef PSE_HCNT
+// the residual hand-offs (h after o_proj / down: 2,304 tagged granules swept by every consumer CU)
+// as counter + direct load: producers store the bf16 row write-through and bump a per-layer
+// counter; each consumer wave polls it, then loads exactly its two 8-column groups and the 256
+// sums of squares in one round of 16-byte sc1 loads and normalises them (no consumer barrier)
+#define PSE_HCNT 0
+#endif
 #ifndef PSE_NS
 #define PSE_NS 8
 #endif
@@ -387,6 +394,50 @@ __device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, NormW 
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// PSE_HCNT: wait for the P producers of hand-off k (hcnt[k]), then load this thread's two groups
+// of the residual row hb and the 256 sums of squares hs (4 per lane: the sum in norm_stage's
+// order) and normalise the groups into xs; `hook` runs before the poll
+template <typename Hook>
+__device__ __forceinline__ bool hnorm_counter(Ctx& x, const int* hcnt, int k, const bf16_t* hb, const float* hs,
+                                              bf16_t* xs, const Hook& hook, NormW& nw) {
+  hook();
+  if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
+  for (uint32_t spins = 0; (int)ld32(hcnt + k) < 256; ++spins) {
+    if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
+      give_up(x, 2);
+      if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(PSE_POLL_SLEEP);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (every read below is an sc1 load)
+  const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(hb), 0, H_ * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hs), 0, (H_ / 16) * 4, 0x00020000);
+  const u32x4 h0 = __builtin_amdgcn_raw_buffer_load_b128(hrs, (uint32_t)norm_grp(x, 0) * 16u, 0, 16 /* sc1 */);
+  const u32x4 h1 = __builtin_amdgcn_raw_buffer_load_b128(hrs, (uint32_t)norm_grp(x, 1) * 16u, 0, 16);
+  const u32x4 sv = __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)x.lane * 16u, 0, 16);
+  if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
+  const float s = wave_sum((__uint_as_float(sv[0]) + __uint_as_float(sv[1])) + (__uint_as_float(sv[2]) + __uint_as_float(sv[3])));
+  const float r = 1.0f / sqrtf(s / (float)H_ + x.eps);
+  u32x4* xv = reinterpret_cast<u32x4*>(xs);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const u32x4 hv = j ? h1 : h0, wv = j ? nw.b : nw.a;
+    u32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float x0 = __uint_as_float(hv[q] << 16), x1 = __uint_as_float(hv[q] & 0xffff0000u);
+      const float w0 = __uint_as_float(wv[q] << 16), w1 = __uint_as_float(wv[q] & 0xffff0000u);
+      o[q] = pack2(w0 * rbf(x0 * r), w1 * rbf(x1 * r));
+    }
+    xv[norm_grp(x, j)] = o;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return !failed(x);
 }
 
 // This consumer wave's 4 tiles of ring slot `seq`: acc += W_tiles . x over k tiles kt0 + 4w ..
@@ -1318,7 +1369,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
       int seq = 0;  // ring slot sequence number
       // o / d: this lane's output row (wave 1, lanes < 16): hidden = residual + bf16(o)
       // (TF/.../modeling_qwen3.py:311,322), published with its sum of squares
-      auto emit_h = [&](int which, uint32_t t, float o) {
+      auto emit_h = [&](int which, uint32_t t, float o, int l) {
         if (wave != LW) return;
         const float hv = rbf(hres + rbf(o));
         hres = lane < 16 ? hv : 0.f;
@@ -1329,8 +1380,19 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         for (int i = 0; i < 16; ++i) s16 += __shfl(sq, i, 64);
         hsq = s16;
         const float hn = __shfl_down(hv, 1, 64);
-        if (lane < 16 && (lane & 1) == 0) st64(a.g_h[which] + c * 8 + lane / 2, gran(pack2(hv, hn), t));
-        if (lane == 0) st64(a.g_ss[which] + c, gran(__float_as_uint(s16), t));
+        if constexpr (PSE_HCNT) {
+          // the row (bf16) over the granule region's first 8 KiB, its sums of squares over the ss
+          // region's first 1 KiB; drained, then one arrival
+          if (lane < 16 && (lane & 1) == 0) st32(reinterpret_cast<bf16_t*>(a.g_h[which]) + c * 16 + lane, pack2(hv, hn));
+          if (lane == 0) st32(reinterpret_cast<float*>(a.g_ss[which]) + c, __float_as_uint(s16));
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          if (lane == 0)
+            __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + l * 2 + which), 1, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+          if (lane < 16 && (lane & 1) == 0) st64(a.g_h[which] + c * 8 + lane / 2, gran(pack2(hv, hn), t));
+          if (lane == 0) st64(a.g_ss[which] + c, gran(__float_as_uint(s16), t));
+        }
       };
 
       for (int l = 0; l < a.layers && !failed(x); ++l) {
@@ -1346,11 +1408,17 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         constexpr int RC = (ATT || MRG || LONG) ? 0 : (PSE_RC < 8 ? PSE_RC : 8);
         NormW nw;
         auto load_nw = [&]() { nw = norm_w(x, Lw.in_norm); };
+        bool normed = false;
         if (l == 0) {  // the embedding row and its sums of squares (previous launch)
           load_nw();
           for (int i = x.tid; i < H_ / 2; i += CW * 64) xs32[i] = reinterpret_cast<const uint32_t*>(a.h)[i];
           for (int i = x.tid; i < NT; i += CW * 64) ssl[i] = a.ss[i];
           cbar(x);
+        } else if (PSE_HCNT) {
+          if (!hnorm_counter(x, a.hcnt, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
+                             reinterpret_cast<const float*>(a.g_ss[1]), xs, load_nw, nw))
+            break;
+          normed = true;
         } else {
   #if PSE_TRACE2
           x.tp = a.trace ? a.trace + ((size_t)l * PSE_TRACE_EV + 10) * 256 + c : nullptr;  // events 10-14
@@ -1362,7 +1430,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
   #endif
           if (!ok) break;
         }
-        norm_stage(x, xs, ssl, NT, nw);
+        if (!normed) norm_stage(x, xs, ssl, NT, nw);
         if (wave == LW) PSE_STAMP(l, 1);
         const uint32_t tq = tagof(epoch, l, OP_QKV);
         #pragma unroll 1
@@ -1423,16 +1491,22 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           PSE_PRIO_UP();
           red_put(x, 0, acc);
           cbar(x);
-          emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f);
+          emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f, l);
           cbar(x);
           PSE_PRIO_DOWN();
         }
         if (wave == LW) PSE_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
-        if (!gather<9>(x, a.g_h[0], H_ / 2 + NT, tagof(epoch, l, OP_O), xs32, H_ / 2, reinterpret_cast<uint32_t*>(ssl),
-                       [&]() { nw = norm_w(x, Lw.post_norm); }))
-          break;
-        norm_stage(x, xs, ssl, NT, nw);
+        if (PSE_HCNT) {
+          if (!hnorm_counter(x, a.hcnt, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
+                             reinterpret_cast<const float*>(a.g_ss[0]), xs, [&]() { nw = norm_w(x, Lw.post_norm); }, nw))
+            break;
+        } else {
+          if (!gather<9>(x, a.g_h[0], H_ / 2 + NT, tagof(epoch, l, OP_O), xs32, H_ / 2, reinterpret_cast<uint32_t*>(ssl),
+                         [&]() { nw = norm_w(x, Lw.post_norm); }))
+            break;
+          norm_stage(x, xs, ssl, NT, nw);
+        }
         if (wave == LW) PSE_STAMP(l, 6);
         const uint32_t tg = tagof(epoch, l, OP_GU);
         auto gu_round = [&](int j) {
@@ -1486,7 +1560,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           PSE_PRIO_UP();
           red_put(x, 0, acc);
           cbar(x);
-          emit_h(1, tagof(epoch, l, OP_DOWN), lane < 16 ? red_get(x, 0, lane) : 0.f);
+          emit_h(1, tagof(epoch, l, OP_DOWN), lane < 16 ? red_get(x, 0, lane) : 0.f, l);
           cbar(x);
           PSE_PRIO_DOWN();
         }
@@ -1511,6 +1585,8 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add((g32*)a.exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (uint32_t)P - 1) {
+      if (PSE_HCNT)
+        for (int k = 0; k < 2 * a.layers; ++k) st32(a.hcnt + k, 0u);
       st32(a.exit_cnt, 0u);
       st32(a.epoch, epoch);
     }
@@ -1540,7 +1616,7 @@ int pse_grid(int device) {
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + 64;
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + 2 * PSE_MAXL * 4 + 64;
 }
 
 hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, bool long_ctx) {
@@ -1556,7 +1632,8 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, boo
   a.g_ss[1] = g; g += H_ / 16;
   a.g_act = g; g += I_ / 2;
   a.g_part = g; g += NG_PART;
-  uint32_t* w = reinterpret_cast<uint32_t*>(g);
+  a.hcnt = reinterpret_cast<int*>(g);
+  uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse_ws_bytes() - 64);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
   const void* k = long_ctx ? (const void*)pse_kernel_t<true> : (const void*)pse_kernel_t<false>;
   if (coop) {
