@@ -7,6 +7,8 @@
 //   Qwen3Model.forward          transformers/models/qwen3/modeling_qwen3.py:367-427
 #include "engine_internal.h"
 
+static int trace_rows(const mtts_config& c) { return std::max(c.layers, c.model_kind == MTTS_MODEL_LOCAL ? c.local_layers : 0); }
+
 static thread_local std::string g_err;
 int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -119,7 +121,8 @@ static int alloc_capacity(mtts_engine* e) {
     } else {
       e->pse4_ws = nullptr;
     }
-    if (getenv("MTTS_PSE_TRACE") && (rc = e->alloc(&e->pse_trace, (size_t)c.layers * PSE_TRACE_EV * 256))) return rc;
+    // (rows: the backbone's layers, or MossTTSLocal's depth layers if more -- lpse.hip stamps those)
+  if (getenv("MTTS_PSE_TRACE") && (rc = e->alloc(&e->pse_trace, (size_t)trace_rows(c) * PSE_TRACE_EV * 256))) return rc;
   }
   // generate state
   const int B = c.max_batch;
@@ -271,7 +274,7 @@ extern "C" int mtts_pse_ctx_max(const mtts_engine* e) {
 extern "C" int mtts_pse_trace(mtts_engine* e, uint64_t* host, size_t n) {
   if (!e || !host) return fail(MTTS_E_INVALID, "null argument");
   if (!e->pse_trace) return fail(MTTS_E_UNSUPPORTED, "engine created without MTTS_PSE_TRACE=1");
-  const size_t have = (size_t)e->c.layers * PSE_TRACE_EV * 256;
+  const size_t have = (size_t)trace_rows(e->c) * PSE_TRACE_EV * 256;
   hipSetDevice(e->device);
   HIPCHK(hipStreamSynchronize(e->stream));
   HIPCHK(hipMemcpy(host, e->pse_trace, std::min(n, have) * sizeof(uint64_t), hipMemcpyDeviceToHost));

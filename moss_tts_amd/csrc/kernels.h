@@ -318,8 +318,11 @@ struct LpseArgs {
   size_t layer_kv;   // elements per layer
   int B, pos;        // rows; the channel position (the new key's slot)
   float eps, scale;
-  int* cnt;          // workspace: hand-off counters (zero between launches), error word
-  uint32_t* err;
+  int* cnt;          // workspace (set by lpse_channel): hand-off counters (zero between launches),
+  uint32_t* err;     // the error word, the launch epoch, the release flags
+  uint32_t* epoch;
+  uint32_t* go;
+  uint64_t* trace;   // nullptr, or [layers][PSE_TRACE_EV][256] s_memrealtime stamps (lpse.hip)
 };
 size_t lpse_lds_bytes();
 bool lpse_supported(int device, int B, int layers, int LH, int Hq, int Hkv, int D, int LI, int F, int H, int Cmax);

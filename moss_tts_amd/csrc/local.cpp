@@ -431,6 +431,7 @@ static int lpse_launch(mtts_engine* e, int B, int i, const int64_t* tok, int ld_
   a.h = p.h; a.qkvb = p.qkvb; a.attnb = p.attnb; a.act = p.act; a.actF = p.actF; a.z = p.z; a.ss = p.ss;
   a.kc = p.kc; a.vc = p.vc; a.layer_kv = p.layer_kv;
   a.B = B; a.pos = i; a.eps = c.rms_eps; a.scale = 1.0f / std::sqrt((float)c.head_dim);
+  a.trace = e->pse_trace;  // (MTTS_PSE_TRACE=1: the stamps of the last channel launch)
   HIPCHK(lpse_channel(a, p.lpse_ws, s));
   return 0;
 }

@@ -115,11 +115,23 @@ __device__ __forceinline__ const bf16_t* lptr(int l, int k) {
   return reinterpret_cast<const bf16_t* const*>(lp_lds + L_PTR)[l * 8 + k];
 }
 
+// trace (MTTS_PSE_TRACE=1 engines, scripts/lpse_trace.py): consumer wave 0 per layer -- 0 q|k|v input
+// ready, 1 normed, 2 q|k|v done; attention units 3 start, 4 done; residual CUs 5 o input in, 6 o done,
+// 12-15 down round j input in, 16 down done; gate|up CUs 7 input normed, 8-11 round j done
+#define LP_STAMP(l, ev)                                                                          \
+  do {                                                                                           \
+    if (a.trace && x.w == 0 && x.lane == 0)                                                      \
+      a.trace[((size_t)(l) * PSE_TRACE_EV + (ev)) * 256 + c] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+
 struct Cx {
   uint32_t* err;
   float eps;
   int c, lane, w, tid, B;
   int bar_gen;
+  int* cnt;        // hand-off counters
+  uint32_t* go;    // LPSE_GO: per (counter, CU) release flags, one 128-byte line each
+  uint32_t epoch;  // this launch's flag value
 };
 
 __device__ __forceinline__ bool failed() {
@@ -146,9 +158,20 @@ __device__ __forceinline__ void cbar(Cx& x) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
 }
 
-// wait until counter k has `target` arrivals (sc1 polls); false on timeout / abort
-__device__ __forceinline__ bool bwait(Cx& x, int* cnt, int k, int target) {
-  for (uint32_t spins = 0; (int)ld32(cnt + k) < target; ++spins) {
+// Hand-off k is complete once `target` producers arrived.  LPSE_GO (default): the producer whose
+// arrival completes it writes this launch's epoch into every consumer CU's own flag line, and a
+// consumer polls only its line -- polled directly, the one counter line took the polls of all 1,024
+// consumer waves (18 ms per frame against 8.4 for the per-op launches, profiles/r04_a_*); 0: poll
+// the counter itself (A/B)
+#ifndef LPSE_GO
+#define LPSE_GO 1
+#endif
+constexpr int GO_STRIDE = 32;  // words: one 128-byte line per flag
+__device__ __forceinline__ uint32_t* go_flag(const Cx& x, int k, int cu) { return x.go + ((size_t)k * P + cu) * GO_STRIDE; }
+
+// wait until hand-off k is complete (sc1 polls); false on timeout / abort
+__device__ __forceinline__ bool bwait(Cx& x, int k, int target) {
+  for (uint32_t spins = 0; LPSE_GO ? ld32(go_flag(x, k, x.c)) != x.epoch : (int)ld32(x.cnt + k) < target; ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed() || ld32(x.err)))) {
       give_up(x.err, 2);
       return false;
@@ -161,11 +184,19 @@ __device__ __forceinline__ bool bwait(Cx& x, int* cnt, int k, int target) {
   return !failed();
 }
 
-// this workgroup's outputs of an op are stored (write-through): drain, barrier, one arrival
-__device__ __forceinline__ void arrive(Cx& x, int* cnt, int k) {
+// this workgroup's outputs of hand-off k are stored (write-through): drain, barrier, one arrival;
+// the arrival that completes it releases every consumer CU's flag
+__device__ __forceinline__ void arrive(Cx& x, int k, int target) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   cbar(x);
-  if (x.tid == 0) __hip_atomic_fetch_add((gi32*)(cnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (x.w == 0) {
+    int t = 0;
+    if (x.lane == 0) t = __hip_atomic_fetch_add((gi32*)(x.cnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0, 64);
+    if (LPSE_GO && t == target - 1)
+#pragma unroll
+      for (int i = 0; i < P / 64; ++i) st32(go_flag(x, k, x.lane + 64 * i), x.epoch);
+  }
 }
 
 // ---- op input staging: rows [B][K] bf16 -> X [k tile][row][32] ----
@@ -450,6 +481,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
   __syncthreads();
   const int L = a.layers;
   const bool resid = c < NR;
+  const uint32_t epoch = ld32(a.epoch) + 1u;  // (the previous launch's last workgroup advanced it)
 
   if (wave == 0) {
     // =================== loader ===================
@@ -529,8 +561,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
     publish(issued);
   } else {
     // =================== consumers ===================
-    Cx x{a.err, a.eps, c, lane, wave - 1, (int)threadIdx.x - 64, a.B, 0};
-    int* cnt = a.cnt;
+    Cx x{a.err, a.eps, c, lane, wave - 1, (int)threadIdx.x - 64, a.B, 0, a.cnt, a.go, epoch};
     int seq = 0;
     float hres = 0.f;  // residual CUs: element (el_b, el_n) of this CU's residual tile
     bool ok = true;
@@ -542,48 +573,56 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
       ok = gemv_unit<2, KT_H / 16, KT_H>(x, seq, acc);
       red_put<2>(x, acc);
       put_pair(x, a.actF, F, p * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-      arrive(x, cnt, C_MIGU);
+      arrive(x, C_MIGU, F_PAIRS);
     }
     if (resid && ok) {
-      ok = bwait(x, cnt, C_MIGU, F_PAIRS);
+      ok = bwait(x, C_MIGU, F_PAIRS);
       stage_plain<F>(x, [&](int b) { return a.actF + (size_t)b * F; });
       f32x4 acc[1];
       ok = ok && gemv_unit<1, KT_F / 16, KT_F>(x, seq, acc);
       red_put<1>(x, acc);
       resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);  // res = 0: bf16(0 + bf16(y)) = bf16(y)
-      arrive(x, cnt, C_MIDOWN);
+      arrive(x, C_MIDOWN, NR);
     }
     for (int l = 0; l < L && ok; ++l) {
       // ---- input RMSNorm + q|k|v: row tile c ----
-      ok = bwait(x, cnt, l == 0 ? C_MIDOWN : c_layer(l - 1, 7), NR);
+      ok = bwait(x, l == 0 ? C_MIDOWN : c_layer(l - 1, 7), NR);
+      LP_STAMP(l, 0);
       stage_norm(x, a.h, a.ss, lptr(l, P_INN));
+      LP_STAMP(l, 1);
       {
         f32x4 acc[1];
         ok = ok && gemv_unit<1, KT_LH / 16, KT_LH>(x, seq, acc);
         red_put<1>(x, acc);
         put_pair(x, a.qkvb, QKVR, c * 16 + el_n(x.tid), rbf(red_get(x, 0)));
-        arrive(x, cnt, c_layer(l, 0));
+        arrive(x, c_layer(l, 0), P);
+        LP_STAMP(l, 2);
       }
       // ---- attention: unit (row b, KV head g) on CU NR + 8 b + g ----
       const int u = c - NR;
       if (!resid && u < HKV * a.B && ok) {
-        ok = bwait(x, cnt, c_layer(l, 0), P);
+        ok = bwait(x, c_layer(l, 0), P);
+        LP_STAMP(l, 3);
         if (ok) attention(x, a, l, u >> 3, u & 7);
-        arrive(x, cnt, c_layer(l, 1));
+        arrive(x, c_layer(l, 1), HKV * a.B);
+        LP_STAMP(l, 4);
       }
       if (resid) {
         // ---- o_proj + residual: row tile c ----
-        ok = ok && bwait(x, cnt, c_layer(l, 1), HKV * a.B);
+        ok = ok && bwait(x, c_layer(l, 1), HKV * a.B);
         stage_plain<HQ * D>(x, [&](int b) { return a.attnb + (size_t)b * HQ * D; });
+        LP_STAMP(l, 5);
         f32x4 acc[1];
         ok = ok && gemv_unit<1, KT_AT / 16, KT_AT>(x, seq, acc);
         red_put<1>(x, acc);
         resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);
-        arrive(x, cnt, c_layer(l, 2));
+        arrive(x, c_layer(l, 2), NR);
+        LP_STAMP(l, 6);
         // ---- down_proj + residual: row tile c, its input in 4 rounds of gate|up output ----
         f32x4 dacc = (f32x4){0.f, 0.f, 0.f, 0.f};
         for (int j = 0; j < 4 && ok; ++j) {
-          ok = bwait(x, cnt, c_layer(l, 3 + j), j < 3 ? NM : GU_PAIRS - 3 * NM);
+          ok = bwait(x, c_layer(l, 3 + j), j < 3 ? NM : GU_PAIRS - 3 * NM);
+          LP_STAMP(l, 12 + j);
           // this wave's B fragments of the round's (up to) 5 slots, straight from act (sc1)
           const int b = x.lane & 15;
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.act, 0, NB * LI * 2, 0x00020000);
@@ -612,11 +651,13 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
         f32x4 acc1[1] = {dacc};
         red_put<1>(x, acc1);
         resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);
-        arrive(x, cnt, c_layer(l, 7));
+        arrive(x, c_layer(l, 7), NR);
+        LP_STAMP(l, 16);
       } else {
         // ---- post-attention RMSNorm + gate|up + SwiGLU: pairs c - NR + 160 j (round j) ----
-        ok = ok && bwait(x, cnt, c_layer(l, 2), NR);
+        ok = ok && bwait(x, c_layer(l, 2), NR);
         stage_norm(x, a.h, a.ss, lptr(l, P_POSTN));
+        LP_STAMP(l, 7);
         for (int j = 0; j < 4; ++j) {
           const int p = c - NR + NM * j;
           if (p >= GU_PAIRS) break;
@@ -624,21 +665,22 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
           ok = ok && gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
           red_put<2>(x, acc);
           put_pair(x, a.act, LI, p * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-          arrive(x, cnt, c_layer(l, 3 + j));
+          arrive(x, c_layer(l, 3 + j), j < 3 ? NM : GU_PAIRS - 3 * NM);
+          LP_STAMP(l, 8 + j);
         }
       }
     }
     // ---- local_transformer.norm + local_to_speech_embedding_mlps[i] (:402-406) ----
     if (ok && c >= 128) {
-      ok = bwait(x, cnt, c_layer(L - 1, 7), NR);
+      ok = bwait(x, c_layer(L - 1, 7), NR);
       stage_norm(x, a.h, a.ss, a.norm);
       f32x4 acc[2];
       ok = ok && gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
       red_put<2>(x, acc);
       put_pair(x, a.actF, F, (c - 128) * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-      arrive(x, cnt, C_MOGU_BASE + 8 * L);
+      arrive(x, C_MOGU_BASE + 8 * L, F_PAIRS);
     } else if (ok) {
-      ok = bwait(x, cnt, C_MOGU_BASE + 8 * L, F_PAIRS);
+      ok = bwait(x, C_MOGU_BASE + 8 * L, F_PAIRS);
       stage_plain<F>(x, [&](int b) { return a.actF + (size_t)b * F; });
       f32x4 acc[1];
       ok = ok && gemv_unit<1, KT_F / 16, KT_F>(x, seq, acc);
@@ -652,8 +694,10 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const int t = __hip_atomic_fetch_add((gi32*)(a.cnt + C_EXIT), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == P - 1)
+    if (t == P - 1) {
       for (int k = 0; k < N_CNT; ++k) st32(a.cnt + k, 0u);
+      st32(a.epoch, epoch);
+    }
   }
 }
 
@@ -673,14 +717,19 @@ bool lpse_supported(int device, int B, int layers, int LH_, int Hq, int Hkv, int
          per_cu >= 1;
 }
 
-size_t lpse_ws_bytes() { return (size_t)N_CNT * 4 + 64; }
+// counters [N_CNT], error word, epoch, then the release flags [N_CNT][P] lines
+constexpr size_t WS_GO = 512;
+size_t lpse_ws_bytes() { return WS_GO + (size_t)N_CNT * P * GO_STRIDE * 4; }
 
 hipError_t lpse_channel(const LpseArgs& a0, void* ws, hipStream_t s) {
   if (a0.layers < 1 || a0.layers > LPSE_MAXL || a0.B < 1 || a0.B > NB || a0.pos < 0 || a0.pos >= CMAX)
     return hipErrorInvalidValue;
   LpseArgs a = a0;
-  a.cnt = reinterpret_cast<int*>(ws);
-  a.err = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + N_CNT * 4);
+  unsigned char* w = reinterpret_cast<unsigned char*>(ws);
+  a.cnt = reinterpret_cast<int*>(w);
+  a.err = reinterpret_cast<uint32_t*>(w + N_CNT * 4);
+  a.epoch = a.err + 1;
+  a.go = reinterpret_cast<uint32_t*>(w + WS_GO);
   hipLaunchKernelGGL(lpse_kernel, dim3(P), dim3(THREADS), lpse_lds_bytes(), s, a);
   return hipGetLastError();
 }
