@@ -271,7 +271,8 @@ struct PseArgs {
   uint64_t *g_qkv, *g_att, *g_h[2], *g_ss[2], *g_act;
   uint64_t* g_part;   // long-context form: per-slice attention partials [q head][half][slice][66]
   uint32_t *err, *epoch, *exit_cnt;
-  int* hcnt;        // pse4 (PSE4_HCNT): residual hand-off counters [layer][2], zero between launches
+  int* hcnt;        // PSE_HCNT / PSE4_HCNT: residual hand-off counters [layer][2], zero between launches
+  uint32_t* go;     // ... = 2: release flags [layer][2][256 CUs], one 128-byte line each (epoch values)
   uint64_t* trace;  // nullptr, or [layers][PSE_TRACE_EV][256] s_memrealtime stamps
   int probe;        // timing probe (MTTS_PSE_PROBE; results invalid): 1 loader issues no DMA,
                     // 2 consumers skip the slot reads and MFMAs

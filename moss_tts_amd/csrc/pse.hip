@@ -400,11 +400,13 @@ __device__ void norm_stage(Ctx& x, bf16_t* xs, const float* ss, int n_ss, NormW 
 // of the residual row hb and the 256 sums of squares hs (4 per lane: the sum in norm_stage's
 // order) and normalise the groups into xs; `hook` runs before the poll
 template <typename Hook>
-__device__ __forceinline__ bool hnorm_counter(Ctx& x, const int* hcnt, int k, const bf16_t* hb, const float* hs,
+__device__ __forceinline__ bool hnorm_counter(Ctx& x, const int* hcnt, const uint32_t* go, int k, const bf16_t* hb, const float* hs,
                                               bf16_t* xs, const Hook& hook, NormW& nw) {
   hook();
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
-  for (uint32_t spins = 0; (int)ld32(hcnt + k) < 256; ++spins) {
+  // (PSE_HCNT 2: this CU's own release flag line; 1: the counter line every consumer wave polls)
+  for (uint32_t spins = 0; PSE_HCNT == 2 ? ld32(go + ((size_t)k * 256 + x.c) * 32) != x.epoch : (int)ld32(hcnt + k) < 256;
+       ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
       if (PSE_GPRIO) __builtin_amdgcn_s_setprio(0);
@@ -1386,9 +1388,14 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           if (lane < 16 && (lane & 1) == 0) st32(reinterpret_cast<bf16_t*>(a.g_h[which]) + c * 16 + lane, pack2(hv, hn));
           if (lane == 0) st32(reinterpret_cast<float*>(a.g_ss[which]) + c, __float_as_uint(s16));
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          int t = 0;
           if (lane == 0)
-            __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + l * 2 + which), 1, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            t = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + l * 2 + which), 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+          t = __shfl(t, 0, 64);
+          if (PSE_HCNT == 2 && t == 255)  // the last producer releases every consumer CU's flag line
+#pragma unroll
+            for (int i = 0; i < 4; ++i) st32(a.go + ((size_t)(l * 2 + which) * 256 + lane + 64 * i) * 32, epoch);
         } else {
           if (lane < 16 && (lane & 1) == 0) st64(a.g_h[which] + c * 8 + lane / 2, gran(pack2(hv, hn), t));
           if (lane == 0) st64(a.g_ss[which] + c, gran(__float_as_uint(s16), t));
@@ -1415,7 +1422,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           for (int i = x.tid; i < NT; i += CW * 64) ssl[i] = a.ss[i];
           cbar(x);
         } else if (PSE_HCNT) {
-          if (!hnorm_counter(x, a.hcnt, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
+          if (!hnorm_counter(x, a.hcnt, a.go, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
                              reinterpret_cast<const float*>(a.g_ss[1]), xs, load_nw, nw))
             break;
           normed = true;
@@ -1498,7 +1505,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         if (wave == LW) PSE_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
         if (PSE_HCNT) {
-          if (!hnorm_counter(x, a.hcnt, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
+          if (!hnorm_counter(x, a.hcnt, a.go, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
                              reinterpret_cast<const float*>(a.g_ss[0]), xs, [&]() { nw = norm_w(x, Lw.post_norm); }, nw))
             break;
         } else {
@@ -1616,7 +1623,8 @@ int pse_grid(int device) {
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + 2 * PSE_MAXL * 4 + 64;
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + 2 * PSE_MAXL * 4 +
+         (PSE_HCNT == 2 ? (size_t)2 * PSE_MAXL * 256 * 128 : 0) + 64;
 }
 
 hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, bool long_ctx) {
@@ -1633,6 +1641,7 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, boo
   a.g_act = g; g += I_ / 2;
   a.g_part = g; g += NG_PART;
   a.hcnt = reinterpret_cast<int*>(g);
+  a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + 2 * PSE_MAXL * 4);
   uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse_ws_bytes() - 64);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
   const void* k = long_ctx ? (const void*)pse_kernel_t<true> : (const void*)pse_kernel_t<false>;

@@ -251,11 +251,13 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
 // residual rows (bf16 [4][H] at hb) into region A as [k tile][row][16 words] and their sums of
 // squares (fp32 [4][256] at hs) into ss32; `hook` runs before the poll (loads independent of it)
 template <typename Hook>
-__device__ __forceinline__ bool hgather(Ctx& x, const int* hcnt, int k, const bf16_t* hb, const float* hs,
+__device__ __forceinline__ bool hgather(Ctx& x, const int* hcnt, const uint32_t* go, int k, const bf16_t* hb, const float* hs,
                                         uint32_t* xa32, uint32_t* ss32, const Hook& hook) {
   hook();
   __builtin_amdgcn_s_setprio(3);
-  for (uint32_t spins = 0; (int)ld32(hcnt + k) < 256; ++spins) {
+  // (PSE4_HCNT 2: this CU's own release flag line; 1: the counter line every consumer wave polls)
+  for (uint32_t spins = 0; PSE4_HCNT == 2 ? ld32(go + ((size_t)k * 256 + x.c) * 32) != x.epoch : (int)ld32(hcnt + k) < 256;
+       ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
       __builtin_amdgcn_s_setprio(0);
@@ -851,8 +853,14 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           if ((erow & 1) == 0) st32(hb + (size_t)ecol * H_ + c * 16 + erow, pack2(hv, hn));
           if (erow == 0) st32(hs + ecol * NT + c, __float_as_uint(s16));
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          if (lane == 0) __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + k), 1, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
+          int t = 0;
+          if (lane == 0)
+            t = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + k), 1, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+          t = __shfl(t, 0, 64);
+          if (PSE4_HCNT == 2 && t == 255)  // the last producer releases every consumer CU's flag line
+#pragma unroll
+            for (int i = 0; i < 4; ++i) st32(a.go + ((size_t)k * 256 + lane + 64 * i) * 32, epoch);
         } else {
           if ((erow & 1) == 0) st64(gh + xword(ecol, c * 16 + erow), gran(pack2(hv, hn), t));
           if (erow == 0) st64(gh + NG_H + ecol * NT + c, gran(__float_as_uint(s16), t));
@@ -873,7 +881,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           for (int i = x.tid; i < NB * NT; i += CW * 64) ss32[i] = __float_as_uint(a.ss[i]);
           cbar(x);
         } else if (PSE4_HCNT) {
-          if (!hgather(x, a.hcnt, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
+          if (!hgather(x, a.hcnt, a.go, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
                        reinterpret_cast<const float*>(a.g_h[1] + NG_H), xa32, ss32, [&]() { nw = norm_w(x, Lw.in_norm); }))
             break;
         } else if (!gather<36>(x, a.g_h[1], NG_H + NG_SS, tagof(epoch, l - 1, OP_DOWN), xa32, NG_H, ss32,
@@ -932,7 +940,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         if (wave == LW) P4_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
         if (PSE4_HCNT) {
-          if (!hgather(x, a.hcnt, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
+          if (!hgather(x, a.hcnt, a.go, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
                        reinterpret_cast<const float*>(a.g_h[0] + NG_H), xa32, ss32, [&]() { nw = norm_w(x, Lw.post_norm); }))
             break;
         } else if (!gather<36>(x, a.g_h[0], NG_H + NG_SS, tagof(epoch, l, OP_O), xa32, NG_H, ss32,
@@ -1040,7 +1048,8 @@ bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I
 }
 
 size_t pse4_ws_bytes() {
-  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 2 * PSE_MAXL * 4 + 64;
+  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 2 * PSE_MAXL * 4 +
+         (PSE4_HCNT == 2 ? (size_t)2 * PSE_MAXL * 256 * 128 : 0) + 64;
 }
 
 hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
@@ -1055,6 +1064,7 @@ hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   a.g_ss[1] = a.g_h[1] + NG_H;
   a.g_act = g; g += NG_ACT;
   a.hcnt = reinterpret_cast<int*>(g);
+  a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + 2 * PSE_MAXL * 4);
   uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse4_ws_bytes() - 64);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
   if (coop) {
