@@ -40,8 +40,14 @@ constexpr int THREADS = (LW + CW) * 64;
 // consumers poll it and then load the 32 KiB of rows + sums of squares in one round of 16-byte sc1
 // loads (lpse.hip's hand-off form; half the bytes and a quarter of the load instructions of a sweep)
 #ifndef PSE4_HCNT
-#define PSE4_HCNT 0
+#define PSE4_HCNT 2
 #endif
+// PSE4_ATTF: the attention output hand-off (8,192 granules per consumer CU) in the same release-flag
+// form (with PSE4_HCNT 2)
+#ifndef PSE4_ATTF
+#define PSE4_ATTF 1
+#endif
+#define P4_AFLAG (PSE4_HCNT == 2 && PSE4_ATTF)
 constexpr int NS = PSE4_NS;
 constexpr int SLOT_KB = 16;
 constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
@@ -247,45 +253,62 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   return ok && !failed(x);
 }
 
-// PSE4_HCNT: wait for the 256 producers of hand-off `k` (counter hcnt[k]), then bulk-load the 4
-// residual rows (bf16 [4][H] at hb) into region A as [k tile][row][16 words] and their sums of
-// squares (fp32 [4][256] at hs) into ss32; `hook` runs before the poll (loads independent of it)
-template <typename Hook>
-__device__ __forceinline__ bool hgather(Ctx& x, const int* hcnt, const uint32_t* go, int k, const bf16_t* hb, const float* hs,
-                                        uint32_t* xa32, uint32_t* ss32, const Hook& hook) {
+// PSE4_HCNT: wait for hand-off k (counter hcnt[k] at `target`, or with PSE4_HCNT 2 this CU's own
+// release flag), then bulk-load 4 rows (bf16 [4][H] at hb) into region A as [k tile][row][16 words]
+// and, with hs, their sums of squares (fp32 [4][256]) into ss32; `hook` runs before the poll (loads
+// independent of it), `each_poll` after every poll (the ring slot drain)
+template <typename Hook, typename Poll = NoHook>
+__device__ __forceinline__ bool hgather(Ctx& x, const int* hcnt, const uint32_t* go, int k, int target, const bf16_t* hb,
+                                        const float* hs, uint32_t* xa32, uint32_t* ss32, const Hook& hook,
+                                        const Poll& each_poll = Poll()) {
   hook();
   __builtin_amdgcn_s_setprio(3);
   // (PSE4_HCNT 2: this CU's own release flag line; 1: the counter line every consumer wave polls)
-  for (uint32_t spins = 0; PSE4_HCNT == 2 ? ld32(go + ((size_t)k * 256 + x.c) * 32) != x.epoch : (int)ld32(hcnt + k) < 256;
+  for (uint32_t spins = 0; PSE4_HCNT == 2 ? ld32(go + ((size_t)k * 256 + x.c) * 32) != x.epoch : (int)ld32(hcnt + k) < target;
        ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
       __builtin_amdgcn_s_setprio(0);
       return false;
     }
+    each_poll();
     __builtin_amdgcn_s_sleep(1);
   }
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (every read below is an sc1 load)
   constexpr int CPR = H_ / 8;  // 16-byte chunks per row
   const __amdgpu_buffer_rsrc_t hrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(hb), 0, NB * H_ * 2, 0x00020000);
-  const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hs), 0, NB * (H_ / 16) * 4, 0x00020000);
   u32x4 v[NB * CPR / (CW * 64)];
 #pragma unroll
   for (int j = 0; j < NB * CPR / (CW * 64); ++j) {
     const int b = j / (CPR / (CW * 64)), c8 = x.tid + (CW * 64) * (j % (CPR / (CW * 64)));
     v[j] = __builtin_amdgcn_raw_buffer_load_b128(hrs, (uint32_t)(b * H_ + c8 * 8) * 2u, 0, 16 /* sc1 */);
   }
-  const u32x4 sv = __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)x.tid * 16u, 0, 16);
+  u32x4 sv = (u32x4){0u, 0u, 0u, 0u};
+  if (hs) {
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(hs), 0, NB * (H_ / 16) * 4, 0x00020000);
+    sv = __builtin_amdgcn_raw_buffer_load_b128(srs, (uint32_t)x.tid * 16u, 0, 16);
+  }
   u32x4* xa = reinterpret_cast<u32x4*>(xa32);
 #pragma unroll
   for (int j = 0; j < NB * CPR / (CW * 64); ++j) {
     const int b = j / (CPR / (CW * 64)), c8 = x.tid + (CW * 64) * (j % (CPR / (CW * 64)));
     xa[((c8 >> 2) * NB + b) * 4 + (c8 & 3)] = v[j];
   }
-  reinterpret_cast<u32x4*>(ss32)[x.tid] = sv;
+  if (hs) reinterpret_cast<u32x4*>(ss32)[x.tid] = sv;
   __builtin_amdgcn_s_setprio(0);
   cbar(x);
   return !failed(x);
+}
+// one arrival at hand-off k after this CU's stores of it drained (by every storing wave); the
+// arrival that completes it (target) releases every consumer CU's flag line (PSE4_HCNT 2)
+__device__ __forceinline__ void harrive(const Ctx& x, int* hcnt, uint32_t* go, int k, int target) {
+  int t = 0;
+  if (x.lane == 0)
+    t = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(hcnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  t = __shfl(t, 0, 64);
+  if (PSE4_HCNT == 2 && t == target - 1)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) st32(go + ((size_t)k * 256 + x.lane + 64 * i) * 32, x.epoch);
 }
 static_assert(NB * (H_ / 16) == 4 * CW * 64, "one 16-byte sums-of-squares chunk per consumer thread");
 
@@ -442,7 +465,8 @@ __device__ __forceinline__ float red_get(int r, int col, int row) {
 // on a failed wait.
 __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask_all,
                                                    const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
-                                                   uint64_t* g_att, uint32_t* err, float eps, float scale, int Cmax,
+                                                   uint64_t* g_att, int* hcnt, uint32_t* go, uint32_t* err, float eps,
+                                                   float scale, int Cmax,
                                                    uint32_t epoch, int bar_gen, int l, int unit, uint32_t tq) {
   Ctx x{err, eps, (int)blockIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64,
         epoch, bar_gen};
@@ -672,9 +696,14 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
       o0 += f * v_s[d];
       o1 += f * v_s[d + 1];
     }
-    st64(g_att + xword(b, (g * G + h) * D + d), gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+    if (P4_AFLAG)  // rows bf16 [4][4096] over the granule region; one arrival below
+      st32(reinterpret_cast<bf16_t*>(g_att) + (size_t)b * HQ_ * D_ + (g * G + h) * D + d, L > 0.f ? pack2(o0 / L, o1 / L) : 0u);
+    else
+      st64(g_att + xword(b, (g * G + h) * D + d), gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
   }
+  if (P4_AFLAG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   cbar(x);
+  if (P4_AFLAG && w == 0) harrive(x, hcnt, go, 2 * PSE_MAXL + l, HKV_ * NB);
   return x.bar_gen;
 }
 
@@ -853,14 +882,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           if ((erow & 1) == 0) st32(hb + (size_t)ecol * H_ + c * 16 + erow, pack2(hv, hn));
           if (erow == 0) st32(hs + ecol * NT + c, __float_as_uint(s16));
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          int t = 0;
-          if (lane == 0)
-            t = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + k), 1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-          t = __shfl(t, 0, 64);
-          if (PSE4_HCNT == 2 && t == 255)  // the last producer releases every consumer CU's flag line
-#pragma unroll
-            for (int i = 0; i < 4; ++i) st32(a.go + ((size_t)k * 256 + lane + 64 * i) * 32, epoch);
+          harrive(x, a.hcnt, a.go, k, 256);
         } else {
           if ((erow & 1) == 0) st64(gh + xword(ecol, c * 16 + erow), gran(pack2(hv, hn), t));
           if (erow == 0) st64(gh + NG_H + ecol * NT + c, gran(__float_as_uint(s16), t));
@@ -881,7 +903,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           for (int i = x.tid; i < NB * NT; i += CW * 64) ss32[i] = __float_as_uint(a.ss[i]);
           cbar(x);
         } else if (PSE4_HCNT) {
-          if (!hgather(x, a.hcnt, a.go, (l - 1) * 2 + 1, reinterpret_cast<const bf16_t*>(a.g_h[1]),
+          if (!hgather(x, a.hcnt, a.go, (l - 1) * 2 + 1, 256, reinterpret_cast<const bf16_t*>(a.g_h[1]),
                        reinterpret_cast<const float*>(a.g_h[1] + NG_H), xa32, ss32, [&]() { nw = norm_w(x, Lw.in_norm); }))
             break;
         } else if (!gather<36>(x, a.g_h[1], NG_H + NG_SS, tagof(epoch, l - 1, OP_DOWN), xa32, NG_H, ss32,
@@ -910,7 +932,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         if (wave == LW) P4_STAMP(l, 2);
         // ---------------- attention (32 units: one per row and KV head) ----------------
         if constexpr (ATT) {
-          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.err, a.eps, a.scale,
+          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.hcnt, a.go, a.err, a.eps, a.scale,
                                    a.Cmax, epoch, x.bar_gen, l, att_u, tq);
           const bool att_ok = bg >= 0;
           if (att_ok) x.bar_gen = bg;
@@ -920,9 +942,14 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         }
         // ---------------- o_proj (+ residual) ----------------
         SlotCache<RC> co;
-        if (!gather<32>(x, a.g_att, NG_ATT, tagof(epoch, l, OP_ATT), xa32, NG_ATT, nullptr, NoHook(),
-                        [&]() { co.drain(x, seq); }))
+        if (P4_AFLAG) {
+          if (!hgather(x, a.hcnt, a.go, 2 * PSE_MAXL + l, HKV_ * NB, reinterpret_cast<const bf16_t*>(a.g_att), nullptr, xa32,
+                       nullptr, NoHook(), [&]() { co.drain(x, seq); }))
+            break;
+        } else if (!gather<32>(x, a.g_att, NG_ATT, tagof(epoch, l, OP_ATT), xa32, NG_ATT, nullptr, NoHook(),
+                               [&]() { co.drain(x, seq); })) {
           break;
+        }
         if (wave == LW) P4_STAMP(l, 4);
         {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -940,7 +967,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         if (wave == LW) P4_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
         if (PSE4_HCNT) {
-          if (!hgather(x, a.hcnt, a.go, l * 2, reinterpret_cast<const bf16_t*>(a.g_h[0]),
+          if (!hgather(x, a.hcnt, a.go, l * 2, 256, reinterpret_cast<const bf16_t*>(a.g_h[0]),
                        reinterpret_cast<const float*>(a.g_h[0] + NG_H), xa32, ss32, [&]() { nw = norm_w(x, Lw.post_norm); }))
             break;
         } else if (!gather<36>(x, a.g_h[0], NG_H + NG_SS, tagof(epoch, l, OP_O), xa32, NG_H, ss32,
@@ -1022,8 +1049,10 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
   if (threadIdx.x == 0) {
     const uint32_t t = __hip_atomic_fetch_add((g32*)a.exit_cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == (uint32_t)P - 1) {
-      if (PSE4_HCNT)
+      if (PSE4_HCNT) {
         for (int k = 0; k < 2 * a.layers; ++k) st32(a.hcnt + k, 0u);
+        for (int k = 0; k < a.layers; ++k) st32(a.hcnt + 2 * PSE_MAXL + k, 0u);
+      }
       st32(a.exit_cnt, 0u);
       st32(a.epoch, epoch);
     }
@@ -1048,8 +1077,8 @@ bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I
 }
 
 size_t pse4_ws_bytes() {
-  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 2 * PSE_MAXL * 4 +
-         (PSE4_HCNT == 2 ? (size_t)2 * PSE_MAXL * 256 * 128 : 0) + 64;
+  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 3 * PSE_MAXL * 4 +
+         (PSE4_HCNT == 2 ? (size_t)3 * PSE_MAXL * 256 * 128 : 0) + 64;
 }
 
 hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
@@ -1064,7 +1093,7 @@ hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   a.g_ss[1] = a.g_h[1] + NG_H;
   a.g_act = g; g += NG_ACT;
   a.hcnt = reinterpret_cast<int*>(g);
-  a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + 2 * PSE_MAXL * 4);
+  a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + 3 * PSE_MAXL * 4);
   uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse4_ws_bytes() - 64);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
   if (coop) {
