@@ -45,7 +45,7 @@ constexpr int THREADS = (LW + CW) * 64;
 // PSE4_ATTF: the attention output hand-off (8,192 granules per consumer CU) in the same release-flag
 // form (with PSE4_HCNT 2)
 #ifndef PSE4_ATTF
-#define PSE4_ATTF 1
+#define PSE4_ATTF 0
 #endif
 #define P4_AFLAG (PSE4_HCNT == 2 && PSE4_ATTF)
 constexpr int NS = PSE4_NS;

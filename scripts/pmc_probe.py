@@ -36,8 +36,8 @@ def run_ttsd():
     from bench import synthetic_prompt, forced_schedule
     from moss_tts_amd.engine import Engine, EngineConfig, sampling_params
     n_vq = 16
-    ids = synthetic_prompt(dict(n_vq=n_vq), np.random.default_rng(1), text_tokens=TTSD_TEXT)
-    T = ids.shape[1]
+    ids = synthetic_prompt(dict(n_vq=n_vq), np.random.default_rng(1), text_tokens=TTSD_TEXT)  # [T, 1 + n_vq]
+    T = ids.shape[0]
     eng = Engine(EngineConfig(n_vq=n_vq, max_batch=1, max_ctx=T + TTSD_B + 64, max_prefill_tokens=1024), 0)
     eng.init_random(0)
     ids_d = torch.from_numpy(ids[None]).cuda()
