@@ -82,6 +82,12 @@ constexpr int THREADS = (LW + CW) * 64;
 // sums of squares in one round of 16-byte sc1 loads and normalises them (no consumer barrier)
 #define PSE_HCNT 0
 #endif
+#ifndef PSE_LONG_RESUME
+// long form: every CU's loader pauses while its slice reads K / V (the reads would queue behind the
+// weight fills); 1: it resumes as soon as the slice's chunks are scored (the partial hop, the merge
+// and the o gather then overlap the stream again), 0: after the whole attention phase
+#define PSE_LONG_RESUME 0
+#endif
 #ifndef PSE_NS
 #define PSE_NS 8
 #endif
@@ -1067,6 +1073,7 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
   } else {
     chunks();
   }
+  if (PSE_LONG_RESUME && x.tid == 0) __hip_atomic_store(&PSE_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   if (lane < HU) {
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;

@@ -44,6 +44,9 @@ constexpr int THREADS = (LW + CW) * 64;
 #endif
 // PSE4_ATTF: the attention output hand-off (8,192 granules per consumer CU) in the same release-flag
 // form (with PSE4_HCNT 2)
+#ifndef PSE4_ADB
+#define PSE4_ADB 0  // attention: double-buffered chunk loads (A/B)
+#endif
 #ifndef PSE4_ATTF
 #define PSE4_ATTF 0
 #endif
@@ -640,10 +643,28 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   };
   auto chunks = [&]() {
+#if PSE4_ADB
+    // two chunks in flight per wave: the next chunk's K / V^T load while this one computes
+    u32x4 ktB[2][QS], vtB[DT];
+    uint32_t mkB[2];
+    int ch = ch0;
+    if (ch + CW < nchunk) load_chunk(ch + CW, ktB, vtB, mkB);
+    while (ch < nchunk) {
+      compute(ch, ktA, vtA, mkA);
+      ch += CW;
+      if (ch >= nchunk) break;
+      if (ch + CW < nchunk) load_chunk(ch + CW, ktA, vtA, mkA);
+      compute(ch, ktB, vtB, mkB);
+      ch += CW;
+      if (ch >= nchunk) break;
+      if (ch + CW < nchunk) load_chunk(ch + CW, ktB, vtB, mkB);
+    }
+#else
     for (int ch = ch0; ch < nchunk; ch += CW) {
       if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
       compute(ch, ktA, vtA, mkA);
     }
+#endif
   };
   if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, gq + G * (D_ / 16) * 32, NKV, tq, graw32 + G * (D_ / 16) * 32, NKV,
                                                nullptr, chunks))
