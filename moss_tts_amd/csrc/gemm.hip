@@ -335,20 +335,28 @@ static int gemm_splits(const GemvArgs& a, int nx, int ny) {
 
 // ---------------------------------------------------------------------------
 // LDS-staged form for packed activations (round 4): a 512-thread block (8 waves, 2 x 4) owns
-// 32 WR weight rows x 64 WN tokens; per 64-deep k-step the block's weight tiles (2 WR row tiles x
-// 2 k tiles) and activation fragments (4 WN token tiles x 2) -- 1 KiB each, contiguous in both
-// packed layouts -- go global -> LDS by LDS-DMA (buffer_load ... lds: no registers), double
-// buffered, while the waves run the previous stage's MFMAs from LDS.  Every A / B fragment a wave
+// 32 WR weight rows x 64 WN tokens; per 32-deep k-step the block's weight tiles (2 WR row tiles)
+// and activation fragments (4 WN token tiles) -- 1 KiB each, contiguous in both packed layouts --
+// go global -> LDS by LDS-DMA (buffer_load ... lds: no registers) into a G3_NST-stage ring, G3_NST - 1
+// k-steps ahead of the waves running the current step's MFMAs from LDS.  Every A / B fragment a wave
 // reads from LDS feeds WN / WR MFMAs (gemm2_kernel re-read them from L1/L2 per wave, ~0.3 MFMA busy
-// at M = 5,792: profiles/r03_b_pmc_mfma.json).  SPLIT: blockIdx.z takes a K range and writes fp32
+// at M = 5,792: profiles/r03_b_pmc_mfma.json; the first, double-buffered 64-deep form of this kernel
+// 0.23-0.39: profiles/r04_*_pmc_mfma.json).  SPLIT: blockIdx.z takes a K range and writes fp32
 // partials for gemm_splitk_reduce (few row blocks: o_proj / down at N 4,096).
+#ifndef G3_NST
+#define G3_NST 4
+#endif
+template <int WR, int WN>
+constexpr size_t gemm3_lds_bytes() { return (size_t)G3_NST * (2 * WR + 4 * WN) * 1024; }
 template <int WR, int WN, int EPI, bool SPLIT = false>
 __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
   typedef __attribute__((address_space(3))) void lvoid;
   constexpr int BR = 2 * WR, BT = 4 * WN;          // row tiles / token tiles per block
-  constexpr int STAGE = (BR + BT) * 2 * 1024;      // bytes per k-step stage
-  constexpr int TILES = (BR + BT) * 2;             // 1 KiB tiles per stage
+  constexpr int TILES = BR + BT;                   // 1 KiB tiles per stage (one k tile)
+  constexpr int STAGE = TILES * 1024;
+  constexpr int TPW = TILES / 8;                   // loads per wave per stage
   static_assert(TILES % 8 == 0, "tiles per stage split over the 8 waves");
+  static_assert(TPW * (G3_NST - 1) <= 63, "vmcnt counts the stages in flight");
   extern __shared__ __attribute__((aligned(16))) unsigned char g3_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -364,21 +372,24 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
   }
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.w), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0, 0x7fffffff, 0x00020000);
-  // stage loads: tile q = wave * (TILES / 8) + i; q < 2 BR: weights (row tile q / 2, k tile q % 2),
-  // else activations (token tile, k tile); rows / tokens past the matrix re-read the last one
+  // stage loads of k tile kt: tile q = wave * TPW + i; q < BR: weights (row tile q), else activations
+  // (token tile q - BR); rows / tokens past the matrix re-read the last one.  Every stage issues
+  // exactly TPW loads per wave (k tiles past the range re-read the last one, never computed), so
+  // the counted vmcnt below is exact at the tail too.
   auto issue = [&](int kt, int buf) {
+    kt = min(kt, kend - 1);
 #pragma unroll
-    for (int i = 0; i < TILES / 8; ++i) {
-      const int q = wave * (TILES / 8) + i;
+    for (int i = 0; i < TPW; ++i) {
+      const int q = wave * TPW + i;
       unsigned char* dst = g3_lds + buf * STAGE + q * 1024;
-      if (q < 2 * BR) {
-        const int rt = min(rb0 + q / 2, n_rt - 1);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lvoid*)dst, 16, (uint32_t)(((size_t)rt * KT + kt + (q & 1)) * 1024 + lane * 16),
+      if (q < BR) {
+        const int rt = min(rb0 + q, n_rt - 1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lvoid*)dst, 16, (uint32_t)(((size_t)rt * KT + kt) * 1024 + lane * 16),
                                                  0, 0, 0);
       } else {
-        const int tt = min(tb0 + (q - 2 * BR) / 2, T - 1);
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lvoid*)dst, 16,
-                                                 (uint32_t)(((size_t)(kt + (q & 1)) * T + tt) * 1024 + lane * 16), 0, 0, 0);
+        const int tt = min(tb0 + q - BR, T - 1);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrs, (lvoid*)dst, 16, (uint32_t)(((size_t)kt * T + tt) * 1024 + lane * 16),
+                                                 0, 0, 0);
       }
     }
   };
@@ -387,30 +398,30 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
   for (int r = 0; r < WR; ++r)
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[r][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  issue(kbeg, 0);
+#pragma unroll
+  for (int st = 0; st < G3_NST - 1; ++st) issue(kbeg + st, st);
   int buf = 0;
-  for (int kt = kbeg; kt < kend; kt += 2) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();  // stage `buf` landed for every wave; the other buffer's readers are done
-    if (kt + 2 < kend) issue(kt + 2, buf ^ 1);
+  for (int kt = kbeg; kt < kend; ++kt) {
+    // this stage's loads have landed once only the G3_NST - 2 younger stages are in flight
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TPW * (G3_NST - 2)) : "memory");
+    __syncthreads();  // stage `buf` landed for every wave; the buffer refilled below was last read a step ago
+    issue(kt + G3_NST - 1, (buf + G3_NST - 1) % G3_NST);
     const u32x4* A = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE);
-    const u32x4* Bx = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE + 2 * BR * 1024);
+    const u32x4* Bx = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE + BR * 1024);
+    u32x4 af[WR], bf[WN];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x4 af[WR], bf[WN];
+    for (int r = 0; r < WR; ++r) af[r] = A[(wr * WR + r) * 64 + lane];
 #pragma unroll
-      for (int r = 0; r < WR; ++r) af[r] = A[((wr * WR + r) * 2 + kk) * 64 + lane];
+    for (int j = 0; j < WN; ++j) bf[j] = Bx[(wn * WN + j) * 64 + lane];
 #pragma unroll
-      for (int j = 0; j < WN; ++j) bf[j] = Bx[((wn * WN + j) * 2 + kk) * 64 + lane];
+    for (int r = 0; r < WR; ++r)
 #pragma unroll
-      for (int r = 0; r < WR; ++r)
-#pragma unroll
-        for (int j = 0; j < WN; ++j)
-          acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[r]),
-                                                             __builtin_bit_cast(bf16x8, bf[j]), acc[r][j], 0, 0, 0);
-    }
-    buf ^= 1;
+      for (int j = 0; j < WN; ++j)
+        acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[r]),
+                                                           __builtin_bit_cast(bf16x8, bf[j]), acc[r][j], 0, 0, 0);
+    buf = buf + 1 == G3_NST ? 0 : buf + 1;
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the surplus tail loads land before the block exits)
   const int g4 = lane >> 4, c16 = lane & 15;
   const int rt0 = rb0 + wr * WR, tt0 = tb0 + wn * WN;
   if constexpr (SPLIT) {
@@ -483,7 +494,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
 template <int WR, int WN, int EPI>
 static hipError_t gemm3_launch(GemvArgs a, hipStream_t s) {
   constexpr int BR = 2 * WR, BT = 4 * WN;
-  const size_t lds = (size_t)2 * (BR + BT) * 2 * 1024;
+  const size_t lds = gemm3_lds_bytes<WR, WN>();
   const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
   static const int force = getenv("MTTS_GEMM3_SPLIT") ? atoi(getenv("MTTS_GEMM3_SPLIT")) : -1;
   int S = 1;
