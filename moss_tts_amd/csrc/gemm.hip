@@ -341,10 +341,11 @@ static int gemm_splits(const GemvArgs& a, int nx, int ny) {
 // k-steps ahead of the waves running the current step's MFMAs from LDS.  Every A / B fragment a wave
 // reads from LDS feeds WN / WR MFMAs (gemm2_kernel re-read them from L1/L2 per wave, ~0.3 MFMA busy
 // at M = 5,792: profiles/r03_b_pmc_mfma.json; the first, double-buffered 64-deep form of this kernel
-// 0.23-0.39: profiles/r04_*_pmc_mfma.json).  SPLIT: blockIdx.z takes a K range and writes fp32
+// 0.23-0.39, this 3-stage ring 105 vs 110 ms for the 32-utterance prefill; 4 stages 123 ms: at 72 KiB
+// the 128-row form fits two blocks per CU; profiles/r04_e_*).  SPLIT: blockIdx.z takes a K range and writes fp32
 // partials for gemm_splitk_reduce (few row blocks: o_proj / down at N 4,096).
 #ifndef G3_NST
-#define G3_NST 4
+#define G3_NST 3
 #endif
 template <int WR, int WN>
 constexpr size_t gemm3_lds_bytes() { return (size_t)G3_NST * (2 * WR + 4 * WN) * 1024; }
@@ -548,8 +549,11 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   static const int big = getenv("MTTS_GEMM_SMALL") && getenv("MTTS_GEMM_SMALL")[0] == '1' ? 1 << 30 : 128;
   // the packed layout is read / written by the 128 x 128 form only
   if ((a0.x_packed || a0.y_packed) && (a0.B < big || a0.K % 64 || a0.pk_tiles * 16 < a0.B)) return hipErrorInvalidValue;
-  // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged form (0: off, A/B)
-  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 512;
+  // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged form (0: off, A/B).  From
+  // 2,048 rows: the 32-utterance prefill (5,792 rows) 127 -> 105 ms, while the TTSD prefill's
+  // 1,024-row chunks ran 82 -> 99 ms on it (4 token blocks x 96 row blocks = 1.5 rounds of the
+  // 256 CUs; gemm2's 128 x 128 tiles make 6), profiles/r04_e_*
+  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 2048;
   if (g3min > 0 && a.x_packed && a.pk_tiles > 2 && a.B >= g3min && a.K % 64 == 0) {
     a.n_row_tiles = (epi == EPI_SWIGLU ? 2 : 1) * n_tiles;
     const bool wide = a.n_row_tiles >= 1024;  // 256-row blocks for q|k|v / gate|up, 128 for N 4,096
