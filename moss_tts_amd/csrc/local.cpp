@@ -44,8 +44,9 @@ struct LocalParts {
   std::vector<ChSampling> ch_table;  // mtts_local_set_sampling: per-channel processors (empty: from mtts_sampling)
   bool no_graph = false;
   std::unordered_map<long long, hipGraphExec_t> graphs;
-  // one channel's depth stage as one persistent launch (lpse.hip); MTTS_LPSE=0: per-op launches
-  bool lpse = true, lpse_ok = false;
+  // one channel's depth stage as one persistent launch (lpse.hip); MTTS_LPSE=1 turns it on.  Off by
+  // default: 9.98 ms per frame against 8.40 for the per-op launches (profiles/r04_b_*)
+  bool lpse = false, lpse_ok = false;
   void* lpse_ws = nullptr;  // lpse_ws_bytes(), zero-filled
   int lpse_timeouts = 0;
 };

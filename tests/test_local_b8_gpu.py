@@ -40,8 +40,8 @@ class DeviceRows:
 
 @pytest.fixture(scope="module", params=["lpse", "per_op"])
 def setup(request):
-    """the engine with each channel's depth stage as one persistent launch (lpse.hip, the default)
-    and with the per-op launches (MTTS_LPSE=0)"""
+    """the engine with each channel's depth stage as one persistent launch (lpse.hip, MTTS_LPSE=1)
+    and with the per-op launches (the default)"""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import os
