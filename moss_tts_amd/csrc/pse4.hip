@@ -468,8 +468,8 @@ __device__ __forceinline__ float red_get(int r, int col, int row) {
 // on a failed wait.
 __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask_all,
                                                    const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
-                                                   uint64_t* g_att, int* hcnt, uint32_t* go, uint32_t* err, float eps,
-                                                   float scale, int Cmax,
+                                                   uint64_t* g_att, int* hcnt, uint32_t* go, uint32_t* err, uint64_t* trace,
+                                                   float eps, float scale, int Cmax,
                                                    uint32_t epoch, int bar_gen, int l, int unit, uint32_t tq) {
   Ctx x{err, eps, (int)blockIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64,
         epoch, bar_gen};
@@ -548,7 +548,13 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
   constexpr int NG = (G_ + 2) * (D_ / 16) * 32;
   constexpr int NQ = HU * (D_ / 16) * 32, NKV = 2 * (D_ / 16) * 32;
   uint64_t* gq = g_qkv + (size_t)b * NG_QKV_ROW + (size_t)g * NG;
+#define P4_ASTAMP(ev)                                                                                 \
+  do {                                                                                                \
+    if (trace && w == 0 && lane == 0)                                                                 \
+      trace[((size_t)l * PSE_TRACE_EV + (ev)) * 256 + x.c] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
   if (!gather<(NQ + CW * 64 - 1) / (CW * 64)>(x, gq, NQ, tq, graw32, NQ, nullptr, prefetch)) return -1;
+  P4_ASTAMP(16);
   if (w < HU) {
     const int bt = w * (D / 16);
     float o0, o1;
@@ -669,6 +675,7 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
   if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, gq + G * (D_ / 16) * 32, NKV, tq, graw32 + G * (D_ / 16) * 32, NKV,
                                                nullptr, chunks))
     return -1;
+  P4_ASTAMP(17);
   // ---- 3. k (wave 0) and v (wave 1), appended at pos ----
   if (w == 0) {
     float o0, o1;
@@ -724,6 +731,7 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
   }
   if (P4_AFLAG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   cbar(x);
+  P4_ASTAMP(18);
   if (P4_AFLAG && w == 0) harrive(x, hcnt, go, 2 * PSE_MAXL + l, HKV_ * NB);
   return x.bar_gen;
 }
@@ -953,7 +961,8 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         if (wave == LW) P4_STAMP(l, 2);
         // ---------------- attention (32 units: one per row and KV head) ----------------
         if constexpr (ATT) {
-          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.hcnt, a.go, a.err, a.eps, a.scale,
+          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.hcnt, a.go, a.err, a.trace,
+                                   a.eps, a.scale,
                                    a.Cmax, epoch, x.bar_gen, l, att_u, tq);
           const bool att_ok = bg >= 0;
           if (att_ok) x.bar_gen = bg;

@@ -15,7 +15,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from moss_tts_amd import _native as N  # noqa: E402
 
 NAMES = ["start", "qkv in", "qkv done", "att done", "o in", "o done", "gu in", "gu r01", "act0 (+gu2)",
-         "act1 (+dn0-7)", "act2 (+dn8-15)", "down done", "L qkv", "L o", "L gu", "L down"]
+         "act1 (+dn0-7)", "act2 (+dn8-15)", "down done", "L qkv", "L o", "L gu", "L down",
+         "A q in", "A chunks + kv in", "A merged"]
 B = 4
 
 
@@ -64,8 +65,8 @@ for name, cus in (("plain CUs", plain), ("attention CUs", att)):
     rows = []
     for l in range(1, layers):
         t0 = np.median(tr[l, 0, cus])
-        rows.append([np.median(tr[l, ev, cus]) - t0 if (tr[l, ev, cus] > 0).all() else np.nan for ev in range(16)])
+        rows.append([np.median(tr[l, ev, cus]) - t0 if (tr[l, ev, cus] > 0).all() else np.nan for ev in range(19)])
     med = np.nanmedian(np.array(rows), axis=0) / 100
-    print(" | ".join(f"{NAMES[ev]} {med[ev]:.1f}" for ev in range(16) if np.isfinite(med[ev])))
+    print(" | ".join(f"{NAMES[ev]} {med[ev]:.1f}" for ev in range(19) if np.isfinite(med[ev])))
 per = [np.median(tr[l, 11] - tr[l - 1, 11]) / 100 for l in range(1, layers)]
 print("layer period (down done -> down done, median over CUs) us:", np.round(per, 1))
