@@ -211,9 +211,9 @@ static void local_engine() {
   for (int i = 0; i < C; ++i) ch[i] = mtts_channel_sampling{i % 2, 1.0f + 0.5f * i, i == 0 ? 20 : 0, 0.9f, 1.2f};
   OK(mtts_local_set_sampling(e, ch.data(), C));
   OK(mtts_local_generate(e, d_ids, nullptr, B, T, 8, -1, &sp, 4, &n, nullptr));
-  ch[0] = mtts_channel_sampling{1, 1.0f, 0, 1.0f, 1.0f};  // sampled text without top_k: refused
+  ch[0] = mtts_channel_sampling{1, 1.0f, 0, 1.0f, 1.0f};  // sampled text without top_k: the key-bin walk
   OK(mtts_local_set_sampling(e, ch.data(), C));
-  EXPECT(mtts_local_generate(e, d_ids, nullptr, B, T, 8, -1, &sp, 4, &n, nullptr) == MTTS_E_UNSUPPORTED, "text top_k");
+  OK(mtts_local_generate(e, d_ids, nullptr, B, T, 8, -1, &sp, 4, &n, nullptr));
   OK(mtts_local_set_sampling(e, nullptr, 0));
   EXPECT(mtts_local_set_sampling(e, ch.data(), C + 1) == MTTS_E_INVALID, "too many channels");
   uint64_t fb = 0;
