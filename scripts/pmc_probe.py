@@ -13,6 +13,7 @@ kernel of the captured decode graph) for rocprofv3 PMC passes:
 HBM traffic per launch = 2 x FETCH_SIZE (gfx950 tallies wide coalesced reads at half their
 bytes, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both in KiB as rocprofv3 reports them."""
 import argparse
+import collections
 import csv
 import glob
 import json
@@ -67,6 +68,7 @@ def summarize_ttsd(d):
     for cname in sorted({r[2] for r in rows}):
         seq = sorted((r for r in rows if r[2] == cname), key=lambda r: r[0])
         seg, dec_seen, tot = -1, True, [0.0, 0.0]
+        per_k = [collections.defaultdict(float), collections.defaultdict(float)]
         for _, kname, _, v in seq:
             if "gemm" in kname and dec_seen:
                 seg, dec_seen = seg + 1, False
@@ -74,7 +76,12 @@ def summarize_ttsd(d):
                 dec_seen = True
             if 0 <= seg < 2:
                 tot[seg] += v
-        out[cname] = {"segments": seg + 1, "gen_kib": tot, "per_step_kib": (tot[1] - tot[0]) / (TTSD_B - TTSD_A)}
+                per_k[seg][kname.split("(")[0]] += v
+        steps = TTSD_B - TTSD_A
+        by_kernel = {k: round((per_k[1][k] - per_k[0].get(k, 0.0)) / steps, 1) for k in per_k[1]}
+        by_kernel = dict(sorted(by_kernel.items(), key=lambda kv: -kv[1])[:8])
+        out[cname] = {"segments": seg + 1, "gen_kib": tot, "per_step_kib": (tot[1] - tot[0]) / steps,
+                      "per_step_kib_by_kernel": by_kernel}
     fetch = out.get("FETCH_SIZE", {}).get("per_step_kib")
     write = out.get("WRITE_SIZE", {}).get("per_step_kib")
     if fetch is not None and write is not None:
