@@ -127,7 +127,7 @@ int mtts_pse_long_active(const mtts_engine* eng);
 int mtts_pse_ctx_max(const mtts_engine* eng);
 /* MossTTSLocal engines: 1 when each channel of a frame's depth stage (adapter in, the depth layers,
  * local_transformer.norm, adapter out) runs as one persistent launch (lpse.hip; the 1.7B depth
- * shape, <= 8 rows, 256 CUs; MTTS_LPSE=0 at creation turns it off), else 0.  A timed-out launch
+ * shape, <= 8 rows, 256 CUs; opt-in: MTTS_LPSE=1 at creation), else 0.  A timed-out launch
  * is handled like the Delay launch's: mtts_generate_poll reports MTTS_E_PSE_TIMEOUT and the engine
  * continues on the per-op launches (mtts_local_generate restarts once); mtts_local_forward checks
  * its own launches and recomputes the frame. */
