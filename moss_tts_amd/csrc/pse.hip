@@ -66,6 +66,9 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_CSLEEP
 #define PSE_CSLEEP 0  // s_sleep of a consumer waiting for a ring slot
 #endif
+#ifndef PSE_SLICE_OLDS
+#define PSE_SLICE_OLDS 1  // attention / slice running output in LDS (0: in registers)
+#endif
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
 #endif
@@ -699,11 +702,23 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   float m_run = -INFINITY, l_run = 0.f;
   // the running P.V output of the unit's HU real q rows: MFMA D rows 0 .. HU-1 (lanes 0-15, first
   // HU of each lane's 4 rows); the padding rows are never kept (HU x DT instead of 4 x DT VGPRs)
-  float o_run[DT][HU];
+  // HU x DT values, kept in this wave's rows of acc_s (PSE_SLICE_OLDS, lanes g4 == 0 own them: the
+  // chunk loop's register peak drops by DT x HU VGPRs, so this noinline callee touches fewer
+  // callee-saved stripes, each saved to scratch and restored per call) or in registers
+  float o_run[PSE_SLICE_OLDS ? 1 : DT][HU];
+  float* o_s = acc_s + w * HU * D + c16;
+  if constexpr (PSE_SLICE_OLDS) {
+    if (g4 == 0)
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
+        for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = 0.f;
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
+  }
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
     const int k0 = ch * KW;
     {
@@ -741,13 +756,16 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
       }
     mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
     mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    // p relative to the running max, so P.V accumulates straight into the running output
+    const float mn = fmaxf(m_run, mc);
+    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
     float lc = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       float pr4[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
+        const float p = (mn == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mn);
         lc += p;
         pr4[r] = p;
       }
@@ -758,26 +776,28 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     }
     lc += __shfl_xor(lc, 16, 64);
     lc += __shfl_xor(lc, 32, 64);
-    const float mn = fmaxf(m_run, mc);
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
-    l_run = l_run * alpha + lc * beta;
+    l_run = l_run * alpha + lc;
     m_run = mn;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
-    float al[HU], be[HU];
+    float al[HU];
 #pragma unroll
-    for (int r = 0; r < HU; ++r) {
-      al[r] = __shfl(alpha, r, 64);
-      be[r] = __shfl(beta, r, 64);
-    }
+    for (int r = 0; r < HU; ++r) al[r] = __shfl(alpha, r, 64);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
-                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < HU; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
+      for (int r = 0; r < HU; ++r) o4[r] = (PSE_SLICE_OLDS ? o_s[r * D + dt * 16] : o_run[PSE_SLICE_OLDS ? 0 : dt][r]) * al[r];
+      o4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]), o4, 0, 0, 0);
+      if constexpr (PSE_SLICE_OLDS) {
+        if (g4 == 0)
+#pragma unroll
+          for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o4[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < HU; ++r) o_run[PSE_SLICE_OLDS ? 0 : dt][r] = o4[r];
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -814,11 +834,11 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
-  if (g4 == 0)
+  if (!PSE_SLICE_OLDS && g4 == 0)
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int r = 0; r < HU; ++r) acc_s[(w * HU + r) * D + dt * 16 + c16] = o_run[dt][r];
+      for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o_run[PSE_SLICE_OLDS ? 0 : dt][r];
   cbar(x);
   if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 19);
   // ---- 4. merge (thread e / 2: 2 output dims of local head h = wave w) and publish ----
@@ -878,11 +898,22 @@ __host__ __device__ inline int pse_merge_unit(int c) {
 // qkv_gran), then per-wave online softmax over the slice's chunks (pse.hip attention()'s chunk
 // math, HU = 4), the 4 wave partials merged, (m, l, o) published unnormalised.  A merge unit also
 // gathers the new token's k / v partials (behind its chunks) and stashes its merge inputs.
-__device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, const int* pos_p, const uint8_t* mask,
-                                                         const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
-                                                         uint64_t* g_part, uint32_t* err, float eps, float scale,
-                                                         int Cmax, uint32_t epoch, int bar_gen, int l, int merge,
-                                                         uint32_t tq) {
+#ifndef PSE_SLICE_INLINE
+#define PSE_SLICE_INLINE 0
+#endif
+#if PSE_SLICE_INLINE
+#define PSE_SLICE_ATTR __attribute__((always_inline))
+#else
+#define PSE_SLICE_ATTR __attribute__((noinline))
+#endif
+// (one instantiation per role: a runtime merge flag joined the two chunk-loop forms into one
+// register allocation of 254 VGPRs, 172 / 182 apart, and every VGPR past v39 a noinline callee
+// touches is a callee-saved stripe spilled to scratch per call)
+template <bool merge>
+__device__ PSE_SLICE_ATTR int attention_slice(const PseLayer* Lp, const int* pos_p, const uint8_t* mask,
+                                              const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
+                                              uint64_t* g_part, uint32_t* err, float eps, float scale, int Cmax,
+                                              uint32_t epoch, int bar_gen, int l, uint32_t tq) {
   const int c = blockIdx.x;
   Ctx x{err, eps, 0, c, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64, epoch, bar_gen};
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = G_;
@@ -935,7 +966,7 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
     qnw = reinterpret_cast<const uint32_t*>(Lw.q_norm)[lane];
     pcs = reinterpret_cast<const uint32_t*>(cos_t + (size_t)pos * D)[lane];
     psn = reinterpret_cast<const uint32_t*>(sin_t + (size_t)pos * D)[lane];
-    if (merge) {
+    if constexpr (merge) {
       knw = reinterpret_cast<const uint32_t*>(Lw.k_norm)[lane];
       mnew = mask[pos];
     }
@@ -980,11 +1011,22 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
     if (i / D >= HU) q_s[i] = 0;
   cbar(x);
   float m_run = -INFINITY, l_run = 0.f;
-  float o_run[DT][HU];
+  // the running output: this wave's rows of acc_s (PSE_SLICE_OLDS, lanes g4 == 0 own them; 32 VGPRs
+  // fewer at the chunk loop's peak, so the callee touches fewer callee-saved stripes) or registers
+  float o_run[PSE_SLICE_OLDS ? 1 : DT][HU];
+  float* o_s = acc_s + w * HU * D + c16;
+  if constexpr (PSE_SLICE_OLDS) {
+    if (g4 == 0)
 #pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
+      for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
+        for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = 0.f;
+  } else {
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+      for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
+  }
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
     const int k0 = ch * KW;
     {
@@ -1019,13 +1061,16 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
       }
     mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
     mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
+    // p relative to the running max, so P.V accumulates straight into o_run (no per-tile temporaries)
+    const float mn = fmaxf(m_run, mc);
+    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
     float lc = 0.f;
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       float pr4[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
+        const float p = (mn == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mn);
         lc += p;
         pr4[r] = p;
       }
@@ -1036,37 +1081,40 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
     }
     lc += __shfl_xor(lc, 16, 64);
     lc += __shfl_xor(lc, 32, 64);
-    const float mn = fmaxf(m_run, mc);
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
-    l_run = l_run * alpha + lc * beta;
+    l_run = l_run * alpha + lc;
     m_run = mn;
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
-    float al[HU], be[HU];
+    float al[HU];
 #pragma unroll
-    for (int r = 0; r < HU; ++r) {
-      al[r] = __shfl(alpha, r, 64);
-      be[r] = __shfl(beta, r, 64);
-    }
+    for (int r = 0; r < HU; ++r) al[r] = __shfl(alpha, r, 64);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
-                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      f32x4 o4;
 #pragma unroll
-      for (int r = 0; r < HU; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
+      for (int r = 0; r < HU; ++r) o4[r] = (PSE_SLICE_OLDS ? o_s[r * D + dt * 16] : o_run[PSE_SLICE_OLDS ? 0 : dt][r]) * al[r];
+      o4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]), o4, 0, 0, 0);
+      if constexpr (PSE_SLICE_OLDS) {
+        if (g4 == 0)
+#pragma unroll
+          for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o4[r];
+      } else {
+#pragma unroll
+        for (int r = 0; r < HU; ++r) o_run[PSE_SLICE_OLDS ? 0 : dt][r] = o4[r];
+      }
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   };
   auto chunks = [&]() {
+#pragma unroll 1
     for (int ch = ch0; ch < ce; ch += CW) {
       if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
       compute(ch, ktA, vtA, mkA);
     }
   };
-  if (merge) {  // the new token's k / v partials, gathered behind this slice's chunks
+  if constexpr (merge) {  // the new token's k / v partials, gathered behind this slice's chunks
     if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + NQ, NKV, tq, graw32 + NQ, NKV, nullptr,
                                                  chunks))
       return -1;
@@ -1078,11 +1126,11 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
-  if (g4 == 0)
+  if (!PSE_SLICE_OLDS && g4 == 0)
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-      for (int r = 0; r < HU; ++r) acc_s[(w * HU + r) * D + dt * 16 + c16] = o_run[dt][r];
+      for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o_run[PSE_SLICE_OLDS ? 0 : dt][r];
   cbar(x);
   // the 4 wave partials -> the slice's (m, l, o) of q head h (thread: 2 dims)
   {
@@ -1116,7 +1164,7 @@ __device__ __attribute__((noinline)) int attention_slice(const PseLayer* Lp, con
 // (score q . k, p = 1: TF/integrations/sdpa_attention.py:79-166 over keys 0..pos), k RMSNorm + RoPE,
 // k / v appended by the group's first unit (TF/cache_utils.py:127-145), the output published as
 // the o_proj input granules.  q_s / graw / the stash still hold this CU's slice inputs.
-__device__ __attribute__((noinline)) int attention_merge(const PseLayer* Lp, const int* pos_p, uint64_t* g_part,
+__device__ PSE_SLICE_ATTR int attention_merge(const PseLayer* Lp, const int* pos_p, uint64_t* g_part,
                                                          uint64_t* g_att, uint32_t* err, float eps, float scale,
                                                          int Cmax, uint32_t epoch, int bar_gen, int l, int u) {
   const int c = blockIdx.x;
@@ -1477,8 +1525,10 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         }
         if constexpr (LONG) {
           // every CU: its slice of the KV head's cached keys; merge units then combine the slices
-          int bg = attention_slice(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_part, a.err, a.eps, a.scale,
-                                   a.Cmax, epoch, x.bar_gen, l, MRG ? 1 : 0, tq);
+          int bg = MRG ? attention_slice<true>(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_part, a.err,
+                                               a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, tq)
+                       : attention_slice<false>(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_part, a.err,
+                                                a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, tq);
           if (bg >= 0) x.bar_gen = bg;
           if (MRG && bg >= 0) {
             bg = attention_merge(a.L + l, a.pos, a.g_part, a.g_att, a.err, a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l,
