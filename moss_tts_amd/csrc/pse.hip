@@ -37,6 +37,7 @@
 // no fences) and granules of earlier launches / layers never match.  Every spin is bounded: a
 // stuck wait sets the error word, and the launch drains.
 #include "kernels.h"
+#include "pse_chunk.h"
 
 namespace mtts {
 
@@ -65,9 +66,6 @@ constexpr int THREADS = (LW + CW) * 64;
 #define PSE_PRIO_DOWN() do { if (PSE_PPRIO) __builtin_amdgcn_s_setprio(0); } while (0)
 #ifndef PSE_CSLEEP
 #define PSE_CSLEEP 0  // s_sleep of a consumer waiting for a ring slot
-#endif
-#ifndef PSE_SLICE_OLDS
-#define PSE_SLICE_OLDS 1  // attention / slice running output in LDS (0: in registers)
 #endif
 #ifndef PSE_APAUSE
 #define PSE_APAUSE 2
@@ -700,107 +698,10 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   cbar(x);
   // ---- 2. the cached keys ----
   float m_run = -INFINITY, l_run = 0.f;
-  // the running P.V output of the unit's HU real q rows: MFMA D rows 0 .. HU-1 (lanes 0-15, first
-  // HU of each lane's 4 rows); the padding rows are never kept (HU x DT instead of 4 x DT VGPRs)
-  // HU x DT values, kept in this wave's rows of acc_s (PSE_SLICE_OLDS, lanes g4 == 0 own them: the
-  // chunk loop's register peak drops by DT x HU VGPRs, so this noinline callee touches fewer
-  // callee-saved stripes, each saved to scratch and restored per call) or in registers
-  float o_run[PSE_SLICE_OLDS ? 1 : DT][HU];
-  float* o_s = acc_s + w * HU * D + c16;
-  if constexpr (PSE_SLICE_OLDS) {
-    if (g4 == 0)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = 0.f;
-  } else {
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
-  }
+  float* o_s = acc_s + w * HU * D + c16;  // the running output (pse_chunk.h)
+  pse_chunk_init<HU, D>(g4, o_s);
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
-    const int k0 = ch * KW;
-    {
-      // the V^T fragment holding pos also read keys pos .. kb+7: cache rows never written (or
-      // stale after a capacity change).  Their p is 0, but 0 * NaN / Inf in the P.V MFMA is NaN:
-      // zero those 16-bit lanes (as attn_body.h's per-op attention does)
-      const int nv = pos - (k0 + 8 * g4);  // keys of this lane's fragments below pos
-      uint32_t vm[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) vt[dt][q] &= vm[q];
-    }
-    f32x4 sacc[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < QS; ++s2)
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][s2]),
-                                                         *reinterpret_cast<const bf16x8*>(&q_s[c16 * D + s2 * 32 + 8 * g4]),
-                                                         sacc[t], 0, 0, 0);
-    }
-    float sv[2][4], mc = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + t * 16 + g4 * 4 + r;
-        const bool valid = key < pos && ((mk[t] >> (8 * r)) & 0xffu);
-        sv[t][r] = valid ? sacc[t][r] * scale : -INFINITY;
-        mc = fmaxf(mc, sv[t][r]);
-      }
-    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
-    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
-    // p relative to the running max, so P.V accumulates straight into the running output
-    const float mn = fmaxf(m_run, mc);
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-    float lc = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float pr4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (mn == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mn);
-        lc += p;
-        pr4[r] = p;
-      }
-      uint2 pk;
-      pk.x = pack2(pr4[0], pr4[1]);
-      pk.y = pack2(pr4[2], pr4[3]);
-      *reinterpret_cast<uint2*>(&p_s[(w * 16 + c16) * KW + t * 16 + g4 * 4]) = pk;
-    }
-    lc += __shfl_xor(lc, 16, 64);
-    lc += __shfl_xor(lc, 32, 64);
-    l_run = l_run * alpha + lc;
-    m_run = mn;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
-    float al[HU];
-#pragma unroll
-    for (int r = 0; r < HU; ++r) al[r] = __shfl(alpha, r, 64);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      f32x4 o4 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o4[r] = (PSE_SLICE_OLDS ? o_s[r * D + dt * 16] : o_run[PSE_SLICE_OLDS ? 0 : dt][r]) * al[r];
-      o4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]), o4, 0, 0, 0);
-      if constexpr (PSE_SLICE_OLDS) {
-        if (g4 == 0)
-#pragma unroll
-          for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o4[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < HU; ++r) o_run[PSE_SLICE_OLDS ? 0 : dt][r] = o4[r];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    pse_chunk_step<HU, D>(ch * KW, pos, g4, c16, kt, vt, mk, q_s, p_s + w * 16 * KW, o_s, scale, m_run, l_run);
   };
   auto chunks = [&]() {
     if (w == 0) PSE_STAMP(l, 16);
@@ -834,11 +735,6 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
-  if (!PSE_SLICE_OLDS && g4 == 0)
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o_run[PSE_SLICE_OLDS ? 0 : dt][r];
   cbar(x);
   if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 19);
   // ---- 4. merge (thread e / 2: 2 output dims of local head h = wave w) and publish ----
@@ -1011,101 +907,10 @@ __device__ PSE_SLICE_ATTR int attention_slice(const PseLayer* Lp, const int* pos
     if (i / D >= HU) q_s[i] = 0;
   cbar(x);
   float m_run = -INFINITY, l_run = 0.f;
-  // the running output: this wave's rows of acc_s (PSE_SLICE_OLDS, lanes g4 == 0 own them; 32 VGPRs
-  // fewer at the chunk loop's peak, so the callee touches fewer callee-saved stripes) or registers
-  float o_run[PSE_SLICE_OLDS ? 1 : DT][HU];
-  float* o_s = acc_s + w * HU * D + c16;
-  if constexpr (PSE_SLICE_OLDS) {
-    if (g4 == 0)
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = 0.f;
-  } else {
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
-  }
+  float* o_s = acc_s + w * HU * D + c16;  // the running output (pse_chunk.h)
+  pse_chunk_init<HU, D>(g4, o_s);
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
-    const int k0 = ch * KW;
-    {
-      const int nv = pos - (k0 + 8 * g4);  // V^T lanes of keys >= pos: zeroed (pse.hip attention())
-      uint32_t vm[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) vt[dt][q] &= vm[q];
-    }
-    f32x4 sacc[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < QS; ++s2)
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][s2]),
-                                                         *reinterpret_cast<const bf16x8*>(&q_s[c16 * D + s2 * 32 + 8 * g4]),
-                                                         sacc[t], 0, 0, 0);
-    }
-    float sv[2][4], mc = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + t * 16 + g4 * 4 + r;
-        const bool valid = key < pos && ((mk[t] >> (8 * r)) & 0xffu);
-        sv[t][r] = valid ? sacc[t][r] * scale : -INFINITY;
-        mc = fmaxf(mc, sv[t][r]);
-      }
-    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
-    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
-    // p relative to the running max, so P.V accumulates straight into o_run (no per-tile temporaries)
-    const float mn = fmaxf(m_run, mc);
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-    float lc = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float pr4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (mn == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mn);
-        lc += p;
-        pr4[r] = p;
-      }
-      uint2 pk;
-      pk.x = pack2(pr4[0], pr4[1]);
-      pk.y = pack2(pr4[2], pr4[3]);
-      *reinterpret_cast<uint2*>(&p_s[(w * 16 + c16) * KW + t * 16 + g4 * 4]) = pk;
-    }
-    lc += __shfl_xor(lc, 16, 64);
-    lc += __shfl_xor(lc, 32, 64);
-    l_run = l_run * alpha + lc;
-    m_run = mn;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
-    float al[HU];
-#pragma unroll
-    for (int r = 0; r < HU; ++r) al[r] = __shfl(alpha, r, 64);
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      f32x4 o4;
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o4[r] = (PSE_SLICE_OLDS ? o_s[r * D + dt * 16] : o_run[PSE_SLICE_OLDS ? 0 : dt][r]) * al[r];
-      o4 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]), o4, 0, 0, 0);
-      if constexpr (PSE_SLICE_OLDS) {
-        if (g4 == 0)
-#pragma unroll
-          for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o4[r];
-      } else {
-#pragma unroll
-        for (int r = 0; r < HU; ++r) o_run[PSE_SLICE_OLDS ? 0 : dt][r] = o4[r];
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    pse_chunk_step<HU, D>(ch * KW, pos, g4, c16, kt, vt, mk, q_s, p_s + w * 16 * KW, o_s, scale, m_run, l_run);
   };
   auto chunks = [&]() {
 #pragma unroll 1
@@ -1126,11 +931,6 @@ __device__ PSE_SLICE_ATTR int attention_slice(const PseLayer* Lp, const int* pos
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
-  if (!PSE_SLICE_OLDS && g4 == 0)
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o_s[r * D + dt * 16] = o_run[PSE_SLICE_OLDS ? 0 : dt][r];
   cbar(x);
   // the 4 wave partials -> the slice's (m, l, o) of q head h (thread: 2 dims)
   {

@@ -20,6 +20,7 @@
 //    of its row (each row has its own cache and mask); the units' CUs pause their loaders while the
 //    attention runs, their k|v half tile goes to the neighbour CU (as in pse.hip).
 #include "kernels.h"
+#include "pse_chunk.h"
 
 namespace mtts {
 
@@ -567,86 +568,10 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
   cbar(x);
   // ---- 2. the cached keys ----
   float m_run = -INFINITY, l_run = 0.f;
-  float o_run[DT][HU];
-#pragma unroll
-  for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-    for (int r = 0; r < HU; ++r) o_run[dt][r] = 0.f;
+  float* o_s = acc_s + w * HU * D + c16;  // the running output (pse_chunk.h)
+  pse_chunk_init<HU, D>(g4, o_s);
   auto compute = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
-    const int k0 = ch * KW;
-    {
-      // keys pos .. kb+7 of the V^T fragment holding pos: never written (or stale) -- zeroed (pse.hip)
-      const int nv = pos - (k0 + 8 * g4);
-      uint32_t vm[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
-#pragma unroll
-      for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-        for (int q = 0; q < 4; ++q) vt[dt][q] &= vm[q];
-    }
-    f32x4 sacc[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int s2 = 0; s2 < QS; ++s2)
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kt[t][s2]),
-                                                         *reinterpret_cast<const bf16x8*>(&q_s[c16 * D + s2 * 32 + 8 * g4]),
-                                                         sacc[t], 0, 0, 0);
-    }
-    float sv[2][4], mc = -INFINITY;
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = k0 + t * 16 + g4 * 4 + r;
-        const bool valid = key < pos && ((mk[t] >> (8 * r)) & 0xffu);
-        sv[t][r] = valid ? sacc[t][r] * scale : -INFINITY;
-        mc = fmaxf(mc, sv[t][r]);
-      }
-    mc = fmaxf(mc, __shfl_xor(mc, 16, 64));
-    mc = fmaxf(mc, __shfl_xor(mc, 32, 64));
-    float lc = 0.f;
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      float pr4[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float p = (mc == -INFINITY || sv[t][r] == -INFINITY) ? 0.f : expf(sv[t][r] - mc);
-        lc += p;
-        pr4[r] = p;
-      }
-      uint2 pk;
-      pk.x = pack2(pr4[0], pr4[1]);
-      pk.y = pack2(pr4[2], pr4[3]);
-      *reinterpret_cast<uint2*>(&p_s[(w * 16 + c16) * KW + t * 16 + g4 * 4]) = pk;
-    }
-    lc += __shfl_xor(lc, 16, 64);
-    lc += __shfl_xor(lc, 32, 64);
-    const float mn = fmaxf(m_run, mc);
-    const float alpha = (m_run == -INFINITY) ? 0.f : expf(m_run - mn);
-    const float beta = (mc == -INFINITY) ? 0.f : expf(mc - mn);
-    l_run = l_run * alpha + lc * beta;
-    m_run = mn;
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[(w * 16 + c16) * KW + 8 * g4]);
-    float al[HU], be[HU];
-#pragma unroll
-    for (int r = 0; r < HU; ++r) {
-      al[r] = __shfl(alpha, r, 64);
-      be[r] = __shfl(beta, r, 64);
-    }
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt) {
-      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
-                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int r = 0; r < HU; ++r) o_run[dt][r] = o_run[dt][r] * al[r] + be[r] * oc[r];
-    }
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    pse_chunk_step<HU, D>(ch * KW, pos, g4, c16, kt, vt, mk, q_s, p_s + w * 16 * KW, o_s, scale, m_run, l_run);
   };
   auto chunks = [&]() {
 #if PSE4_ADB
@@ -694,11 +619,6 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
     ml_s[(w * HU + lane) * 2] = m_run;
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
-  if (g4 == 0)
-#pragma unroll
-    for (int dt = 0; dt < DT; ++dt)
-#pragma unroll
-      for (int r = 0; r < HU; ++r) acc_s[(w * HU + r) * D + dt * 16 + c16] = o_run[dt][r];
   cbar(x);
   // ---- 4. merge (thread e / 2: 2 dims of local head e / D) and publish ----
   const int e = 2 * x.tid, h = e / D, d = e % D;
