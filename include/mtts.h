@@ -253,6 +253,14 @@ int mtts_k_gemv_splitk(const uint16_t* wpacked, const uint16_t* x, int ldx, uint
  * add + per-16-column sums of squares into ss_out when non-NULL, 2 swiglu) */
 int mtts_k_gemm(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                 int ldres, int M, int N, int K, int epi, float* ss_out, int ld_ss_out, void* stream);
+/* the prefill projections' packed-activation form (the engine's >= 128-row prompts): x_packed holds
+ * ceil(M / 16) token tiles in the fragment order xpkT_index (kernels.h: u16 index
+ * ((((k / 32) T + m / 16) 64 + m % 16 + 16 ((k % 32) / 8)) 8 + k % 8), T = ceil(M / 16)); y row-major
+ * (epi 0 / 1) or, y_packed = 1 (epi 2 only, the down projection's input), packed the same way over
+ * N columns.  ws_dev / ws_floats: fp32 split-K partials (0: no split). */
+int mtts_k_gemm_packed(const uint16_t* wpacked, const uint16_t* x_packed, uint16_t* y, int ldy, int y_packed,
+                       const uint16_t* res, int ldres, int M, int N, int K, int epi, float* ss_out, int ld_ss_out,
+                       float* ws_dev, size_t ws_floats, void* stream);
 int mtts_k_rmsnorm(const uint16_t* x, size_t x_off, size_t x_stride, const uint16_t* w, uint16_t* y, int M, int H,
                    float eps, void* stream);
 int mtts_k_embed(const int64_t* ids, int C, const uint16_t* emb_text, const uint16_t* emb_audio, int audio_rows,

@@ -106,6 +106,7 @@ _SIGS = {
     "mtts_k_gemv": (I, [P, P, I, P, I, P, I, I, I, I, I, I, I, I, P]),
     "mtts_k_gemv_ex": (I, [P, P, I, P, I, P, I, I, I, I, I, P, I, I, P, F, P, I, I, P]),
     "mtts_k_gemm": (I, [P, P, I, P, I, P, I, I, I, I, I, P, I, P]),
+    "mtts_k_gemm_packed": (I, [P, P, P, I, I, P, I, I, I, I, I, P, I, P, SZ, P]),
     "mtts_k_gemv_splitk_ws_bytes": (SZ, [I, I]),
     "mtts_k_gemv_splitk_splits": (I, [I, I, I]),
     "mtts_k_gemv_splitk": (I, [P, P, I, P, I, P, I, I, I, I, I, P, I, P, P]),

@@ -202,40 +202,51 @@ __global__ __launch_bounds__(G * 64) void attn_prefill_kernel(AttnArgs a) {
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt) o_run[dt] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  for (int k0 = 0; k0 <= kend; k0 += 32) {
-    // ---- S = Q . K^T for keys k0 .. k0+31 (two 16-key tiles) ----
-    f32x4 sacc[2];
-    uint32_t mk[2];
+  // K / V^T / mask of a 32-key chunk: branch-free buffer loads (keys past kend read zero through
+  // an out-of-range offset), so the next chunk's loads are in flight while this one computes
+  constexpr uint32_t OOBA = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(kbase), 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(vbase), 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mrow), 0, Cmax, 0x00020000);
+  auto load_chunk = [&](int k0, u32x4 (&kf)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
 #pragma unroll
     for (int t = 0; t < 2; ++t) {
       const int key = k0 + t * 16 + c16;
-      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-      mk[t] = key <= kend ? mrow[key] : 0u;
+      const bool ok = key <= kend;
+      mk[t] = __builtin_amdgcn_raw_buffer_load_b8(mrs, ok ? (uint32_t)key : OOBA, 0, 0);
 #pragma unroll
-      for (int st = 0; st < QS; ++st) {
-        const u32x4 kf = (key <= kend && st * 32 + 8 * g4 < D)
-                             ? *reinterpret_cast<const u32x4*>(kbase + (size_t)key * D + st * 32 + 8 * g4)
-                             : (u32x4){0u, 0u, 0u, 0u};
-        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[st], __builtin_bit_cast(bf16x8, kf), sacc[t], 0, 0, 0);
-      }
+      for (int st = 0; st < QS; ++st)
+        kf[t][st] = __builtin_amdgcn_raw_buffer_load_b128(
+            krs, (ok && st * 32 + 8 * g4 < D) ? (uint32_t)(key * D + st * 32 + 8 * g4) * 2u : OOBA, 0, 0);
     }
-    // V^T B-operand fragments: dim dt*16 + c16, keys k0 + 8*g4 .. +7 (zero beyond kend)
-    u32x4 vt[DT];
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
       const int kb = k0 + 8 * g4;
-      vt[dt] = kb <= kend ? *reinterpret_cast<const u32x4*>(vbase + (size_t)(dt * 16 + c16) * Cmax + kb)
-                          : (u32x4){0u, 0u, 0u, 0u};
-      if (kb <= kend && kb + 7 > kend) {
-        u32x4 v = vt[dt];
+      vt[dt] = __builtin_amdgcn_raw_buffer_load_b128(vrs, kb <= kend ? (uint32_t)((dt * 16 + c16) * Cmax + kb) * 2u : OOBA,
+                                                     0, 0);
+    }
+  };
+  auto compute = [&](int k0, const u32x4 (&kf)[2][QS], u32x4 (&vt)[DT], const uint32_t (&mk)[2]) {
+    // ---- S = Q . K^T for keys k0 .. k0+31 (two 16-key tiles) ----
+    f32x4 sacc[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t lo = kb + 2 * i <= kend ? (v[i] & 0xffffu) : 0u;
-          const uint32_t hi = kb + 2 * i + 1 <= kend ? (v[i] >> 16) : 0u;
-          v[i] = lo | (hi << 16);
-        }
-        vt[dt] = v;
-      }
+    for (int t = 0; t < 2; ++t) {
+      sacc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int st = 0; st < QS; ++st)
+        sacc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[st], __builtin_bit_cast(bf16x8, kf[t][st]), sacc[t], 0, 0, 0);
+    }
+    // V^T B-operand fragments: dim dt*16 + c16, keys k0 + 8*g4 .. +7; keys past kend zeroed (cache
+    // rows not yet written: 0 * NaN in the P.V MFMA would be NaN)
+    {
+      const int nv = kend + 1 - (k0 + 8 * g4);
+      uint32_t vm[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vt[dt][q] &= vm[q];
     }
     // ---- online softmax per token row (row = g4*4 + i, keys over the 16-lane group) ----
     float alpha[4];
@@ -268,17 +279,38 @@ __global__ __launch_bounds__(G * 64) void attn_prefill_kernel(AttnArgs a) {
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    // ---- O = O * alpha + P . V ----
+    // ---- O = O * alpha + P . V (accumulated in the MFMA) ----
     const bf16x8 pf = *reinterpret_cast<const bf16x8*>(&p_s[wave][c16][8 * g4]);
 #pragma unroll
     for (int dt = 0; dt < DT; ++dt) {
-      const f32x4 oc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]),
-                                                              (f32x4){0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      f32x4 o4 = o_run[dt];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) o_run[dt][i] = o_run[dt][i] * alpha[i] + oc[i];
+      for (int i = 0; i < 4; ++i) o4[i] *= alpha[i];
+      o_run[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, __builtin_bit_cast(bf16x8, vt[dt]), o4, 0, 0, 0);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  };
+  u32x4 kA[2][QS], vA[DT];
+  uint32_t mA[2];
+  load_chunk(0, kA, vA, mA);
+  if constexpr (G <= 4) {
+    // two chunks per iteration, each one's loads issued while the other computes (256 VGPRs: two
+    // waves per SIMD; 8-wave blocks keep one chunk in flight)
+    u32x4 kB[2][QS], vB[DT];
+    uint32_t mB[2];
+    for (int k0 = 0; k0 <= kend; k0 += 64) {
+      if (k0 + 32 <= kend) load_chunk(k0 + 32, kB, vB, mB);
+      compute(k0, kA, vA, mA);
+      if (k0 + 32 > kend) break;
+      if (k0 + 64 <= kend) load_chunk(k0 + 64, kA, vA, mA);
+      compute(k0 + 32, kB, vB, mB);
+    }
+  } else {
+    for (int k0 = 0; k0 <= kend; k0 += 32) {
+      if (k0 > 0) load_chunk(k0, kA, vA, mA);
+      compute(k0, kA, vA, mA);
+    }
   }
   // ---- normalise and store: token s0 + g4*4 + i, dims dt*16 + c16 ----
 #pragma unroll

@@ -1275,6 +1275,20 @@ extern "C" int mtts_k_gemm(const uint16_t* w, const uint16_t* x, int ldx, uint16
   return 0;
 }
 
+extern "C" int mtts_k_gemm_packed(const uint16_t* w, const uint16_t* x, uint16_t* y, int ldy, int y_packed,
+                                  const uint16_t* res, int ldres, int M, int N, int K, int epi, float* ss_out,
+                                  int ld_ss_out, float* ws, size_t ws_floats, void* stream) {
+  if (K % 64 || M < 128) return fail(MTTS_E_INVALID, "packed prefill GEMM: K % 64 == 0 and M >= 128");
+  if (epi != EPI_STORE && epi != EPI_RESADD && epi != EPI_SWIGLU) return fail(MTTS_E_INVALID, "epi 0/1/2 only");
+  if (y_packed && epi != EPI_SWIGLU) return fail(MTTS_E_INVALID, "packed outputs: epi 2 only");
+  GemvArgs a = gemv_args(w, x, K, y, ldy, M, N, K);
+  a.res = res; a.ldres = ldres; a.ss_out = ss_out; a.ld_ss_out = ld_ss_out;
+  a.x_packed = 1; a.y_packed = y_packed ? 1 : 0; a.pk_tiles = (M + 15) / 16;
+  a.ws = ws; a.ws_floats = ws ? ws_floats : 0;
+  HIPCHK(gemm_ex(a, epi, (hipStream_t)stream));
+  return 0;
+}
+
 // full-control GEMV (fused norm prologue, sum-of-squares epilogue, waves-per-block override)
 extern "C" int mtts_k_gemv_ex(const uint16_t* w, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                               int ldres, int B, int N, int K, int epi, const float* ss_in, int ld_ss, int n_ss,

@@ -266,55 +266,61 @@ static void gemm_launch(const GemvArgs& a, int n_tiles, hipStream_t s) {
   }
 }
 
-// Split-K reduce + epilogue: thread (token m, 16-column output tile) sums the S partials in
-// split order (deterministic) and applies the same epilogue as gemm2_kernel (bf16 rounding
-// points of TF/models/qwen3/modeling_qwen3.py:81-83, 311, 322).
+// Split-K reduce + epilogue: thread (token m, 16-column output tile ot, 4-column group q) sums the
+// S partials in split order (deterministic) and applies the same epilogue as gemm2_kernel (bf16
+// rounding points of TF/models/qwen3/modeling_qwen3.py:81-83, 311, 322).  Four threads per tile (a
+// 181-row o_proj / down reduce is 185 K threads, one f32x4 load per split each; one thread per tile
+// ran 12 us on 46 K latency-bound threads); the residual epilogue's per-tile sum of squares adds
+// the groups as the GEMM epilogue does, (s0 + s1) + (s2 + s3), across the 4 adjacent lanes.
 template <int EPI>
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
   const int n_ot = (a.N + 15) / 16;
   const int id = blockIdx.x * 256 + threadIdx.x;
-  if (id >= a.B * n_ot) return;
-  const int m = id / n_ot, ot = id - m * n_ot;
+  const bool live = id < a.B * n_ot * 4;
+  const int t = live ? id >> 2 : 0, q = id & 3;
+  const int m = t / n_ot, ot = t - m * n_ot;
   const size_t ld = (size_t)a.n_row_tiles * 16;
   const float* p = a.ws + (size_t)m * ld;
   const size_t zs = (size_t)a.B * ld;
-  float o[16];
-  float ssq = 0.f;
+  f32x4 g = (f32x4){0.f, 0.f, 0.f, 0.f}, u = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int c = (EPI == EPI_SWIGLU ? 2 * ot : ot) * 16 + q * 4;
+  for (int z = 0; z < S; ++z) {
+    g += *reinterpret_cast<const f32x4*>(p + z * zs + c);
+    if constexpr (EPI == EPI_SWIGLU) u += *reinterpret_cast<const f32x4*>(p + z * zs + c + 16);
+  }
+  float o[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    f32x4 g = (f32x4){0.f, 0.f, 0.f, 0.f}, u = (f32x4){0.f, 0.f, 0.f, 0.f};
-    const int c = (EPI == EPI_SWIGLU ? 2 * ot : ot) * 16 + q * 4;
-    for (int z = 0; z < S; ++z) {
-      g += *reinterpret_cast<const f32x4*>(p + z * zs + c);
-      if constexpr (EPI == EPI_SWIGLU) u += *reinterpret_cast<const f32x4*>(p + z * zs + c + 16);
+  for (int i = 0; i < 4; ++i) {
+    const int n = ot * 16 + q * 4 + i;
+    float v;
+    if constexpr (EPI == EPI_STORE) {
+      v = rbf(g[i]);
+    } else if constexpr (EPI == EPI_RESADD) {
+      v = n < a.N ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(g[i])) : 0.f;
+    } else {
+      const float gg = rbf(g[i]), uu = rbf(u[i]);
+      v = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
     }
+    o[i] = v;
+  }
+  if (live) {
+    bf16_t* yr = a.y + (size_t)m * a.ldy + ot * 16 + q * 4;
+    if (ot * 16 + q * 4 + 3 < a.N && (a.ldy % 4) == 0) {
+      uint2 pk;
+      pk.x = pack2(o[0], o[1]);
+      pk.y = pack2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(yr) = pk;
+    } else {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = ot * 16 + q * 4 + i;
-      float v;
-      if constexpr (EPI == EPI_STORE) {
-        v = rbf(g[i]);
-      } else if constexpr (EPI == EPI_RESADD) {
-        v = n < a.N ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(g[i])) : 0.f;
-      } else {
-        const float gg = rbf(g[i]), uu = rbf(u[i]);
-        v = rbf(rbf(gg / (1.0f + expf(-gg))) * uu);
-      }
-      o[q * 4 + i] = v;
+      for (int i = 0; i < 4; ++i)
+        if (ot * 16 + q * 4 + i < a.N) yr[i] = f2bf(o[i]);
     }
   }
-  bf16_t* yr = a.y + (size_t)m * a.ldy + ot * 16;
-#pragma unroll
-  for (int i = 0; i < 16; ++i)
-    if (ot * 16 + i < a.N) yr[i] = f2bf(o[i]);
   if constexpr (EPI == EPI_RESADD) {
-    // per 4-column groups as the GEMM epilogue adds them (then across the 4 groups)
-    float s4[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-      s4[q] = (o[4 * q] * o[4 * q] + o[4 * q + 1] * o[4 * q + 1]) + (o[4 * q + 2] * o[4 * q + 2] + o[4 * q + 3] * o[4 * q + 3]);
-    ssq = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-    if (a.ss_out) a.ss_out[(size_t)m * a.ld_ss_out + ot] = ssq;
+    float s4 = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+    s4 += __shfl_xor(s4, 1, 64);
+    s4 += __shfl_xor(s4, 2, 64);
+    if (a.ss_out && live && q == 0) a.ss_out[(size_t)m * a.ld_ss_out + ot] = s4;
   }
 }
 
@@ -344,24 +350,37 @@ static int gemm_splits(const GemvArgs& a, int nx, int ny) {
 // 0.23-0.39, this 3-stage ring 105 vs 110 ms for the 32-utterance prefill; 4 stages 123 ms: at 72 KiB
 // the 128-row form fits two blocks per CU; profiles/r04_e_*).  SPLIT: blockIdx.z takes a K range and writes fp32
 // partials for gemm_splitk_reduce (few row blocks: o_proj / down at N 4,096).
+//
+// Shape <NWR, NWN, WR, WN, NST>: NWR x NWN waves, each WR weight row tiles x WN token tiles, an
+// NST-stage ring.  <2, 4, *, 4, 3> for long prompts; <3, 2, 2, 6, 8> for prompts of <= 192 token rows
+// (the batch-1 clone prefill, 181 rows): every token of the prompt in one block, so each weight
+// byte leaves HBM once, 96-row blocks (gate|up: 256 of them, one per CU), and seven 18 KiB stages
+// in flight per CU -- the HBM latency x bandwidth product (0.8 us x 8 TB/s under load,
+// profiles/r03_m_lat_probe.txt) is ~25 KiB of weights per CU, which gemm2_kernel's register-
+// staged k loop (issue, wait, 64 MFMAs) left idle most of the time (gate|up 89 us at 181 rows).
 #ifndef G3_NST
 #define G3_NST 3
 #endif
-template <int WR, int WN>
-constexpr size_t gemm3_lds_bytes() { return (size_t)G3_NST * (2 * WR + 4 * WN) * 1024; }
-template <int WR, int WN, int EPI, bool SPLIT = false>
-__global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
+
+template <int NWR, int NWN, int WR, int WN, int NST>
+constexpr size_t gemm3_lds_bytes() { return (size_t)NST * (NWR * WR + NWN * WN) * 1024; }
+template <int NWR, int NWN, int WR, int WN, int NST, int EPI, bool SPLIT = false>
+__global__ __launch_bounds__(NWR * NWN * 64) void gemm3_kernel(GemvArgs a) {
   typedef __attribute__((address_space(3))) void lvoid;
-  constexpr int BR = 2 * WR, BT = 4 * WN;          // row tiles / token tiles per block
+  constexpr int NW = NWR * NWN;                    // waves
+  constexpr int BR = NWR * WR, BT = NWN * WN;      // row tiles / token tiles per block
   constexpr int TILES = BR + BT;                   // 1 KiB tiles per stage (one k tile)
   constexpr int STAGE = TILES * 1024;
-  constexpr int TPW = TILES / 8;                   // loads per wave per stage
-  static_assert(TILES % 8 == 0, "tiles per stage split over the 8 waves");
-  static_assert(TPW * (G3_NST - 1) <= 63, "vmcnt counts the stages in flight");
+  constexpr int TPW = TILES / NW;                  // loads per wave per stage
+  static_assert(TILES % NW == 0, "tiles per stage split over the waves");
+  static_assert(TPW * (NST - 1) <= 63, "vmcnt counts the stages in flight");
+  static_assert(EPI != EPI_SWIGLU || WR % 2 == 0, "gate|up row tile pairs stay within a wave");
   extern __shared__ __attribute__((aligned(16))) unsigned char g3_lds[];
   const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int wr = wave & 1, wn = wave >> 1;
+  // (wave-uniform for the compiler: the LDS-DMA destination goes through M0, and a per-lane one
+  // is a readfirstlane loop around every load)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave % NWR, wn = wave / NWR;
   const int KT = a.KT, T = a.pk_tiles, n_rt = a.n_row_tiles;
   const int rb0 = blockIdx.x * BR, tb0 = blockIdx.y * BT;
   if (rb0 >= n_rt || tb0 >= T) return;
@@ -373,12 +392,15 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
   }
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.w), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0, 0x7fffffff, 0x00020000);
-  // stage loads of k tile kt: tile q = wave * TPW + i; q < BR: weights (row tile q), else activations
+  // stage loads of k step `step` (k tile kt): tile q = wave * TPW + i; q < BR: weights (row tile q), else activations
   // (token tile q - BR); rows / tokens past the matrix re-read the last one.  Every stage issues
   // exactly TPW loads per wave (k tiles past the range re-read the last one, never computed), so
   // the counted vmcnt below is exact at the tail too.
-  auto issue = [&](int kt, int buf) {
-    kt = min(kt, kend - 1);
+  // (a k order rotated per block, so that blocks do not read the same activation tiles in
+  // lockstep, measured slower: the 32-utterance prefill 92.6 -> 106.7 ms, profiles/r04_i_*)
+  const int KS = kend - kbeg;
+  auto issue = [&](int step, int buf) {
+    const int kt = kbeg + min(step, KS - 1);
 #pragma unroll
     for (int i = 0; i < TPW; ++i) {
       const int q = wave * TPW + i;
@@ -400,13 +422,15 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[r][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int st = 0; st < G3_NST - 1; ++st) issue(kbeg + st, st);
+  for (int st = 0; st < NST - 1; ++st) issue(st, st);
   int buf = 0;
-  for (int kt = kbeg; kt < kend; ++kt) {
-    // this stage's loads have landed once only the G3_NST - 2 younger stages are in flight
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(TPW * (G3_NST - 2)) : "memory");
-    __syncthreads();  // stage `buf` landed for every wave; the buffer refilled below was last read a step ago
-    issue(kt + G3_NST - 1, (buf + G3_NST - 1) % G3_NST);
+  for (int i = 0; i < KS; ++i) {
+    // this stage's loads have landed once only the NST - 2 younger stages are in flight
+    // stage `buf` landed for every wave; the buffer refilled below was last read a step ago.  A bare
+    // barrier: __syncthreads' release fence waits for every LDS-DMA load in flight (vmcnt(0)), which
+    // would leave one stage of prefetch instead of NST - 1
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(TPW * (NST - 2)) : "memory");
+    issue(i + NST - 1, (buf + NST - 1) % NST);
     const u32x4* A = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE);
     const u32x4* Bx = reinterpret_cast<const u32x4*>(g3_lds + buf * STAGE + BR * 1024);
     u32x4 af[WR], bf[WN];
@@ -420,7 +444,7 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
       for (int j = 0; j < WN; ++j)
         acc[r][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[r]),
                                                            __builtin_bit_cast(bf16x8, bf[j]), acc[r][j], 0, 0, 0);
-    buf = buf + 1 == G3_NST ? 0 : buf + 1;
+    buf = buf + 1 == NST ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the surplus tail loads land before the block exits)
   const int g4 = lane >> 4, c16 = lane & 15;
@@ -490,35 +514,50 @@ __global__ __launch_bounds__(512) void gemm3_kernel(GemvArgs a) {
   }
 }
 
-// gemm3 tile shape by row count: 256-row blocks for the wide matrices, 128 for N 4,096 (o_proj /
-// down), split K until the grid covers the CUs (its partials through gemm_splitk_reduce)
-template <int WR, int WN, int EPI>
-static hipError_t gemm3_launch(GemvArgs a, hipStream_t s) {
-  constexpr int BR = 2 * WR, BT = 4 * WN;
-  const size_t lds = gemm3_lds_bytes<WR, WN>();
+// gemm3 launch of one shape: split K until the grid covers the CUs (partials through
+// gemm_splitk_reduce; row-major outputs only), down to MINK k tiles per split
+template <int NWR, int NWN, int WR, int WN, int NST, int EPI>
+static hipError_t gemm3_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
+  constexpr int BR = NWR * WR, BT = NWN * WN;
+  const size_t lds = gemm3_lds_bytes<NWR, NWN, WR, WN, NST>();
   const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
   static const int force = getenv("MTTS_GEMM3_SPLIT") ? atoi(getenv("MTTS_GEMM3_SPLIT")) : -1;
   int S = 1;
   if (!a.y_packed && a.ws) {
     if (force > 0) S = force;
     else if (force < 0)
-      while (grid.x * grid.y * S < 128 && a.KT / (2 * S) >= 16) S *= 2;  // (a grid of half the CUs and up runs whole)
-    while (S > 1 && (a.KT % (2 * S) || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
+      while ((int)(grid.x * grid.y) * S < cover && a.KT / (2 * S) >= mink) S *= 2;
+    while (S > 1 && (a.KT % S || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
   }
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm3_kernel<WR, WN, EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)gemm3_kernel<WR, WN, EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
+  const dim3 block(NWR * NWN * 64);
   if (S > 1) {
-    hipLaunchKernelGGL((gemm3_kernel<WR, WN, EPI, true>), dim3(grid.x, grid.y, S), dim3(512), lds, s, a);
-    const int n = a.B * ((a.N + 15) / 16);
+    hipLaunchKernelGGL((gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, true>), dim3(grid.x, grid.y, S), block, lds, s, a);
+    const int n = a.B * ((a.N + 15) / 16) * 4;
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
   } else {
-    hipLaunchKernelGGL((gemm3_kernel<WR, WN, EPI, false>), grid, dim3(512), lds, s, a);
+    hipLaunchKernelGGL((gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, false>), grid, block, lds, s, a);
   }
   return hipGetLastError();
+}
+
+// gemm3 shape by prompt rows: <= 192 token rows (12 tiles) one token block of 96-row blocks, split
+// to >= 256 workgroups (q|k|v 4, o_proj / down 8 ways); longer prompts 256-row blocks for the wide
+// matrices, 128 for N 4,096 (o_proj / down), split to >= 128 workgroups
+template <int EPI>
+static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
+  static const int small_max = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 12;
+  if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, 8, EPI>(a, 256, 8, s);
+  static const int wide_min = getenv("MTTS_GEMM3_WIDE") ? atoi(getenv("MTTS_GEMM3_WIDE")) : 1024;  // A/B
+  if (a.n_row_tiles >= wide_min) return gemm3_launch<2, 4, 8, 4, G3_NST, EPI>(a, 128, 16, s);
+  return gemm3_launch<2, 4, 4, 4, G3_NST, EPI>(a, 128, 16, s);
 }
 
 template <int WR, int WN, int EPI>
@@ -531,7 +570,7 @@ static void gemm2_launch(GemvArgs a, hipStream_t s) {
   const int S = (a.y_packed || (a.x_packed && !pk_split)) ? 1 : gemm_splits<WR, WN, 4>(a, (int)grid.x, (int)grid.y);
   if (S > 1) {
     hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4, true>), dim3(grid.x, grid.y, S), dim3(256), 0, s, a);
-    const int n = a.B * ((a.N + 15) / 16);
+    const int n = a.B * ((a.N + 15) / 16) * 4;
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
     return;
   }
@@ -550,17 +589,18 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   // the packed layout is read / written by the 128 x 128 form only
   if ((a0.x_packed || a0.y_packed) && (a0.B < big || a0.K % 64 || a0.pk_tiles * 16 < a0.B)) return hipErrorInvalidValue;
   // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged form (0: off, A/B).  From
-  // 2,048 rows: the 32-utterance prefill (5,792 rows) 127 -> 105 ms, while the TTSD prefill's
-  // 1,024-row chunks ran 82 -> 99 ms on it (4 token blocks x 96 row blocks = 1.5 rounds of the
-  // 256 CUs; gemm2's 128 x 128 tiles make 6), profiles/r04_e_*
-  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 2048;
-  if (g3min > 0 && a.x_packed && a.pk_tiles > 2 && a.B >= g3min && a.K % 64 == 0) {
+  // 512 rows since its k loop keeps NST - 1 stages in flight (a __syncthreads per k step had waited
+  // them all out): 724-row prefill 20.5 -> 18.7 ms, 1,024-row 29.2 -> 28.0 (profiles/r04_i_*); at
+  // 2,048 rows the 32-utterance prefill 127 -> 105 ms (profiles/r04_e_*)
+  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 512;
+  // (and prompts of <= 192 rows: gemm3's one-token-block form, MTTS_GEMM3_SMALL tiles, 0: off)
+  static const int g3small = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 12;
+  if (g3min > 0 && a.x_packed && a.pk_tiles > 2 && (a.B >= g3min || a.pk_tiles <= g3small) && a.K % 64 == 0) {
     a.n_row_tiles = (epi == EPI_SWIGLU ? 2 : 1) * n_tiles;
-    const bool wide = a.n_row_tiles >= 1024;  // 256-row blocks for q|k|v / gate|up, 128 for N 4,096
     switch (epi) {
-      case EPI_STORE: return wide ? gemm3_launch<8, 4, EPI_STORE>(a, s) : gemm3_launch<4, 4, EPI_STORE>(a, s);
-      case EPI_RESADD: return wide ? gemm3_launch<8, 4, EPI_RESADD>(a, s) : gemm3_launch<4, 4, EPI_RESADD>(a, s);
-      case EPI_SWIGLU: return wide ? gemm3_launch<8, 4, EPI_SWIGLU>(a, s) : gemm3_launch<4, 4, EPI_SWIGLU>(a, s);
+      case EPI_STORE: return gemm3_pick<EPI_STORE>(a, s);
+      case EPI_RESADD: return gemm3_pick<EPI_RESADD>(a, s);
+      case EPI_SWIGLU: return gemm3_pick<EPI_SWIGLU>(a, s);
       default: return hipErrorInvalidValue;
     }
   }

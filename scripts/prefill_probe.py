@@ -15,7 +15,9 @@ from moss_tts_amd.engine import Engine, EngineConfig, sampling_params  # noqa: E
 shapes = [(1, 181), (1, 512), (4, 181), (32, 181), (1, 2048)]
 if os.environ.get("PREFILL_SHAPES"):  # e.g. "1x181,4x181"
     shapes = [tuple(int(v) for v in t.split("x")) for t in os.environ["PREFILL_SHAPES"].split(",")]
-e = Engine(EngineConfig(max_batch=32, max_ctx=2304, max_prefill_tokens=8192), 0)
+# PREFILL_MAXCTX / PREFILL_CHUNK: the TTSD long form (e.g. 9,700 / 1,024: position-chunked prefill)
+e = Engine(EngineConfig(max_batch=32, max_ctx=int(os.environ.get("PREFILL_MAXCTX", 2304)),
+                        max_prefill_tokens=int(os.environ.get("PREFILL_CHUNK", 8192))), 0)
 e.init_random(0)
 sp = sampling_params(text_temperature=0, audio_temperature=0)
 rng = np.random.default_rng(0)

@@ -189,6 +189,70 @@ def test_gemm_prefill(N, M, Nr, K, epi):
         assert np.allclose(ss.cpu().numpy(), want_ss, rtol=1e-5, atol=1e-6)
 
 
+def xpk_indices(M, K):
+    """u16 index of (token m, column k) in the packed prefill activations (kernels.h xpkT_index)."""
+    T = (M + 15) // 16
+    m = np.arange(M)[:, None]
+    k = np.arange(K)[None, :]
+    return (((((k >> 5) * T + (m >> 4)) * 64 + (m & 15) + 16 * ((k & 31) >> 3)) << 3) + (k & 7)), T
+
+
+@pytest.mark.parametrize("M,Nr,K,epi", [(181, 6144, 4096, 0), (181, 4096, 4096, 1), (181, 12288, 4096, 2),
+                                        (181, 4096, 12288, 1), (130, 1000, 512, 1), (192, 96, 1024, 2),
+                                        (2048, 4096, 4096, 1), (2048, 1536, 2048, 2)])
+def test_gemm_packed_prefill(N, M, Nr, K, epi):
+    """Prefill GEMM on fragment-packed activations (the engine's >= 128-row prompts) at the 8B
+    projections' shapes: 181 rows take gemm3's one-token-block form (split K for q|k|v, o_proj,
+    down), 2,048 the 256 / 128-row blocks; the gate|up output packed for the down projection.
+    Oracle linear + epilogues within 2 bf16 ulp (rows' scale / 4 floor), the residual epilogue's
+    sums of squares to 1e-5."""
+    rng = np.random.default_rng(M + Nr + K + epi)
+    ctx = O._Ctx("bf16")
+    x = rand_bf16(rng, (M, K))
+    rows = 2 * Nr if epi == 2 else Nr
+    W = rand_bf16(rng, (rows, K), K ** -0.5)
+    packed = torch.zeros(N.load().mtts_k_packed_bytes(rows, K) // 2, dtype=torch.bfloat16, device="cuda")
+    keep = [dev_bf16(W[:Nr]), dev_bf16(W[Nr:]) if epi == 2 else None]
+    if epi == 2:
+        N.call("mtts_k_pack", P(keep[0]), P(packed), Nr, K, 0, 1, 0, None)
+        N.call("mtts_k_pack", P(keep[1]), P(packed), Nr, K, 0, 1, 1, None)
+    else:
+        N.call("mtts_k_pack", P(keep[0]), P(packed), Nr, K, 0, 0, 0, None)
+    idx, T = xpk_indices(M, K)
+    xp = np.zeros(T * 16 * K, np.uint16)
+    xp[idx] = np.asarray(x, np.float32).view(np.uint32) >> 16
+    xd = torch.from_numpy(xp.view(np.int16)).cuda().view(torch.bfloat16)
+    res = rand_bf16(rng, (M, Nr))
+    ypk = epi == 2
+    y = dev_bf16(res) if epi == 1 else torch.zeros(M, Nr, dtype=torch.bfloat16, device="cuda")
+    yp = torch.zeros(T * 16 * Nr, dtype=torch.bfloat16, device="cuda") if ypk else None
+    nt = (Nr + 15) // 16
+    ss = torch.zeros(M, nt, dtype=torch.float32, device="cuda")
+    ws = torch.zeros(8 << 20, dtype=torch.float32, device="cuda")
+    N.call("mtts_k_gemm_packed", P(packed), P(xd), P(yp if ypk else y), Nr, 1 if ypk else 0,
+           P(y) if epi == 1 else None, Nr, M, Nr, K, epi, P(ss) if epi == 1 else None, nt, P(ws), ws.numel(), None)
+    torch.cuda.synchronize()
+    lin = O.linear(ctx, x, W[:Nr])
+    if epi == 0:
+        want = lin
+    elif epi == 1:
+        want = ctx.r(res + lin)
+    else:
+        want = ctx.r(ctx.r(O.silu(lin)) * O.linear(ctx, x, W[Nr:]))
+    if ypk:
+        oidx, _ = xpk_indices(M, Nr)
+        flat = yp.view(torch.int16).cpu().numpy().view(np.uint16)
+        got = (flat[oidx].astype(np.uint32) << 16).view(np.float32)
+    else:
+        got = host(y)
+    rowscale = np.abs(want).max(axis=1, keepdims=True)
+    assert within_band(got, want, 2.0, scale=np.maximum(np.abs(want), rowscale / 4)).all(), np.abs(got - want).max()
+    if epi == 1:
+        g2 = np.pad(got, ((0, 0), (0, nt * 16 - Nr))).reshape(M, nt, 16)
+        want_ss = (g2.astype(np.float64) ** 2).sum(-1)
+        assert np.allclose(ss.cpu().numpy(), want_ss, rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("B,Nr,K,splits", [(8, 1536, 8960, 0), (1, 1536, 8960, 3), (16, 1000, 4096, 2),
                                            (3, 64, 2048, 7)])
 def test_gemv_splitk(N, B, Nr, K, splits):
