@@ -361,9 +361,85 @@ static int gemm_splits(const GemvArgs& a, int nx, int ny) {
 #ifndef G3_NST
 #define G3_NST 3
 #endif
+#ifndef G3S_NST
+#define G3S_NST 5  // the <= 192-row form's stages
+#endif
+
 
 template <int NWR, int NWN, int WR, int WN, int NST>
 constexpr size_t gemm3_lds_bytes() { return (size_t)NST * (NWR * WR + NWN * WN) * 1024; }
+// gemm3 epilogue of one wave's WR x WN tiles (gemm2_kernel's): lane -> token (tt0 + j) * 16 + c16,
+// output columns n0 .. n0 + 3; SPLIT: the fp32 partial tile of K range blockIdx.z
+template <int WR, int WN, int EPI, bool SPLIT>
+__device__ __forceinline__ void gemm_tile_epilogue(const GemvArgs& a, const f32x4 (&acc)[WR][WN], int rt0, int tt0,
+                                                   int lane) {
+  const int n_rt = a.n_row_tiles;
+  const int g4 = lane >> 4, c16 = lane & 15;
+  if constexpr (SPLIT) {
+    const size_t ld = (size_t)n_rt * 16;
+    float* wsz = a.ws + (size_t)blockIdx.z * a.B * ld;
+#pragma unroll
+    for (int r = 0; r < WR; ++r) {
+      if (rt0 + r >= n_rt) continue;
+#pragma unroll
+      for (int j = 0; j < WN; ++j) {
+        const int m = (tt0 + j) * 16 + c16;
+        if (m < a.B) *reinterpret_cast<f32x4*>(wsz + (size_t)m * ld + (rt0 + r) * 16 + g4 * 4) = acc[r][j];
+      }
+    }
+    return;
+  }
+  // epilogue (gemm2_kernel's): lane -> token (tt0 + j) * 16 + c16, output columns n0 .. n0 + 3
+  constexpr int OT = EPI == EPI_SWIGLU ? WR / 2 : WR;
+#pragma unroll
+  for (int q = 0; q < OT; ++q) {
+    const int ot = EPI == EPI_SWIGLU ? rt0 / 2 + q : rt0 + q;
+    const int n0 = ot * 16 + g4 * 4;
+#pragma unroll
+    for (int j = 0; j < WN; ++j) {
+      const int m = (tt0 + j) * 16 + c16;
+      const bool mok = m < a.B && n0 < a.N;
+      float o[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int n = n0 + i;
+        if constexpr (EPI == EPI_STORE) {
+          o[i] = rbf(acc[q][j][i]);
+        } else if constexpr (EPI == EPI_RESADD) {
+          o[i] = (mok && n < a.N) ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(acc[q][j][i])) : 0.f;
+        } else {
+          const float g = rbf(acc[2 * q][j][i]);
+          const float u = rbf(acc[2 * q + 1][j][i]);
+          o[i] = rbf(rbf(g / (1.0f + expf(-g))) * u);
+        }
+      }
+      if (mok && a.y_packed) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (n0 + i < a.N) a.y[xpkT_index(m, n0 + i, a.pk_tiles)] = f2bf(o[i]);
+      } else if (mok) {
+        bf16_t* yr = a.y + (size_t)m * a.ldy;
+        if (n0 + 3 < a.N && (a.ldy % 4) == 0) {
+          uint2 pk;
+          pk.x = pack2(o[0], o[1]);
+          pk.y = pack2(o[2], o[3]);
+          *reinterpret_cast<uint2*>(yr + n0) = pk;
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (n0 + i < a.N) yr[n0 + i] = f2bf(o[i]);
+        }
+      }
+      if constexpr (EPI == EPI_RESADD) {
+        float ss = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
+        ss += __shfl_xor(ss, 16, 64);
+        ss += __shfl_xor(ss, 32, 64);
+        if (a.ss_out && mok && g4 == 0) a.ss_out[(size_t)m * a.ld_ss_out + ot] = ss;
+      }
+    }
+  }
+}
+
 template <int NWR, int NWN, int WR, int WN, int NST, int EPI, bool SPLIT = false>
 __global__ __launch_bounds__(NWR * NWN * 64) void gemm3_kernel(GemvArgs a) {
   typedef __attribute__((address_space(3))) void lvoid;
@@ -447,71 +523,7 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm3_kernel(GemvArgs a) {
     buf = buf + 1 == NST ? 0 : buf + 1;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the surplus tail loads land before the block exits)
-  const int g4 = lane >> 4, c16 = lane & 15;
-  const int rt0 = rb0 + wr * WR, tt0 = tb0 + wn * WN;
-  if constexpr (SPLIT) {
-    const size_t ld = (size_t)n_rt * 16;
-    float* wsz = a.ws + (size_t)blockIdx.z * a.B * ld;
-#pragma unroll
-    for (int r = 0; r < WR; ++r) {
-      if (rt0 + r >= n_rt) continue;
-#pragma unroll
-      for (int j = 0; j < WN; ++j) {
-        const int m = (tt0 + j) * 16 + c16;
-        if (m < a.B) *reinterpret_cast<f32x4*>(wsz + (size_t)m * ld + (rt0 + r) * 16 + g4 * 4) = acc[r][j];
-      }
-    }
-    return;
-  }
-  // epilogue (gemm2_kernel's): lane -> token (tt0 + j) * 16 + c16, output columns n0 .. n0 + 3
-  constexpr int OT = EPI == EPI_SWIGLU ? WR / 2 : WR;
-#pragma unroll
-  for (int q = 0; q < OT; ++q) {
-    const int ot = EPI == EPI_SWIGLU ? rt0 / 2 + q : rt0 + q;
-    const int n0 = ot * 16 + g4 * 4;
-#pragma unroll
-    for (int j = 0; j < WN; ++j) {
-      const int m = (tt0 + j) * 16 + c16;
-      const bool mok = m < a.B && n0 < a.N;
-      float o[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int n = n0 + i;
-        if constexpr (EPI == EPI_STORE) {
-          o[i] = rbf(acc[q][j][i]);
-        } else if constexpr (EPI == EPI_RESADD) {
-          o[i] = (mok && n < a.N) ? rbf(bf2f(a.res[(size_t)m * a.ldres + n]) + rbf(acc[q][j][i])) : 0.f;
-        } else {
-          const float g = rbf(acc[2 * q][j][i]);
-          const float u = rbf(acc[2 * q + 1][j][i]);
-          o[i] = rbf(rbf(g / (1.0f + expf(-g))) * u);
-        }
-      }
-      if (mok && a.y_packed) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          if (n0 + i < a.N) a.y[xpkT_index(m, n0 + i, a.pk_tiles)] = f2bf(o[i]);
-      } else if (mok) {
-        bf16_t* yr = a.y + (size_t)m * a.ldy;
-        if (n0 + 3 < a.N && (a.ldy % 4) == 0) {
-          uint2 pk;
-          pk.x = pack2(o[0], o[1]);
-          pk.y = pack2(o[2], o[3]);
-          *reinterpret_cast<uint2*>(yr + n0) = pk;
-        } else {
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-            if (n0 + i < a.N) yr[n0 + i] = f2bf(o[i]);
-        }
-      }
-      if constexpr (EPI == EPI_RESADD) {
-        float ss = (o[0] * o[0] + o[1] * o[1]) + (o[2] * o[2] + o[3] * o[3]);
-        ss += __shfl_xor(ss, 16, 64);
-        ss += __shfl_xor(ss, 32, 64);
-        if (a.ss_out && mok && g4 == 0) a.ss_out[(size_t)m * a.ld_ss_out + ot] = ss;
-      }
-    }
-  }
+  gemm_tile_epilogue<WR, WN, EPI, SPLIT>(a, acc, rb0 + wr * WR, tb0 + wn * WN, lane);
 }
 
 // gemm3 launch of one shape: split K until the grid covers the CUs (partials through
@@ -520,6 +532,8 @@ template <int NWR, int NWN, int WR, int WN, int NST, int EPI>
 static hipError_t gemm3_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
   constexpr int BR = NWR * WR, BT = NWN * WN;
   const size_t lds = gemm3_lds_bytes<NWR, NWN, WR, WN, NST>();
+  const void* k_full = (const void*)gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, false>;
+  const void* k_split = (const void*)gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, true>;
   const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
   static const int force = getenv("MTTS_GEMM3_SPLIT") ? atoi(getenv("MTTS_GEMM3_SPLIT")) : -1;
   int S = 1;
@@ -531,19 +545,20 @@ static hipError_t gemm3_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
   }
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, false>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, true>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(k_full, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute(k_split, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   const dim3 block(NWR * NWN * 64);
+  void* args[] = {&a};
   if (S > 1) {
-    hipLaunchKernelGGL((gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, true>), dim3(grid.x, grid.y, S), block, lds, s, a);
+    hipError_t e = hipLaunchKernel(k_split, dim3(grid.x, grid.y, S), block, args, lds, s);
+    if (e != hipSuccess) return e;
     const int n = a.B * ((a.N + 15) / 16) * 4;
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
   } else {
-    hipLaunchKernelGGL((gemm3_kernel<NWR, NWN, WR, WN, NST, EPI, false>), grid, block, lds, s, a);
+    hipError_t e = hipLaunchKernel(k_full, grid, block, args, lds, s);
+    if (e != hipSuccess) return e;
   }
   return hipGetLastError();
 }
@@ -554,8 +569,11 @@ static hipError_t gemm3_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
 template <int EPI>
 static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   static const int small_max = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 12;
-  if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, 8, EPI>(a, 256, 8, s);
+  static const int small_mink = getenv("MTTS_GEMM3_SMALL_MINK") ? atoi(getenv("MTTS_GEMM3_SMALL_MINK")) : 8;  // A/B
   static const int wide_min = getenv("MTTS_GEMM3_WIDE") ? atoi(getenv("MTTS_GEMM3_WIDE")) : 1024;  // A/B
+  // (a register-staged variant -- global -> VGPRs -> ds_write_b128, two LDS stages -- measured
+  // slower: 181 rows 7.97 -> 8.20 ms, 32 utterances 91.9 -> 95.7 ms, profiles/r04_j_*)
+  if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, G3S_NST, EPI>(a, 256, small_mink, s);
   if (a.n_row_tiles >= wide_min) return gemm3_launch<2, 4, 8, 4, G3_NST, EPI>(a, 128, 16, s);
   return gemm3_launch<2, 4, 4, 4, G3_NST, EPI>(a, 128, 16, s);
 }
