@@ -533,19 +533,27 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm3_kernel(GemvArgs a) {
 // ahead, a register ring indexed at compile time), read by the one wave that uses them.  gemm3's
 // form moved 18 KiB per CU per k step through LDS-DMA, ~18 B/clk/CU whatever the source
 // (profiles/r04_m_gemm3_probe.txt); here LDS-DMA carries 6 KiB and the vector path 12 KiB.
-template <int R>
-constexpr size_t gemm5_lds_bytes() { return (size_t)(R + 1) * 6 * 1024; }
-template <int R, int EPI, bool SPLIT = false>
-__global__ __launch_bounds__(384) void gemm5_kernel(GemvArgs a) {
+// Shape <NWR, NWN, WR, WN>: NWR x NWN waves, each WR weight row tiles x WN token tiles; the block's
+// BR = NWR WR weight tiles per k step are split over the waves' LDS-DMA loads, each wave loads its own
+// WN activation fragments.  <1, 6, 6, 2> for <= 192 rows.
+template <int NWR, int NWN, int WR, int R>
+constexpr size_t gemm5_lds_bytes() { return (size_t)(R + 1) * NWR * WR * 1024; }
+template <int NWR, int NWN, int WR, int WN, int R, int EPI, bool SPLIT = false>
+__global__ __launch_bounds__(NWR * NWN * 64) void gemm5_kernel(GemvArgs a) {
   typedef __attribute__((address_space(3))) void lvoid;
-  constexpr int NST = R + 1, BR = 6, WN = 2;
+  constexpr int NW = NWR * NWN, NST = R + 1, BR = NWR * WR, BT = NWN * WN;
+  constexpr int TPW = BR / NW;  // weight tiles per wave per k step
+  static_assert(BR % NW == 0, "weight tiles split over the waves");
+  static_assert((TPW + WN) * R <= 63, "vmcnt counts the k steps in flight");
+  static_assert(EPI != EPI_SWIGLU || WR % 2 == 0, "gate|up row tile pairs stay within a wave");
   constexpr int STAGE = BR * 1024;
   extern __shared__ __attribute__((aligned(16))) unsigned char g5_lds[];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave % NWR, wn = wave / NWR;
   const int KT = a.KT, T = a.pk_tiles, n_rt = a.n_row_tiles;
-  const int rb0 = blockIdx.x * BR;
-  if (rb0 >= n_rt) return;
+  const int rb0 = blockIdx.x * BR, tb0 = blockIdx.y * BT;
+  if (rb0 >= n_rt || tb0 >= T) return;
   int kbeg = 0, kend = KT;
   if constexpr (SPLIT) {
     const int KSp = KT / gridDim.z;
@@ -555,16 +563,20 @@ __global__ __launch_bounds__(384) void gemm5_kernel(GemvArgs a) {
   const int KS = kend - kbeg;
   const __amdgpu_buffer_rsrc_t wrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.w), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.x), 0, 0x7fffffff, 0x00020000);
-  const int rt = min(rb0 + wave, n_rt - 1);  // this wave's weight tile of every stage
   int tt[WN];
 #pragma unroll
-  for (int j = 0; j < WN; ++j) tt[j] = min(wave * WN + j, T - 1);
+  for (int j = 0; j < WN; ++j) tt[j] = min(tb0 + wn * WN + j, T - 1);
   // k steps past the range re-read the last k tile (never computed): every step issues the same
   // loads, so each wait below is exact
   auto issue_w = [&](int step) {
     const int kt = kbeg + min(step, KS - 1);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lvoid*)(g5_lds + (step % NST) * STAGE + wave * 1024), 16,
-                                             (uint32_t)(((size_t)rt * KT + kt) * 1024 + lane * 16), 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int q = wave * TPW + t;
+      const int rt = min(rb0 + q, n_rt - 1);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrs, (lvoid*)(g5_lds + (step % NST) * STAGE + q * 1024), 16,
+                                               (uint32_t)(((size_t)rt * KT + kt) * 1024 + lane * 16), 0, 0, 0);
+    }
   };
   auto issue_x = [&](u32x4 (&dst)[WN], int step) {
     const int kt = kbeg + min(step, KS - 1);
@@ -572,9 +584,9 @@ __global__ __launch_bounds__(384) void gemm5_kernel(GemvArgs a) {
     for (int j = 0; j < WN; ++j)
       dst[j] = __builtin_amdgcn_raw_buffer_load_b128(xrs, (uint32_t)(((size_t)kt * T + tt[j]) * 1024 + lane * 16), 0, 0);
   };
-  f32x4 acc[BR][WN];
+  f32x4 acc[WR][WN];
 #pragma unroll
-  for (int r = 0; r < BR; ++r)
+  for (int r = 0; r < WR; ++r)
 #pragma unroll
     for (int j = 0; j < WN; ++j) acc[r][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   u32x4 xr[R][WN];
@@ -589,15 +601,15 @@ __global__ __launch_bounds__(384) void gemm5_kernel(GemvArgs a) {
       const int i = i0 + r;
       // step i's weight tiles (every wave's LDS-DMA) and this wave's activations have landed once
       // only the R - 1 younger steps' loads (1 + WN per step) are in flight
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((1 + WN) * (R - 1)) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((TPW + WN) * (R - 1)) : "memory");
       issue_w(i + R);  // into stage (i + R) % NST = (i - 1) % NST, read at step i - 1
       if (i < KS) {
         const u32x4* A = reinterpret_cast<const u32x4*>(g5_lds + (i % NST) * STAGE);
-        u32x4 af[BR];
+        u32x4 af[WR];
 #pragma unroll
-        for (int rr = 0; rr < BR; ++rr) af[rr] = A[rr * 64 + lane];
+        for (int rr = 0; rr < WR; ++rr) af[rr] = A[(wr * WR + rr) * 64 + lane];
 #pragma unroll
-        for (int rr = 0; rr < BR; ++rr)
+        for (int rr = 0; rr < WR; ++rr)
 #pragma unroll
           for (int j = 0; j < WN; ++j)
             acc[rr][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[rr]),
@@ -607,30 +619,34 @@ __global__ __launch_bounds__(384) void gemm5_kernel(GemvArgs a) {
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  gemm_tile_epilogue<BR, WN, EPI, SPLIT>(a, acc, rb0, wave * WN, lane);
+  gemm_tile_epilogue<WR, WN, EPI, SPLIT>(a, acc, rb0 + wr * WR, tb0 + wn * WN, lane);
 }
 
-template <int R, int EPI>
+template <int NWR, int NWN, int WR, int WN, int R, int EPI>
 static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
-  const size_t lds = gemm5_lds_bytes<R>();
-  const dim3 grid((a.n_row_tiles + 5) / 6);
+  constexpr int BR = NWR * WR, BT = NWN * WN;
+  const size_t lds = gemm5_lds_bytes<NWR, NWN, WR, R>();
+  const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
   int S = 1;
   if (!a.y_packed && a.ws) {
-    while ((int)grid.x * S < cover && a.KT / (2 * S) >= mink) S *= 2;
+    while ((int)(grid.x * grid.y) * S < cover && a.KT / (2 * S) >= mink) S *= 2;
     while (S > 1 && (a.KT % S || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
   }
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)gemm5_kernel<R, EPI, false>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    (void)hipFuncSetAttribute((const void*)gemm5_kernel<R, EPI, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm5_kernel<NWR, NWN, WR, WN, R, EPI, false>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    (void)hipFuncSetAttribute((const void*)gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr = true;
   }
   if (S > 1) {
-    hipLaunchKernelGGL((gemm5_kernel<R, EPI, true>), dim3(grid.x, 1, S), dim3(384), lds, s, a);
+    hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>), dim3(grid.x, grid.y, S), dim3(NWR * NWN * 64),
+                       lds, s, a);
     const int n = a.B * ((a.N + 15) / 16) * 4;
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
   } else {
-    hipLaunchKernelGGL((gemm5_kernel<R, EPI, false>), grid, dim3(384), lds, s, a);
+    hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, false>), grid, dim3(NWR * NWN * 64), lds, s, a);
   }
   return hipGetLastError();
 }
@@ -684,8 +700,16 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // slower: 181 rows 7.97 -> 8.20 ms, 32 utterances 91.9 -> 95.7 ms, profiles/r04_j_*)
   // MTTS_GEMM5 (A/B): the split-path form for <= 12 token tiles
   static const int g5 = getenv("MTTS_GEMM5") ? atoi(getenv("MTTS_GEMM5")) : 1;
-  if (a.pk_tiles <= small_max && g5) return gemm5_launch<4, EPI>(a, 256, small_mink, s);
+  if (a.pk_tiles <= small_max && g5) return gemm5_launch<1, 6, 6, 2, 4, EPI>(a, 256, small_mink, s);
   if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, G3S_NST, EPI>(a, 256, small_mink, s);
+  // MTTS_GEMM5_LONG (A/B, 0: gemm3): the long-prompt shapes with split paths as well -- batch-4 prefill
+  // 18.6 -> 17.5 ms, 1,024 rows 27.7 -> 26.6, TTSD long form 75.2 -> 71.6, 32 utterances unchanged
+  // (profiles/r04_p_gemm5_long_ab.txt)
+  static const int g5l = getenv("MTTS_GEMM5_LONG") ? atoi(getenv("MTTS_GEMM5_LONG")) : 1;
+  if (g5l) {
+    if (a.n_row_tiles >= wide_min) return gemm5_launch<2, 4, 8, 4, 2, EPI>(a, 128, 16, s);
+    return gemm5_launch<2, 4, 4, 4, 2, EPI>(a, 128, 16, s);
+  }
   if (a.n_row_tiles >= wide_min) return gemm3_launch<2, 4, 8, 4, G3_NST, EPI>(a, 128, 16, s);
   return gemm3_launch<2, 4, 4, 4, G3_NST, EPI>(a, 128, 16, s);
 }
