@@ -348,18 +348,28 @@ def main_local(args, world, rank, local):
     B = args.batch if args.batch > 1 else 8
     frames = args.decode_steps if args.decode_steps != 208 else 173
     rng = np.random.default_rng(1 + rank)
-    prompts = [local_prompt(rng) for _ in range(B)]
-    ids = np.stack(prompts)  # equal lengths
-    T = ids.shape[1]
+    # ragged, as configs[3]'s 8 different 200-char prompts are: 36-60 text tokens per row, left-padded
+    # the processor's way (`_pad`, moss_tts_local/processing_moss_tts.py:415-436; the backbone's
+    # positions then exclude each row's pads, as GenerationMixin's do)
+    prompts = [local_prompt(rng, text_tokens=int(n)) for n in rng.integers(36, 61, B)]
+    T = max(p.shape[0] for p in prompts)
+    ids = np.full((B, T, 33), 1024, np.int64)
+    ids[..., 0] = 151643
+    mask = np.zeros((B, T), bool)
+    for b, p in enumerate(prompts):
+        ids[b, T - p.shape[0]:] = p
+        mask[b, T - p.shape[0]:] = True
     ecfg = EngineConfig(hidden=2048, layers=args.layers if args.layers != 36 else 28, n_heads=16, n_kv=8, head_dim=128,
                         inter=6144, n_vq=32, max_batch=B, max_ctx=T + frames + 16, max_prefill_tokens=max(256 * B, 256),
                         model_kind=1, local_hidden=1536, local_layers=4, local_inter=8960, local_mlp_ffn=2048)
     eng = Engine(ecfg, local)
     eng.init_random(seed=0)
     ids_d = torch.from_numpy(ids).cuda()
+    mask_d = torch.from_numpy(mask).cuda()
+    mask_u8 = mask_d.to(torch.uint8).contiguous()
 
     def one():
-        return eng.local_generate_ids(ids_d, None, frames, -1, chunk=32)
+        return eng.local_generate_ids(ids_d, mask_d, frames, -1, chunk=32)
 
     for _ in range(args.warmup):
         out = one()
@@ -396,8 +406,9 @@ def main_local(args, world, rank, local):
     for k in range(8):
         torch.cuda.synchronize()
         a = time.perf_counter()
-        Nn.check(Nn.load().mtts_local_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()), None, B, T, frames, -1,
-                                                     sp, None), "begin")
+        Nn.check(Nn.load().mtts_local_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()),
+                                                     ctypes.c_void_p(mask_u8.data_ptr()), B, T, frames, -1, sp, None),
+                 "begin")
         if k >= 3:
             Nn.check(Nn.load().mtts_local_generate_decode(eng._h, 12, None), "decode")
         Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
@@ -430,7 +441,8 @@ def main_local(args, world, rank, local):
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
             "data": "synthetic (random-init bf16 weights at the MossTTSLocal-1.7B shape; synthetic clone prompts)",
             "config": {"workload": f"MossTTSLocal bf16 batch={B} on 1xMI355X (depth transformer, 1+32 channels/frame)",
-                       "n_vq": 32, "batch_per_gpu": B, "prompt_tokens": int(T), "frames": frames,
+                       "n_vq": 32, "batch_per_gpu": B, "prompt_tokens": int(T),
+                       "prompt_rows_unpadded": [int(m) for m in mask.sum(1)], "frames": frames,
                        "parallelism": f"dp{world}", "sampling": "greedy"},
             "audio_s_per_s_per_gpu": round(audio_total / dt_max / world, 4),
             "audio_frames_per_utt": made[0],

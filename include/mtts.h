@@ -137,12 +137,17 @@ int mtts_local_lpse_active(const mtts_engine* eng);
  * the launch is turned off for this engine and the work re-runs on the per-op launches.
  * (MossTTSLocal engines: the persistent channel launch's word.) */
 int mtts_pse_inject_timeout(mtts_engine* eng);
-/* A batch-1 mtts_forward through the persistent launch does not synchronise: its error word is
- * copied asynchronously and checked lazily -- without blocking at the next mtts_forward /
- * mtts_generate_begin, blocking here.  MTTS_E_PSE_TIMEOUT (reported once): a launch timed out, the
- * logits of the forwards since the last clean check are invalid, and the engine now runs the
- * per-op launches (recompute those forwards).  Also reads the word of forwards the caller
- * captured into its own graph.  0: every forward so far is valid. */
+/* A one-token mtts_forward through a persistent launch checks the launch's error word before it
+ * returns (default): a timed-out launch is recomputed on the per-op launches inside the same call,
+ * so the logits it returns are valid (the engine then stays on the per-op launches).
+ * mtts_engine_set_pse_lazy(eng, 1) opts into the non-synchronising form: the word is copied
+ * asynchronously and checked lazily -- without blocking at the next mtts_forward, blocking here
+ * and at mtts_generate_begin.  MTTS_E_PSE_TIMEOUT (reported once, by this call or the next
+ * mtts_forward, also when a generation start found it first): a launch timed out, the logits of
+ * the lazy forwards since the last clean check are invalid, and the engine now runs the per-op
+ * launches (recompute those forwards).  Also reads the word of forwards the caller captured into
+ * its own graph.  0: every forward so far is valid. */
+int mtts_engine_set_pse_lazy(mtts_engine* eng, int lazy);
 int mtts_pse_check(mtts_engine* eng);
 /* per-layer event stamps (s_memrealtime, 100 MHz) of the last persistent streaming launch:
  * [layers][20][256 workgroups] (engine created with MTTS_PSE_TRACE=1; see pse.hip) */

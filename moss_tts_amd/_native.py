@@ -82,6 +82,7 @@ _SIGS = {
     "mtts_pse_ctx_max": (I, [P]),
     "mtts_pse_inject_timeout": (I, [P]),
     "mtts_pse_check": (I, [P]),
+    "mtts_engine_set_pse_lazy": (I, [P, I]),
     "mtts_engine_load_weight_stream": (I, [P, ctypes.c_char_p, P, SZ, I, P]),
     "mtts_engine_kv_write": (I, [P, I, I, I, I, P, P]),
     "mtts_engine_kv_fill": (I, [P, ctypes.c_uint16]),

@@ -104,10 +104,11 @@ __device__ __forceinline__ void attn_decode_body(const DecAttnArgs& a, const int
     const __amdgpu_buffer_rsrc_t kws =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(a.kn_w), 0, D * 2, 0x00020000);
     const bool rope = a.cos_t != nullptr;
+    const int rpos = a.rope_off ? max(0, pos - a.rope_off[b]) : pos;  // RoPE position (cache slot: pos)
     const __amdgpu_buffer_rsrc_t crs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(rope ? a.cos_t + (size_t)pos * D : row), 0, D * 2, 0x00020000);
+        const_cast<bf16_t*>(rope ? a.cos_t + (size_t)rpos * D : row), 0, D * 2, 0x00020000);
     const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<bf16_t*>(rope ? a.sin_t + (size_t)pos * D : row), 0, D * 2, 0x00020000);
+        const_cast<bf16_t*>(rope ? a.sin_t + (size_t)rpos * D : row), 0, D * 2, 0x00020000);
 #pragma unroll
     for (int jj = 0; jj < JOBS; ++jj) {
       const int j = wave + jj * NWV;

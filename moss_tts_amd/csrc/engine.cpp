@@ -96,6 +96,8 @@ static int alloc_capacity(mtts_engine* e) {
   if ((rc = e->alloc(&e->part, e->part_floats))) return rc;
   if ((rc = e->alloc(&e->logits, (size_t)c.max_batch * e->heads_ld))) return rc;
   if ((rc = e->alloc(&e->d_pos, 4))) return rc;
+  if ((rc = e->alloc(&e->rope_off, (size_t)c.max_batch))) return rc;
+  if (hipMemset(e->rope_off, 0, (size_t)c.max_batch * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if ((rc = e->alloc(&e->att_cnt, (size_t)c.max_batch * Hkv))) return rc;
   if (hipMemset(e->att_cnt, 0, (size_t)c.max_batch * Hkv * sizeof(int)) != hipSuccess) return fail(MTTS_E_HIP, "memset");
   if ((rc = e->alloc(&e->sk_part, SK_PART_FLOATS)) || (rc = e->alloc(&e->sk_cnt, (size_t)SK_TILES))) return rc;
@@ -474,6 +476,10 @@ Stack backbone_stack(mtts_engine* e) {
   st.h = e->h; st.xn = e->xn; st.qkvb = e->qkvb; st.qb = e->qb; st.attnb = e->attnb; st.act = e->act;
   st.rows = e->Mmax;
   st.ss = e->ss; st.part = e->part; st.att_cnt = e->att_cnt;
+  // MossTTSLocal: its `generate` is GenerationMixin's, whose position ids exclude a row's left pads
+  // (cumsum(mask) - 1, transformers/generation/utils.py:751-773); MossTTSDelay's own loop
+  // includes them (positions = cache slots, TF/.../modeling_qwen3.py:386-389)
+  st.rope_off = e->lp ? e->rope_off : nullptr;
   return st;
 }
 
@@ -580,6 +586,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     DecAttnArgs da{};
     da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
     da.kc = kc; da.vc = vc; da.mask = st.mask + (size_t)b0 * st.Cmax; da.pos = pos_base; da.out = st.attnb;
+    da.rope_off = st.rope_off ? st.rope_off + b0 : nullptr;
     da.part = st.part; da.cnt = st.att_cnt;
     // small batches: blocks only publish partials; the o_proj GEMV merges them in its prologue
     da.publish_only = fuse_attn ? 1 : 0;
@@ -596,6 +603,7 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       qa.qkv = st.qkvb; qa.q_out = st.qb; qa.kc = kc; qa.vc = vc;
       qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = st.cos_t; qa.sin_t = st.sin_t;
       qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = st.Cmax; qa.eps = eps; qa.M = M;
+      qa.rope_off = st.rope_off ? st.rope_off + b0 : nullptr;
       HIPCHK(qk_norm_rope(qa, s));
       AttnArgs aa;
       aa.q = st.qb; aa.kc = kc; aa.vc = vc; aa.mask = st.mask + (size_t)b0 * st.Cmax; aa.pos_base = pos_base;
@@ -777,10 +785,25 @@ static int pse_lazy_check(mtts_engine* e, bool block) {
                                   "the last check are invalid (recompute them: the engine now runs the per-op launches)");
 }
 
+static int pse_report_owed(mtts_engine* e) {
+  if (!e->pse_unreported) return 0;
+  e->pse_unreported = false;
+  return fail(MTTS_E_PSE_TIMEOUT, "persistent streaming decode: a wait timed out in a teacher-forced forward before "
+                                  "the last generation; those forwards' logits are invalid (the engine now runs the "
+                                  "per-op launches)");
+}
+
+extern "C" int mtts_engine_set_pse_lazy(mtts_engine* e, int lazy) {
+  if (!e) return fail(MTTS_E_INVALID, "null engine");
+  e->pse_lazy = lazy != 0;
+  return 0;
+}
+
 extern "C" int mtts_pse_check(mtts_engine* e) {
   if (!e) return fail(MTTS_E_INVALID, "null engine");
   hipSetDevice(e->device);
   if (int rc = pse_lazy_check(e, true)) return rc;
+  if (int rc = pse_report_owed(e)) return rc;
   // forwards the caller captured into its own graph: read the word itself
   if (e->pse_ws && pse_tripped(e, e->stream))
     return fail(MTTS_E_PSE_TIMEOUT, "persistent streaming decode: a wait timed out (results since the last check "
@@ -796,6 +819,7 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   if (B <= 0 || B > c.max_batch || S <= 0 || past < 0 || past + S > c.max_ctx) return fail(MTTS_E_INVALID, "bad B/S/past");
   hipSetDevice(e->device);
   if (int rc = pse_lazy_check(e, false)) return rc;
+  if (int rc = pse_report_owed(e)) return rc;
   hipStream_t s = enter(e, stream);
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
   e->pse_choose(past + S);
@@ -804,7 +828,17 @@ extern "C" int mtts_forward(mtts_engine* e, const int64_t* ids, const uint8_t* m
   if (!rc && S == 1 && e->pse_takes(B) && (e->pse_now || (B == 1 && e->pse_long_now)) && e->pse_err(B)) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     HIPCHK(hipStreamIsCapturing(s, &cs));
-    if (cs == hipStreamCaptureStatusNone) {  // (inside a caller's capture: mtts_pse_check reads the word)
+    if (cs != hipStreamCaptureStatusNone) {
+      // inside a caller's capture: mtts_pse_check reads the word
+    } else if (!e->pse_lazy) {
+      // default: check now; a timed-out launch wrote only its own granules, the residual and this
+      // step's KV rows, so the step is recomputed on the per-op launches (which rewrite those rows)
+      // and the caller gets valid logits from this very call
+      if (pse_tripped(e, s)) {
+        e->pse_choose(past + S);
+        rc = forward_chunked(e, ids, B, S, past, reinterpret_cast<bf16_t*>(logits), s);
+      }
+    } else {
       HIPCHK(hipMemcpyAsync(e->pse_err_host, e->pse_err(B), 4, hipMemcpyDeviceToHost, s));
       HIPCHK(hipEventRecord(e->ev_pse, s));
       e->pse_pending = true;
@@ -868,9 +902,12 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   if (B <= 0 || B > c.max_batch || T <= 0 || max_new <= 0 || T + max_new > c.max_ctx)
     return fail(MTTS_E_INVALID, "B/T/max_new_tokens exceed the engine capacity");
   hipSetDevice(e->device);
-  // a tripped teacher-forced launch of earlier forwards: switch before this generation (reported
-  // by those forwards' check, not here: this generation is valid)
-  if (pse_lazy_check(e, true)) g_err.clear();
+  // a tripped teacher-forced launch of earlier (lazily checked) forwards: switch before this
+  // generation, which is valid; the timeout stays owed to the caller (pse_report_owed)
+  if (pse_lazy_check(e, true)) {
+    g_err.clear();
+    e->pse_unreported = true;
+  }
   hipStream_t s = enter(e, stream);
   GenDev& g = e->hst;
   std::memset(&g, 0, sizeof(g));
@@ -998,6 +1035,11 @@ extern "C" int mtts_generate(mtts_engine* e, const int64_t* ids, const uint8_t* 
       rc = mtts_generate_poll(e, &steps, &done, stream);
       if (rc) break;
       if (done >= 0 || steps >= max_new) break;
+      // every issued step advances the device's step counter (finalize), so a counter behind the
+      // issued steps with nothing left to issue is a broken state, not a wait: fail, never spin
+      if (e->steps_issued >= e->gen_max_new)
+        return fail(MTTS_E_HIP, "generation stalled: the device step counter is at " + std::to_string(steps) + " of " +
+                                    std::to_string(e->steps_issued) + " issued steps");
       rc = mtts_generate_decode(e, std::min(chunk, max_new - steps), stream);
       if (rc) break;
     }
@@ -1060,6 +1102,7 @@ extern "C" int mtts_k_qk_norm_rope(const uint16_t* qkv, uint16_t* q_out, uint16_
   QKRopeArgs a;
   a.qkv = qkv; a.q_out = q_out; a.kc = kc; a.vc = vc; a.qn_w = qn; a.kn_w = kn; a.cos_t = cs; a.sin_t = sn;
   a.pos_base = pos; a.S = S; a.Hq = Hq; a.Hkv = Hkv; a.D = D; a.Cmax = Cmax; a.eps = eps; a.M = M;
+  a.rope_off = nullptr;
   HIPCHK(qk_norm_rope(a, (hipStream_t)stream));
   return 0;
 }

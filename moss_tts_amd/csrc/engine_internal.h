@@ -49,6 +49,7 @@ struct Stack {
   bool attn_direct = false; // the context never spans two attention blocks: the attention writes its
                             // rows directly and o_proj is a plain GEMV (no split partials to merge)
   int attn_nwv = 0;         // decode attention waves per block for this stack (0: the engine default)
+  const int* rope_off = nullptr;  // [rows] RoPE position offsets (MossTTSLocal backbone; null: positions = slots)
 };
 
 constexpr int SK_TILES = 256;                   // split-K GEMV: most output tiles, and
@@ -79,7 +80,8 @@ struct mtts_engine {
   float* part = nullptr;
   size_t part_floats = 0;
   bf16_t* logits = nullptr;
-  int* d_pos = nullptr;  // pos_base for teacher-forced forwards / prefill
+  int* d_pos = nullptr;
+  int* rope_off = nullptr;  // [max_batch]: MossTTSLocal backbone rows' left-pad counts (Stack::rope_off)  // pos_base for teacher-forced forwards / prefill
   int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
   int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
   bool full_text_head = false;    // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)
@@ -129,6 +131,13 @@ struct mtts_engine {
   uint32_t* pse_err_host = nullptr;
   hipEvent_t ev_pse = nullptr;
   bool pse_pending = false;
+  // teacher-forced forwards through a launch: by default checked synchronously (a timed-out launch
+  // is recomputed on the per-op launches inside the same call); mtts_engine_set_pse_lazy(e, 1)
+  // opts into the async check above (no host sync per forward; errors surface on a later call)
+  bool pse_lazy = false;
+  // a lazily detected timeout that a generation start swallowed (that generation is valid) is
+  // still owed to the caller: the next mtts_pse_check / mtts_forward reports it once
+  bool pse_unreported = false;
   bool pse_coop = false;            // MTTS_PSE_COOP=1: cooperative launch (hipLaunchCooperativeKernel)
   uint64_t* pse_trace = nullptr;    // MTTS_PSE_TRACE=1: per-layer event stamps of the last launch
   // generate state

@@ -106,6 +106,9 @@ struct QKRopeArgs {
   const bf16_t* cos_t;  // [max_pos, D]
   const bf16_t* sin_t;
   const int* pos_base;  // device: position of token s=0 (same for all rows)
+  // device [rows] or null: RoPE position of row b's token = max(0, pos - rope_off[b]) (MossTTSLocal:
+  // GenerationMixin's positions exclude a row's left pads); the cache slot stays pos
+  const int* rope_off;
   int S;                // tokens per row
   int Hq, Hkv, D;
   int Cmax;
@@ -138,6 +141,7 @@ struct DecAttnArgs {
   bf16_t* vc;
   const uint8_t* mask;  // [Bmax][Cmax]
   const int* pos;       // device: absolute position of the new token
+  const int* rope_off;  // device [B] or null: the token's RoPE position is max(0, pos - rope_off[b])
   bf16_t* out;          // [B, Hq * D]
   float* part;          // split partials [B][Hkv][ns][G*(D+2)]
   int* cnt;             // arrival tickets [B][Hkv], zero between launches
@@ -336,6 +340,9 @@ hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);
 // local.hip (MossTTSLocal depth stage)
 hipError_t moss_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s);
 hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld_out, int B, hipStream_t s);
+// per-row count of masked (pad) columns among the first n of a [B][ld] key mask: the offset
+// between a row's cache slots and its RoPE positions (kernels.h QKRopeArgs::rope_off)
+hipError_t row_pad_count(const uint8_t* mask, int ld, int n, int B, int* out, hipStream_t s);
 hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, int C, int64_t* gen_ids, int Ltot,
                       uint8_t* mask, int Cmax, int* finished, uint8_t* seen, int audio_rows, hipStream_t s);
 hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, uint8_t* seen,

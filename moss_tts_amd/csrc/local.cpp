@@ -551,6 +551,7 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   p.n_ch = n_channels(e, n_vq_for_inference);
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
   HIPCHK(local_init(ids, mask, B, T, p.C, e->gen_ids, c.max_ctx, e->mask, c.max_ctx, p.finished, p.seen, e->audio_rows, s));
+  HIPCHK(row_pad_count(e->mask, c.max_ctx, T, B, e->rope_off, s));  // left pads: RoPE offsets
   int rc = forward_chunked(e, ids, B, T, 0, nullptr, s, p.hid, p.n_ch);
   if (!rc) rc = local_depth(e, B, p.n_ch, nullptr, 0, nullptr, 0, s);
   if (!rc) rc = local_frame_end(e, s);
@@ -622,6 +623,11 @@ extern "C" int mtts_local_generate(mtts_engine* e, const int64_t* ids, const uin
       rc = mtts_generate_poll(e, &steps, &done, stream);
       if (rc) break;
       if (done >= 0 || steps >= max_new) break;
+      // every issued step advances the device's step counter (finalize), so a counter behind the
+      // issued steps with nothing left to issue is a broken state, not a wait: fail, never spin
+      if (e->steps_issued >= e->gen_max_new)
+        return fail(MTTS_E_HIP, "generation stalled: the device step counter is at " + std::to_string(steps) + " of " +
+                                    std::to_string(e->steps_issued) + " issued steps");
       rc = mtts_local_generate_decode(e, std::min(chunk, max_new - steps), stream);
       if (rc) break;
     }
@@ -644,6 +650,7 @@ extern "C" int mtts_local_forward(mtts_engine* e, const int64_t* ids, const uint
   const int n_ch = n_channels(e, n_vq_for_inference);
   hipStream_t s = enter(e, stream);
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
+  HIPCHK(row_pad_count(e->mask, c.max_ctx, past + S, B, e->rope_off, s));  // left pads: RoPE offsets
   int rc = forward_chunked(e, ids, B, S, past, nullptr, s, p.hid, n_ch);
   if (!rc) rc = local_depth(e, B, n_ch, forced, p.C, reinterpret_cast<bf16_t*>(logits), ld_logits, s);
   if (!rc && local_lpse_takes(e, B)) {

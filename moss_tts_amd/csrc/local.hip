@@ -280,6 +280,25 @@ hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, 
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void row_pad_count_kernel(const uint8_t* __restrict__ mask, int ld, int n,
+                                                            int* __restrict__ out) {
+  const int b = blockIdx.x;
+  int z = 0;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) z += mask[(size_t)b * ld + t] == 0;
+  __shared__ int tot;
+  if (threadIdx.x == 0) tot = 0;
+  __syncthreads();
+  atomicAdd(&tot, z);
+  __syncthreads();
+  if (threadIdx.x == 0) out[b] = tot;
+}
+
+hipError_t row_pad_count(const uint8_t* mask, int ld, int n, int B, int* out, hipStream_t s) {
+  if (B <= 0 || n < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(row_pad_count_kernel, dim3(B), dim3(256), 0, s, mask, ld, n, out);
+  return hipGetLastError();
+}
+
 // End of a frame (:425-446): channels >= n_ch are 0; finished rows emit eos / pad; the frame
 // is appended at column T0 + step and unmasked for the next forward; a row finishes on eos
 // in channel 0.  One block, a thread per row.

@@ -160,6 +160,7 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
   const int hd = gw % heads;
   const int b = m / a.S, s = m % a.S;
   const int pos = *a.pos_base + s;
+  const int rpos = a.rope_off ? max(0, pos - a.rope_off[b]) : pos;  // RoPE position (cache slot: pos)
   const int D = a.D;
   const bool act = 2 * lane < D;
   const bf16_t* src = a.qkv + (size_t)m * heads * D + (size_t)hd * D;
@@ -199,8 +200,8 @@ __global__ __launch_bounds__(256) void qk_norm_rope_kernel(QKRopeArgs a) {
   const float sg = (2 * lane < D / 2) ? -1.f : 1.f;
   float c0 = 0.f, c1 = 0.f, s0 = 0.f, s1 = 0.f;
   if (act) {
-    const uint32_t pc = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)pos * D + 2 * lane);
-    const uint32_t ps = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)pos * D + 2 * lane);
+    const uint32_t pc = *reinterpret_cast<const uint32_t*>(a.cos_t + (size_t)rpos * D + 2 * lane);
+    const uint32_t ps = *reinterpret_cast<const uint32_t*>(a.sin_t + (size_t)rpos * D + 2 * lane);
     c0 = __uint_as_float(pc << 16); c1 = __uint_as_float(pc & 0xffff0000u);
     s0 = __uint_as_float(ps << 16); s1 = __uint_as_float(ps & 0xffff0000u);
   }

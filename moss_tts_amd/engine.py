@@ -153,10 +153,17 @@ class Engine:
         """Longest context (prompt + new tokens) a batch-1 decode runs through pse.hip; 0 if inactive."""
         return int(N.load().mtts_pse_ctx_max(self._h))
 
+    def set_pse_lazy(self, lazy: bool = True):
+        """Opt into lazily checked teacher-forced forwards through the persistent launch (no host
+        sync per `forward`; a timed-out launch surfaces as `PseTimeout` from `pse_check` or a later
+        `forward`).  Default: each `forward` checks its launch and recomputes a timed-out step on
+        the per-op launches before returning."""
+        N.check(N.load().mtts_engine_set_pse_lazy(self._h, 1 if lazy else 0), "set_pse_lazy")
+
     def pse_check(self):
         """Blocking check of the persistent launch's error word for the teacher-forced forwards so
-        far (`forward` itself does not synchronise).  Raises `PseTimeout` once when a launch timed
-        out: those forwards' logits are invalid, the engine now runs the per-op launches."""
+        far.  Raises `PseTimeout` once when a lazily checked launch (`set_pse_lazy`) timed out:
+        those forwards' logits are invalid, the engine now runs the per-op launches."""
         N.check(N.load().mtts_pse_check(self._h), "pse_check")
 
     def kv_write(self, layer: int, row: int, pos0: int, k, v):

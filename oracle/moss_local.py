@@ -23,8 +23,12 @@ Parity pinning: tests/golden/make_golden_local.py runs the REFERENCE's own modul
 (backbone `model.model`, the MLP adapters, `local_transformer.layers[i]` + `.norm`, the
 norms and heads) in a restated greedy loop, because the reference `generate()` itself does
 not run on the installed transformers 5.15.  Batches are unpadded in the
-fixtures: for left-padded batches the reference's position ids come from transformers'
-generation utilities, which differ between versions -- parity unpinned there.
+fixtures.  Positions (round 5): the reference forward takes `position_ids`, so the installed
+GenerationMixin (transformers 5.15) fills them: cumsum(attention_mask) - 1 with pads set to 0
+(`transformers/generation/utils.py:751-773`, called at :2564-2567), then last + 1 per step
+(:975-985).  A left-padded row's positions therefore EXCLUDE its pads (the Delay model's
+`generate` runs its own loop, whose positions include them).  `generate` below restates that;
+the ragged fixtures (`l_*_ragged_*`) pin it to the reference's modules driven with those ids.
 """
 from dataclasses import dataclass
 from typing import Dict, List
@@ -198,13 +202,28 @@ def embed(ctx, W, cfg, ids, n_ch):
     return e
 
 
-def backbone(ctx, W, cfg, ids, attention_mask, cache, n_ch):
+def hf_position_ids(attention_mask):
+    """GenerationMixin._prepare_position_ids_for_generation (transformers 5.15,
+    `generation/utils.py:751-773`): cumsum(mask) - 1, pads set to 0.  [B, T] int64."""
+    m = np.asarray(attention_mask, bool)
+    pos = np.cumsum(m, axis=-1) - 1
+    return np.where(m, pos, 0).astype(np.int64)
+
+
+def backbone(ctx, W, cfg, ids, attention_mask, cache, n_ch, position_ids=None):
     """Qwen3Model over the summed embeddings; returns the final-normed hidden state of the
-    last position [B, H].  Positions are arange(S) + past (unpadded batches)."""
+    last position [B, H].  position_ids [B, S] (RoPE; None: arange(S) + past); the causal mask
+    works on cache slots (arange(S) + past) and attention_mask [B, past + S]."""
     B, S, _ = ids.shape
     past = cache.length()
     pos = np.arange(S) + past
-    cos, sin = rope_cos_sin(ctx, cfg, pos)
+    if position_ids is None:
+        cos, sin = rope_cos_sin(ctx, cfg, pos)
+    else:
+        rp = np.asarray(position_ids, np.int64).reshape(B, S)
+        cos, sin = rope_cos_sin(ctx, cfg, rp.reshape(-1))
+        cos = cos.reshape(B, 1, S, -1)
+        sin = sin.reshape(B, 1, S, -1)
     h = embed(ctx, W, cfg, ids, n_ch)
     km = np.asarray(attention_mask, bool)
     for l in range(cfg.layers):
@@ -256,12 +275,13 @@ def generate(W, cfg: LCfg, input_ids, attention_mask=None, max_new_tokens=100, n
     nq = cfg.n_vq if n_vq_for_inference is None else n_vq_for_inference
     n_ch = min(C, 1 + nq)
     mask = np.ones((B, T), bool) if attention_mask is None else np.asarray(attention_mask, bool)
+    pos = hf_position_ids(mask)  # grows by last + 1 per step (utils.py:975-985)
     cache = Cache(cfg.layers)
     unfinished = np.ones(B, np.int64)
     cur = ids
     step_in = ids
     for _ in range(max_new_tokens):
-        g = backbone(ctx, W, cfg, step_in, mask, cache, n_ch)
+        g = backbone(ctx, W, cfg, step_in, mask, cache, n_ch, position_ids=pos[:, -step_in.shape[1]:])
         step = cur.shape[1] - T
         fr = local_frame(ctx, W, cfg, g, n_ch, trace=trace,
                          forced=None if forced is None else forced[:, step, :n_ch])
@@ -272,6 +292,7 @@ def generate(W, cfg: LCfg, input_ids, attention_mask=None, max_new_tokens=100, n
             nxt[:, i] = nxt[:, i] * unfinished + pddp * (1 - unfinished)
         cur = np.concatenate([cur, nxt[:, None, :]], axis=1)
         mask = np.concatenate([mask, np.ones((B, 1), bool)], axis=1)
+        pos = np.concatenate([pos, pos[:, -1:] + 1], axis=1)
         unfinished = unfinished & (nxt[:, 0] != cfg.eos_token_id).astype(np.int64)
         step_in = nxt[:, None, :]
         if unfinished.max() == 0 or (forced is not None and cur.shape[1] - T >= forced.shape[1]):

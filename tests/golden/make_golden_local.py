@@ -9,7 +9,13 @@ The reference `generate()` (GenerationMixin + `CustomMixin._sample`,
 `moss_tts_local/modeling_moss_tts.py:315-477`) does not run on the installed transformers
 5.15, so the greedy loop of `_sample` (:377-456) is restated here around
 the reference's modules, called exactly as `_sample` calls them:
-  backbone    `model.model(...)` with a DynamicCache, `hidden_states[-1][:, -1]` (:384-390)
+  backbone    `model.model(...)` with a DynamicCache, `hidden_states[-1][:, -1]` (:384-390),
+              with the `attention_mask` and `position_ids` that the installed GenerationMixin
+              hands the forward (the reference forward takes `position_ids`, :536 / :656, so
+              `generate` fills them, transformers/generation/utils.py:2564-2567):
+              cumsum(mask) - 1 with pads set to 0 (:751-773), then last + 1 per step, the mask
+              grown by ones (`_update_model_kwargs_for_generation`, :975-992); for a left-padded
+              row the positions EXCLUDE its pads (the Delay path's include them)
   depth loop  `speech_embedding_to_local_mlp` (:395, :423), `local_transformer.layers[l]`
               + `local_transformer.norm` over the channel inputs so far (the body of
               `MossTTSLocalTransformer.forward`, :260-281, whose mask helper call fails on
@@ -69,20 +75,23 @@ def ref_model(cfg, W, dtype):
 
 
 @torch.no_grad()
-def ref_generate(m, cfg, ids, max_new, n_vq_inf, dtype):
+def ref_generate(m, cfg, ids, max_new, n_vq_inf, dtype, mask0=None):
     from transformers.cache_utils import DynamicCache
     dt = torch.bfloat16 if dtype == "bf16" else torch.float32
     B, T, C = ids.shape
     n_ch = min(C, 1 + n_vq_inf)
     cur = torch.from_numpy(ids)
-    mask = torch.ones(B, T, dtype=torch.long)
+    mask = torch.ones(B, T, dtype=torch.long) if mask0 is None else torch.from_numpy(mask0.astype(np.int64))
+    pos = mask.cumsum(-1) - 1
+    pos = pos.masked_fill(mask == 0, 0)
     cache = DynamicCache()
     unfinished = torch.ones(B, dtype=torch.long)
     step_in = cur
     logits_trace = []
     for step in range(max_new):
-        out = m.model(input_ids=step_in, attention_mask=mask, past_key_values=cache, use_cache=True,
-                      output_hidden_states=True, return_dict=True, n_vq_for_inference=n_vq_inf)
+        out = m.model(input_ids=step_in, attention_mask=mask, position_ids=pos[:, -step_in.shape[1]:],
+                      past_key_values=cache, use_cache=True, output_hidden_states=True, return_dict=True,
+                      n_vq_for_inference=n_vq_inf)
         g = out.hidden_states[-1][:, -1, :]
         last = out.last_hidden_state[:, -1, :]
         assert torch.equal(g, last), "hidden_states[-1] is the final-normed state"
@@ -114,6 +123,7 @@ def ref_generate(m, cfg, ids, max_new, n_vq_inf, dtype):
             nxt[:, i] = nxt[:, i] * unfinished + pddp * (1 - unfinished)
         cur = torch.cat([cur, nxt[:, None, :]], 1)
         mask = torch.cat([mask, torch.ones(B, 1, dtype=torch.long)], 1)
+        pos = torch.cat([pos, pos[:, -1:] + 1], 1)
         unfinished = unfinished & (nxt[:, 0] != cfg.eos_token_id).long()
         step_in = nxt[:, None, :]
         if unfinished.max() == 0:
@@ -147,6 +157,20 @@ def prompt(cfg, rng, n_text, ref_frames):
     return np.stack(rows)
 
 
+def left_pad(cfg, rows):
+    """the processor's batch layout: left pads (channel 0 pad_token_id, codebooks
+    audio_pad_code), attention mask False there"""
+    T = max(r.shape[0] for r in rows)
+    C = rows[0].shape[1]
+    ids = np.full((len(rows), T, C), cfg.audio_pad_code, np.int64)
+    ids[..., 0] = cfg.pad_token_id
+    mask = np.zeros((len(rows), T), bool)
+    for b, r in enumerate(rows):
+        ids[b, T - r.shape[0]:] = r
+        mask[b, T - r.shape[0]:] = True
+    return ids, mask
+
+
 def main():
     cases = {}
     arrays = {}
@@ -157,21 +181,28 @@ def main():
         ("l_nvq8_clone_bf16", 8, 8, 2, 22, 10, 6, 10, 0.0, "bf16"),
         ("l_nvq8_depth4_bf16", 8, 4, 1, 23, 9, 4, 10, 0.0, "bf16"),
         ("l_nvq4_stop_fp32", 4, 4, 2, 24, 8, 0, 30, 40.0, "fp32"),
+        # ragged (left-padded) batches, `MossTTSDelayProcessor._pad` (processing_moss_tts.py:415-436)
+        ("l_nvq4_ragged_fp32", 4, 4, 3, 25, [5, 14, 9], [0, 3, 1], 12, 0.0, "fp32"),
+        ("l_nvq8_ragged_bf16", 8, 8, 3, 26, [12, 4, 8], [2, 0, 5], 10, 0.0, "bf16"),
     ]
     for name, n_vq, nq_inf, B, seed, n_text, ref_frames, steps, eos_boost, dtype in specs:
         cfg = L.tiny_lcfg(n_vq=n_vq)
         W = L.make_weights(cfg, seed, dtype=dtype, eos_boost=eos_boost)
         rng = np.random.default_rng(seed)
-        p = [prompt(cfg, rng, n_text, ref_frames) for _ in range(B)]
-        ids = np.stack(p)  # equal lengths: unpadded batch
+        nt = n_text if isinstance(n_text, list) else [n_text] * B
+        rf = ref_frames if isinstance(ref_frames, list) else [ref_frames] * B
+        p = [prompt(cfg, rng, nt[b], rf[b]) for b in range(B)]
+        ids, mask = left_pad(cfg, p)
         m = ref_model(cfg, W, dtype)
-        out, lt = ref_generate(m, cfg, ids, steps, nq_inf, dtype)
+        out, lt = ref_generate(m, cfg, ids, steps, nq_inf, dtype, mask0=mask if not mask.all() else None)
         arrays[name + "/input_ids"] = ids
+        if not mask.all():
+            arrays[name + "/attention_mask"] = mask
         arrays[name + "/out"] = out
         for k, lg in enumerate(lt):
             arrays[f"{name}/logit{k}"] = lg.astype(np.float32)
         cases[name] = dict(n_vq=n_vq, n_vq_inf=nq_inf, B=B, seed=seed, steps=steps, eos_boost=eos_boost, dtype=dtype,
-                           n_logits=len(lt), out_len=int(out.shape[1]))
+                           n_logits=len(lt), out_len=int(out.shape[1]), padded=bool(not mask.all()))
         print(name, ids.shape, "->", out.shape, flush=True)
     np.savez_compressed(os.path.join(OUT, "golden_local.npz"), **arrays)
     with open(os.path.join(OUT, "cases_local.json"), "w") as f:

@@ -14,10 +14,15 @@
 //   make -C tests/native && tests/native/asan_driver     (GPU box)
 #include <hip/hip_runtime.h>
 
+#include <unistd.h>
+
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mtts.h"
@@ -32,6 +37,44 @@ static int g_fail = 0;
     }                                                                                           \
   } while (0)
 #define OK(x) EXPECT((x) == 0, #x)
+
+// Progress log + watchdog (round 5).  One run of this driver inside the GPU
+// suite once went silent for 180 s and was killed with its output captured, so nothing said where
+// it was.  Every phase now writes a line (flushed) to $MTTS_ASAN_LOG (else stderr) before it
+// starts, and a watchdog thread ends the process with exit code 3, naming the phase, when one
+// phase runs longer than $MTTS_ASAN_PHASE_TIMEOUT seconds (default 90).  The last line before
+// `return` says "exit": a stall after it is the LeakSanitizer leak check or the runtime's teardown
+// (the watchdog is suspended with every other thread during the leak check; the test's own
+// subprocess timeout covers that window).
+static FILE* g_log = nullptr;
+static std::atomic<int> g_phase_id{0};
+static std::atomic<long long> g_phase_t0{0};
+static const char* volatile g_phase = "start";
+static long long now_ms() {
+  return std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+static long long g_start_ms = now_ms();
+static void phase(const char* name) {
+  g_phase = name;
+  g_phase_t0.store(now_ms());
+  g_phase_id.fetch_add(1);
+  fprintf(g_log, "[%8.3f s] %s\n", (now_ms() - g_start_ms) / 1000.0, name);
+  fflush(g_log);
+}
+static void watchdog(int limit_s) {
+  for (;;) {
+    std::this_thread::sleep_for(std::chrono::milliseconds(500));
+    const long long age = now_ms() - g_phase_t0.load();
+    if (age > (long long)limit_s * 1000) {
+      fprintf(g_log, "[%8.3f s] STALL: phase '%s' has run %.1f s (limit %d s)\n", (now_ms() - g_start_ms) / 1000.0,
+              (const char*)g_phase, age / 1000.0, limit_s);
+      fflush(g_log);
+      fprintf(stderr, "asan driver: STALL in phase '%s' after %.1f s\n", (const char*)g_phase, age / 1000.0);
+      fflush(stderr);
+      _exit(3);
+    }
+  }
+}
 
 template <class T>
 static T* dev(size_t n) {
@@ -80,6 +123,7 @@ static void delay_engine() {
   const int n_vq = 4, C = n_vq + 1, B = 3, T = 20, max_new = 24;
   mtts_config c = tiny(n_vq, MTTS_MODEL_DELAY);
   mtts_engine* e = nullptr;
+  phase("delay: create + init_random");
   OK(mtts_engine_create(&c, 0, &e));
   if (!e) return;
   OK(mtts_engine_init_random(e, 7));
@@ -87,6 +131,7 @@ static void delay_engine() {
   OK(mtts_engine_weight_bytes(e, &wb));
   EXPECT(wb > 0, "weight bytes");
   // weight loading by name: host and device sources, bad names and sizes
+  phase("delay: load_weight by name");
   const int H = c.hidden;
   std::vector<uint16_t> host((size_t)c.vocab * H, 0x3f80);
   OK(mtts_engine_load_weight(e, "language_model.norm.weight", host.data(), H * 2, 0));
@@ -101,6 +146,7 @@ static void delay_engine() {
   EXPECT(mtts_engine_load_weight(nullptr, "x", host.data(), 2, 0) == MTTS_E_INVALID, "null engine");
   OK(mtts_engine_init_random(e, 7));
   // forward: prefill + 3 decode steps, ragged mask
+  phase("delay: teacher-forced forward (prefill + 3 steps)");
   std::vector<int64_t> ids = prompt(B, T + 3, C, 1);
   int64_t* d_ids = dev<int64_t>(ids.size());
   hipMemcpy(d_ids, ids.data(), ids.size() * 8, hipMemcpyHostToDevice);
@@ -141,8 +187,14 @@ static void delay_engine() {
   mtts_sampling sampled{1.5f, 1.f, 50, 1.7f, 0.8f, 25, 1.1f, 2};
   mtts_sampling wide{1.0f, 0.9f, 0, 1.2f, 0.95f, 0, 1.0f, 3};
   int64_t* d_out = dev<int64_t>((size_t)B * (T + max_new) * C);
+  const char* gen_names[3][2] = {{"delay: generate greedy", "delay: generate greedy, forced"},
+                                 {"delay: generate sampled", "delay: generate sampled, forced"},
+                                 {"delay: generate wide text top_k", "delay: generate wide text top_k, forced"}};
+  int gi = 0;
   for (const mtts_sampling* sp : {&greedy, &sampled, &wide}) {
+    int fi = 0;
     for (const int32_t* f : {(const int32_t*)nullptr, (const int32_t*)d_forced}) {
+      phase(gen_names[gi][fi++]);
       int n = 0;
       OK(mtts_generate(e, d_gp, d_gm, B, T, max_new, sp, f, 8, &n, nullptr));
       EXPECT(n >= 1 && n <= max_new, "generated rows");
@@ -152,8 +204,10 @@ static void delay_engine() {
       OK(mtts_generate_stats(e, &hs));
       EXPECT(hs >= 1, "text head steps");
     }
+    ++gi;
   }
   // stepwise API
+  phase("delay: stepwise begin / poll / decode");
   OK(mtts_generate_begin(e, d_gp, d_gm, B, T, max_new, &sampled, nullptr, nullptr));
   int steps = 0, done = -2;
   OK(mtts_generate_poll(e, &steps, &done, nullptr));
@@ -164,6 +218,7 @@ static void delay_engine() {
          "max_new beyond capacity");
   EXPECT(mtts_generate_fetch(e, d_out, -1, nullptr) == MTTS_E_INVALID, "bad n_rows");
   // capacity regrow keeps the weights; generate again at the larger size
+  phase("delay: reserve + generate at the larger capacity");
   OK(mtts_engine_reserve(e, 4, 256, 128));
   {
     int n = 0;
@@ -171,6 +226,7 @@ static void delay_engine() {
   }
   EXPECT(mtts_engine_reserve(e, 0, 256, 0) == MTTS_E_INVALID, "bad reserve");
   // roofline probe
+  phase("delay: time_gemv probes");
   float ms = 0.f;
   uint64_t nb = 0;
   for (int which = 0; which < 5; ++which) OK(mtts_engine_time_gemv(e, which, 0, 2, 3, &ms, &nb));
@@ -178,6 +234,7 @@ static void delay_engine() {
   EXPECT(mtts_engine_time_gemv(e, 6, 0, 1, 1, &ms, &nb) == MTTS_E_UNSUPPORTED, "depth stack on a Delay engine");
   EXPECT(mtts_local_forward(e, d_ids, mask.data(), 1, 1, 0, -1, nullptr, d_logits, ld, nullptr) == MTTS_E_UNSUPPORTED,
          "local entry point on a MossTTSDelay engine");
+  phase("delay: destroy");
   OK(mtts_engine_destroy(e));
   for (void* p : {(void*)dsrc, (void*)d_ids, (void*)d_logits, (void*)d_gp, (void*)d_gm, (void*)d_forced, (void*)d_out})
     hipFree(p);
@@ -187,6 +244,7 @@ static void local_engine() {
   const int n_vq = 4, C = n_vq + 1, B = 2, T = 12;
   mtts_config c = tiny(n_vq, MTTS_MODEL_LOCAL);
   mtts_engine* e = nullptr;
+  phase("local: create + init_random");
   OK(mtts_engine_create(&c, 0, &e));
   if (!e) return;
   OK(mtts_engine_init_random(e, 5));
@@ -198,15 +256,18 @@ static void local_engine() {
   const int ld = (c.vocab + 7) / 8 * 8;
   uint16_t* d_lg = dev<uint16_t>((size_t)C * B * ld);
   int64_t* d_forced = dev<int64_t>((size_t)B * C);
+  phase("local: teacher-forced frames");
   OK(mtts_local_forward(e, d_ids, d_m, B, T, 0, -1, d_forced, d_lg, ld, nullptr));
   OK(mtts_local_forward(e, d_ids, d_m, B, T, 0, 2, d_forced, d_lg, ld, nullptr));
   EXPECT(mtts_local_forward(e, d_ids, d_m, B, T, 0, -1, d_forced, d_lg, 8, nullptr) == MTTS_E_INVALID, "small ld");
   mtts_sampling sp{1.5f, 1.f, 50, 1.0f, 0.95f, 50, 1.1f, 4};
   int64_t* d_out = dev<int64_t>((size_t)B * (T + 16) * C);
   int n = 0;
+  phase("local: generate greedy / sampled");
   OK(mtts_local_generate(e, d_ids, nullptr, B, T, 8, -1, nullptr, 4, &n, nullptr));
   OK(mtts_local_generate(e, d_ids, nullptr, B, T, 8, 2, &sp, 4, &n, nullptr));
   OK(mtts_generate_fetch(e, d_out, n, nullptr));
+  phase("local: per-channel sampling tables");
   std::vector<mtts_channel_sampling> ch(C);
   for (int i = 0; i < C; ++i) ch[i] = mtts_channel_sampling{i % 2, 1.0f + 0.5f * i, i == 0 ? 20 : 0, 0.9f, 1.2f};
   OK(mtts_local_set_sampling(e, ch.data(), C));
@@ -216,6 +277,7 @@ static void local_engine() {
   OK(mtts_local_generate(e, d_ids, nullptr, B, T, 8, -1, &sp, 4, &n, nullptr));
   OK(mtts_local_set_sampling(e, nullptr, 0));
   EXPECT(mtts_local_set_sampling(e, ch.data(), C + 1) == MTTS_E_INVALID, "too many channels");
+  phase("local: frame bytes + time_gemv probes + destroy");
   uint64_t fb = 0;
   OK(mtts_local_frame_bytes(e, -1, &fb));
   float ms = 0.f;
@@ -234,6 +296,7 @@ static void codec() {
   k.stages[1] = mtts_codec_stage{64, 1, 2, 2, 32, 128, 1};
   k.patch = 24; k.rope_theta = 10000.f; k.rms_eps = 1e-6f; k.max_batch = 2; k.max_frames = 64; k.max_chunk_frames = 6;
   mtts_codec* d = nullptr;
+  phase("codec: create / decode / chunked decode / load_weight / destroy");
   OK(mtts_codec_create(&k, 0, &d));
   if (!d) return;
   OK(mtts_codec_init_random(d, 3));
@@ -262,6 +325,7 @@ static void codec() {
 
 static void kernels() {
   // kernel-level entry points on caller-owned buffers
+  phase("kernel-level entry points");
   const int B = 2, N = 48, K = 64;
   const size_t pb = mtts_k_packed_bytes(N, K);
   uint16_t* w = dev<uint16_t>((size_t)N * K);
@@ -282,6 +346,12 @@ static void kernels() {
 }
 
 int main() {
+  const char* lp = getenv("MTTS_ASAN_LOG");
+  g_log = lp && *lp ? fopen(lp, "a") : nullptr;
+  if (!g_log) g_log = stderr;
+  const char* lim = getenv("MTTS_ASAN_PHASE_TIMEOUT");
+  std::thread(watchdog, lim && atoi(lim) > 0 ? atoi(lim) : 90).detach();
+  phase("HIP init");
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) {
     fprintf(stderr, "no GPU\n");
@@ -297,7 +367,9 @@ int main() {
   local_engine();
   codec();
   kernels();
+  phase("final device synchronize");
   hipDeviceSynchronize();
+  phase("exit (LeakSanitizer leak check, runtime teardown)");
   printf("asan driver: %s (%d failed checks)\n", g_fail ? "FAILED" : "ok", g_fail);
   return g_fail ? 1 : 0;
 }

@@ -2,6 +2,7 @@
 numpy oracle on the same seeded inputs.  bf16 tolerance: results within the
 bf16 rounding band of the oracle (different fp32 summation order)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -199,7 +200,7 @@ def xpk_indices(M, K):
 
 @pytest.mark.parametrize("M,Nr,K,epi", [(181, 6144, 4096, 0), (181, 4096, 4096, 1), (181, 12288, 4096, 2),
                                         (181, 4096, 12288, 1), (130, 1000, 512, 1), (192, 96, 1024, 2),
-                                        (2048, 4096, 4096, 1), (2048, 1536, 2048, 2)])
+                                        (2048, 4096, 4096, 1), (2048, 1536, 2048, 2), (1024, 12288, 4096, 2)])
 def test_gemm_packed_prefill(N, M, Nr, K, epi):
     """Prefill GEMM on fragment-packed activations (the engine's >= 128-row prompts) at the 8B
     projections' shapes: 181 rows take gemm3's one-token-block form (split K for q|k|v, o_proj,
@@ -251,6 +252,20 @@ def test_gemm_packed_prefill(N, M, Nr, K, epi):
         g2 = np.pad(got, ((0, 0), (0, nt * 16 - Nr))).reshape(M, nt, 16)
         want_ss = (g2.astype(np.float64) ** 2).sum(-1)
         assert np.allclose(ss.cpu().numpy(), want_ss, rtol=1e-5, atol=1e-6)
+
+
+def test_gemm_packed_prefill_gemm3_forms():
+    """The gemm3 (LDS-DMA-only) forms that MTTS_GEMM5=0 / MTTS_GEMM5_LONG=0 fall back to, pinned
+    against the oracle by the same cases (the switches are read once per process, so
+    they run in a child pytest)."""
+    import subprocess
+    import sys
+    env = dict(os.environ, MTTS_GEMM5="0", MTTS_GEMM5_LONG="0")
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-p", "no:cacheprovider", "-m", "gpu",
+                        os.path.abspath(__file__) + "::test_gemm_packed_prefill"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert " passed" in r.stdout and "failed" not in r.stdout, r.stdout[-2000:]
 
 
 @pytest.mark.parametrize("B,Nr,K,splits", [(8, 1536, 8960, 0), (1, 1536, 8960, 3), (16, 1000, 4096, 2),

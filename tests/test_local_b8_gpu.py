@@ -138,14 +138,51 @@ def test_local_ragged_batch_teacher_forced(setup):
         band(lg[k].float().cpu().numpy(), trace[k], k)
 
 
-def test_local_b8_generate(setup):
-    """greedy generate (hipGraph frames, device pick) vs the oracle's greedy _sample loop"""
+def left_padded(T, seed):
+    """the benchmark's ragged batch as the processor lays it out (`_pad`,
+    moss_tts_local/processing_moss_tts.py:415-436): rows of different lengths left-padded with
+    pad_token_id / audio_pad_code, attention mask False there (pads 0..21 of T)"""
+    ids = prompts(T, seed)
+    pads = np.array([0, 3, 7, 21, 1, 12, 0, 16])
+    mask = np.ones((B, T), bool)
+    for b, p in enumerate(pads):
+        ids[b, :p] = CFG.audio_pad_code
+        ids[b, :p, 0] = CFG.pad_token_id
+        mask[b, :p] = False
+    return ids, mask
+
+
+def test_local_b8_left_padded(setup):
+    """configs[3]'s ragged prompts: a left-padded batch of 8 against the oracle, whose backbone
+    positions are GenerationMixin's (cumsum(mask) - 1: pads excluded, pinned to the reference's
+    modules by tests/test_oracle_local.py's ragged fixtures).  Teacher-forced logits of every
+    channel of two frames, then greedy generate (ids equal, or the first divergence a near tie)."""
     eng, W = setup
-    T, steps = 40, 3
-    ids = prompts(T, 3)
-    out = eng.local_generate_ids(torch.from_numpy(ids), None, steps).cpu().numpy()
-    want_rows = L.generate(W, CFG, ids, max_new_tokens=steps, dtype="bf16")
+    T, steps = 44, 3
+    ids, mask = left_padded(T, 9)
+    rng = np.random.default_rng(10)
+    C = CFG.n_vq + 1
+    frames = np.concatenate([rng.integers(200, 20000, (B, 2, 1)), rng.integers(0, 1024, (B, 2, CFG.n_vq))], 2)
+    allr = np.concatenate([ids, frames], 1)
+    got = []
+    for f in range(2):
+        x, past = (allr[:, :T], 0) if f == 0 else (allr[:, T + f - 1:T + f], T + f - 1)
+        m = np.ones((B, past + x.shape[1]), np.uint8)
+        m[:, :T] = mask
+        lg = eng.local_forward(torch.from_numpy(np.ascontiguousarray(x)), torch.from_numpy(m), past,
+                               torch.from_numpy(np.ascontiguousarray(allr[:, T + f])))
+        got += [t.float().cpu().numpy() for t in lg]
+    trace = []
+    L.generate(W, CFG, ids, attention_mask=mask, max_new_tokens=2, dtype="bf16", trace=trace, forced=frames)
+    for k in range(2 * C):
+        band(got[k], trace[k], k)
+    out = eng.local_generate_ids(torch.from_numpy(ids), torch.from_numpy(mask), steps).cpu().numpy()
+    want_rows = L.generate(W, CFG, ids, attention_mask=mask, max_new_tokens=steps, dtype="bf16")
     want = np.stack([np.concatenate([ids[b, :T - r[0] - 1], r[1]], 0) for b, r in enumerate(want_rows)])
+    _check_generate(W, ids, mask, out, want, T)
+
+
+def _check_generate(W, ids, mask, out, want, T):
     assert out.shape[2] == ids.shape[2] and np.array_equal(out[:, :T], ids)
     n = min(out.shape[1], want.shape[1])
     diff = np.argwhere(out[:, :n] != want[:, :n])
@@ -155,7 +192,8 @@ def test_local_b8_generate(setup):
     f = int(diff[:, 1].min()) - T
     assert f >= 0
     trace = []
-    L.generate(W, CFG, ids, max_new_tokens=f + 1, dtype="bf16", trace=trace, forced=want[:, T:T + f + 1])
+    L.generate(W, CFG, ids, attention_mask=mask, max_new_tokens=f + 1, dtype="bf16", trace=trace,
+               forced=want[:, T:T + f + 1])
     C = CFG.n_vq + 1
     rows = diff[diff[:, 1] == T + f]
     for b in np.unique(rows[:, 0]):
@@ -163,6 +201,17 @@ def test_local_b8_generate(setup):
         lg = trace[f * C + i][b]
         u = float(ulp_bf16(np.abs(lg[np.isfinite(lg)]).max()))
         assert margin_top2(lg) <= 24 * u, f"frame {f} row {b} channel {i}: divergence without a near tie"
+
+
+def test_local_b8_generate(setup):
+    """greedy generate (hipGraph frames, device pick) vs the oracle's greedy _sample loop"""
+    eng, W = setup
+    T, steps = 40, 3
+    ids = prompts(T, 3)
+    out = eng.local_generate_ids(torch.from_numpy(ids), None, steps).cpu().numpy()
+    want_rows = L.generate(W, CFG, ids, max_new_tokens=steps, dtype="bf16")
+    want = np.stack([np.concatenate([ids[b, :T - r[0] - 1], r[1]], 0) for b, r in enumerate(want_rows)])
+    _check_generate(W, ids, None, out, want, T)
 
 
 # (last in the file: it turns the launch off for the module's engine)

@@ -205,32 +205,52 @@ def test_pse_generation_crosses_the_context_range(engines):
 
 def test_pse_timeout_falls_back_to_launches(engines):
     """A persistent launch that gives up waiting (its workgroups not all resident: other work on
-    the device) is reported once, lazily (round 4: a teacher-forced forward no longer synchronises
-    the host): mtts_pse_check -- or the next forward once the async copy of the error word has
-    landed -- raises PseTimeout, the engine switches to the per-op launches, and the recomputed
-    steps are bit-identical to them; generate() restarts there by itself.  The timeout is
-    injected through the error word (mtts_pse_inject_timeout)."""
+    the device) never hands the caller invalid logits unannounced.  Default: the forward checks
+    its own launch and recomputes the step on the per-op launches before returning (ADVICE r4:
+    the HF-style `forward` path has no `pse_check` of its own).  Opt-in lazy form
+    (`set_pse_lazy`, no host sync per forward): `pse_check` -- or the next forward once the async
+    copy of the error word has landed -- raises PseTimeout once; a generation started in between
+    is valid and leaves the timeout owed to the next check.  Either way the engine switches to the
+    per-op launches and the recomputed steps are bit-identical to them; generate() restarts there
+    by itself.  The timeout is injected through the error word (mtts_pse_inject_timeout)."""
     from moss_tts_amd.engine import sampling_params
     from moss_tts_amd._native import PseTimeout
     ref, _ = engines
     ids, mask = prompt(120, 3, 17)
     want = decode_logits(ref, ids, mask, 120, 3)
-    for how in ("pse_check", "next_forward"):
+    sp = sampling_params(text_temperature=0, audio_temperature=0)
+    for how in ("sync", "pse_check", "next_forward", "generate_then_check"):
         e = make(True)
         try:
+            e.set_pse_lazy(how != "sync")
             e.forward(torch.from_numpy(ids[:, :120].copy()), torch.from_numpy(mask[:, :120]), 0)
             e.pse_check()  # the prefill (GEMM path) is clean
+            assert e.pse_active()
             e.inject_pse_timeout()  # the first decode step's launch sees the word set
-            e.forward(torch.from_numpy(ids[:, 120:121].copy()), torch.from_numpy(mask[:, :121]), 120)
+            lg = e.forward(torch.from_numpy(ids[:, 120:121].copy()), torch.from_numpy(mask[:, :121]), 120)
+            if how == "sync":
+                # recomputed inside the call: valid logits, nothing owed
+                assert np.array_equal(lg.float().cpu().numpy()[0], want[0])
+                assert not e.pse_active()
+                e.pse_check()
+                continue
             if how == "pse_check":
                 with pytest.raises(PseTimeout):
                     e.pse_check()
-            else:
+            elif how == "next_forward":
                 torch.cuda.synchronize()  # the async copy has landed: the next forward reports it
                 with pytest.raises(PseTimeout):
                     e.forward(torch.from_numpy(ids[:, 121:122].copy()), torch.from_numpy(mask[:, :122]), 121)
+            else:
+                g = torch.from_numpy(ids[:, :120].copy())
+                g[0, -1, 0] = 151652
+                e.generate_ids(g, torch.from_numpy(mask[:, :120].astype(bool)), 8, sp)  # valid: runs per-op
+                with pytest.raises(PseTimeout):
+                    e.pse_check()  # the swallowed timeout is still reported
             assert not e.pse_active()
             e.pse_check()  # reported once
+            if how == "generate_then_check":  # the generation rewrote the cache: prefill again
+                e.forward(torch.from_numpy(ids[:, :120].copy()), torch.from_numpy(mask[:, :120]), 0)
             got = []
             for s in range(3):  # the invalid step recomputed, then on
                 p = 120 + s
