@@ -108,13 +108,39 @@ def dp_global_leg(eng, world, rank, n_steps, forced, sp, per_gpu=4, reps=2):
     dt = float(dt[0])
     frames = [count_audio_frames(rows.numpy(), int(sl), 32) for sl, rows in out]
     audio_s = sum(frames) / FRAME_RATE * reps
+    # first-chunk latency of this rank's shard (its per-GPU batch, global padding): prefill + the
+    # decode steps until the first 1 s of audio (13 frames) has all 32 codebooks (frame f is final
+    # n_vq - 1 steps after its first code, processing_moss_tts.py:515-525); p50 over 5 runs
+    import ctypes
+    from moss_tts_amd import _native as Nn
+    from moss_tts_amd.dp import shard_bounds
+    lo, hi = shard_bounds(B, world, rank)
+    ids_d = ids[lo:hi].contiguous().cuda()
+    mask_d = mask[lo:hi].to(torch.uint8).contiguous().cuda()
+    first_steps = 1 + 13 + 32
+    lat = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        Nn.check(Nn.load().mtts_generate_begin(eng._h, ctypes.c_void_p(ids_d.data_ptr()), ctypes.c_void_p(mask_d.data_ptr()),
+                                               hi - lo, int(ids.shape[1]), n_steps, ctypes.byref(sp),
+                                               ctypes.c_void_p(forced.data_ptr()), None), "begin")
+        Nn.check(Nn.load().mtts_generate_decode(eng._h, first_steps - 1, None), "decode")
+        Nn.check(Nn.load().mtts_generate_poll(eng._h, None, None, None), "poll")
+        lat.append((time.perf_counter() - a) * 1e3)
+    p50 = torch.tensor([float(np.median(lat))], dtype=torch.float64, device="cuda")
+    if world > 1:
+        dist.all_reduce(p50, op=dist.ReduceOp.MAX)
     return {"workload": f"BASELINE configs[2] form: MossTTSDelay bf16, one global batch of {B} synthetic direct prompts "
                         f"(T {int(lens.min())}-{int(lens.max())}, seed 0), global left padding, row-sharded data "
                         f"parallel over {world} GPU(s) via moss_tts_amd.dp.generate_dp (gather + right-pad)",
             "global_batch": B, "per_gpu": per_gpu, "n_gpus": world, "reps": reps,
             "audio_s_per_s": round(audio_s / dt, 3), "audio_s_per_s_per_gpu": round(audio_s / dt / world, 3),
             "ms_per_global_batch": round(dt / reps * 1e3, 2), "frames_per_utt": int(np.median(frames)),
-            "padded_T": int(ids.shape[1])}
+            "padded_T": int(ids.shape[1]),
+            "p50_first_chunk_ms": round(float(p50[0]), 2),
+            "first_chunk_def": (f"per-GPU shard of {hi - lo} rows (max over ranks): prefill + {first_steps - 1} decode "
+                                "steps (first 1 s of audio codes complete), codec excluded")}
 
 
 def forced_schedule(n_steps, n_vq, gen_frames):
@@ -164,58 +190,81 @@ def _torch_cpu_layer(W, h, cos, sin, kc, vc, pos0, n_heads, n_kv, D, eps=1e-6):
     return h + (F.silu(x @ W["g"].T) * (x @ W["u"].T)) @ W["d"].T
 
 
-def cpu_baseline(args, T, n_steps, frames):
+def cpu_baseline(args, T, n_steps, frames, timed_steps=8):
     """A CPU restatement of the decode path at the full 8B shape in bf16 torch-CPU ops (the
     oracle's layer math on torch matmuls, in the reference deployment's dtype: `torch_dtype=bf16`,
-    clis/moss_tts_app.py:95-107) on this host's cores, on a bounded sample: one prefill layer over
-    T tokens, 6 decode layer-steps at the prompt's context and one pass of the 1+32 heads; composed
-    into one utterance (36 layers x (prefill + n_steps decode) + heads per step).  SURVEY.md §6
-    measured the reference's own torch-CPU path at 0.44 s per decode step (0.18 audio-s/s) on the
-    8-core build container; round 3's fp32 form of this port ran 2.7x slower than that (bf16 halves
-    the bytes a CPU GEMV streams: 40 vs 52 GB/s, 5.0 vs 7.8 ms per gate+down pair on the build
-    container's 8 cores)."""
+    clis/moss_tts_app.py:95-107) on this host's cores.  Round 5: WHOLE steps timed end to end -- the
+    33-channel embedding sum, 36 decoder layers with their own KV caches, the final norm, the 1+32
+    heads and the greedy picks -- a full prefill over the T prompt tokens, then `timed_steps` decode
+    steps after one untimed warm-up step; the utterance is prefill + n_steps x the mean step.  (One
+    layer's weights serve all 36 layers: 385 MB per layer does not stay in the host caches, so every
+    layer still streams its bytes from DRAM, and the 14 GB a distinct set would need is not
+    generated.)  SURVEY.md §6 measured the reference's own torch-CPU path at 0.44 s per decode step
+    (0.18 audio-s/s) on the 8-core build container."""
     import torch
     cores = torch.get_num_threads()
-    H, I, D, nh, nkv = 4096, 12288, 128, 32, 8
+    H, I, D, nh, nkv, L, n_vq, V, A = 4096, 12288, 128, 32, 8, 36, 32, 151936, 1025
     g = torch.Generator().manual_seed(0)
-
     bf = torch.bfloat16
 
-    def rnd(*shape):
-        return (torch.randn(*shape, generator=g) * shape[-1] ** -0.5).to(bf)
+    base = torch.empty(1 << 20, dtype=bf).uniform_(-1.0, 1.0, generator=g)
+
+    def rnd(*shape):  # uniform(-1, 1) * sqrt(3 / K) (variance 1 / K): a 1 M-value random block tiled, since
+        # a generator fills ~0.1 G values/s single-threaded and the values do not change the work
+        t = torch.empty(*shape, dtype=bf)
+        flat = t.view(-1)
+        n = flat.numel()
+        full = n // base.numel()
+        if full:
+            flat[:full * base.numel()].view(full, -1).copy_(base.expand(full, -1))
+        flat[full * base.numel():] = base[:n - full * base.numel()]
+        return t.mul_((3.0 / shape[-1]) ** 0.5)
 
     one = lambda n: torch.ones(n, dtype=bf)  # noqa: E731
     W = {"q": rnd(nh * D, H), "k": rnd(nkv * D, H), "v": rnd(nkv * D, H), "o": rnd(H, nh * D), "g": rnd(I, H),
          "u": rnd(I, H), "d": rnd(H, I), "in": one(H), "post": one(H), "qn": one(D), "kn": one(D)}
+    heads = rnd(V + n_vq * A, H)
+    emb_t = rnd(V, H)
+    emb_a = rnd(n_vq, A, H)
     inv = 1.0 / (1e6 ** (torch.arange(0, D, 2, dtype=torch.float32) / D))
-    f = torch.arange(T + 16, dtype=torch.float32)[:, None] * inv[None]
+    C = T + timed_steps + 2
+    f = torch.arange(C, dtype=torch.float32)[:, None] * inv[None]
     cos, sin = torch.cat([f, f], -1).cos().to(bf), torch.cat([f, f], -1).sin().to(bf)
-    kc, vc = torch.zeros(1, nkv, T + 16, D, dtype=bf), torch.zeros(1, nkv, T + 16, D, dtype=bf)
+    kcs = [torch.zeros(1, nkv, C, D, dtype=bf) for _ in range(L)]
+    vcs = [torch.zeros(1, nkv, C, D, dtype=bf) for _ in range(L)]
+    ids = torch.randint(0, 1024, (1, T, n_vq + 1), generator=g)
+
+    def step(ids_s, pos0):
+        S = ids_s.shape[1]
+        h = emb_t[ids_s[..., 0]]
+        for j in range(n_vq):  # the 33-way embedding sum (modeling_moss_tts.py:196-213)
+            h = h + emb_a[j][ids_s[..., j + 1]]
+        for l in range(L):
+            h = _torch_cpu_layer(W, h, cos[pos0:pos0 + S], sin[pos0:pos0 + S], kcs[l], vcs[l], pos0, nh, nkv, D)
+        x = h[:, -1]
+        x = x * torch.rsqrt(x.float().pow(2).mean(-1, keepdim=True) + 1e-6).to(bf)
+        lg = x @ heads.T  # 1 + 32 heads (:279-300)
+        nxt = torch.empty(1, 1, n_vq + 1, dtype=torch.long)
+        nxt[0, 0, 0] = lg[0, :V].argmax()
+        nxt[0, 0, 1:] = lg[0, V:].view(n_vq, A)[:, :A - 1].argmax(-1)
+        return nxt
+
     with torch.inference_mode():
         t0 = time.perf_counter()
-        _torch_cpu_layer(W, torch.randn(1, T, H, generator=g).to(bf), cos[:T], sin[:T], kc, vc, 0, nh, nkv, D)
-        t_prefill_layer = time.perf_counter() - t0
-        nd = 6
-        for s in range(nd + 1):  # the first decode step warms the kernels up (untimed)
-            if s == 1:
-                t0 = time.perf_counter()
-            _torch_cpu_layer(W, torch.randn(1, 1, H, generator=g).to(bf), cos[T + s:T + s + 1], sin[T + s:T + s + 1],
-                             kc, vc, T + s, nh, nkv, D)
-        t_dec_layer = (time.perf_counter() - t0) / nd
-        del W
-        heads = rnd(151936 + 32 * 1025, H)
-        x = torch.randn(1, H, generator=g).to(bf)
+        cur = step(ids, 0)
+        t_prefill = time.perf_counter() - t0
+        cur = step(cur, T)  # warm-up decode step (untimed)
         t0 = time.perf_counter()
-        for _ in range(2):
-            _ = x @ heads.T
-        t_heads = (time.perf_counter() - t0) / 2
-        del heads
-    utt = 36 * (t_prefill_layer + n_steps * t_dec_layer) + (n_steps + 1) * t_heads
+        for s in range(timed_steps):
+            cur = step(cur, T + 1 + s)
+        t_step = (time.perf_counter() - t0) / timed_steps
+    del W, heads, emb_t, emb_a, kcs, vcs
+    utt = t_prefill + n_steps * t_step
     return {"value": round(frames / FRAME_RATE / utt, 5), "unit": "audio-s/s", "cores": int(cores), "kind": "port",
-            "sample": (f"bf16 torch-CPU restatement of the layer math at the 8B shape, batch 1: 1 prefill layer "
-                       f"(T={T}, {t_prefill_layer:.2f}s) + {nd} decode layer-steps ({t_dec_layer * 1e3:.1f}ms each) "
-                       f"+ the 1+32 heads ({t_heads * 1e3:.0f}ms), composed to one utterance of {n_steps} steps = "
-                       f"{utt:.1f}s"),
+            "sample": (f"bf16 torch-CPU restatement of the whole decode path at the 8B shape, batch 1: a full prefill "
+                       f"(36 layers over T={T} tokens + heads, {t_prefill:.2f}s) and {timed_steps} whole decode steps "
+                       f"(embedding sum, 36 layers, norm, 1+32 heads, greedy picks; {t_step * 1e3:.0f}ms each) timed end "
+                       f"to end; one utterance = prefill + {n_steps} steps = {utt:.1f}s"),
             "reference_measured_in_build_container": "SURVEY.md §6: the reference's torch-CPU decode step 0.44 s "
                                                       "(0.18 audio-s/s), 8 cores"}
 
@@ -558,7 +607,9 @@ def main():
     max_b = max([args.batch] + extra)
     prompt_cap = 64 + text_tokens + 2 * n_vq + 64
     ecfg = EngineConfig(layers=args.layers, n_vq=n_vq, max_batch=max_b, max_ctx=prompt_cap + n_steps + 16,
-                        max_prefill_tokens=max(256 * max_b, 256) if args.config == "clone" else 1024)
+                        # TTSD: the whole ~2,100-token script in one prefill chunk, so every weight byte
+                        # streams once (1,024-token chunks streamed the 13.9 GB three times)
+                        max_prefill_tokens=max(256 * max_b, 256) if args.config == "clone" else 4096)
     eng = Engine(ecfg, local)
     eng.init_random(seed=0)
     forced = torch.from_numpy(forced_schedule(n_steps, n_vq, gen_frames)).cuda()
@@ -710,7 +761,9 @@ def main():
             "audio_frames_per_utt": frames0,
             "decode_path": (f"batch {args.batch}: the 36-layer stack as one persistent streaming launch (csrc/"
                             f"{'pse.hip' if args.batch == 1 else 'pse4.hip'}) for steps with context <= "
-                            f"{eng.pse_ctx_max()}, per-op hipGraph launches beyond"
+                            f"{eng.pse_ctx_max()}, "
+                            + ("its long-context (all-CU attention) form beyond"
+                               if args.batch == 1 and eng.pse_long_active() else "per-op hipGraph launches beyond")
                             if (eng.pse_active() and args.batch == 1) or (eng.pse4_active() and args.batch == 4)
                             else "per-op hipGraph launches"),
             "p50_first_chunk_ms": round(p50, 2),

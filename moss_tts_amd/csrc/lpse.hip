@@ -17,10 +17,16 @@
 //
 //  * CU roles.  96 "residual" CUs own one 16-column tile of the depth residual stream each (LH =
 //    1536 = 96 tiles): o_proj and down_proj row tile c, the residual in registers, and the adapter
-//    into the stack (mi down).  The 160 others run gate|up (560 gate/up tile pairs, pair
-//    c - 96 + 160 j in round j) and, for the attention, one unit per (row, KV head) on CUs 96 ...
+//    into the stack (mi down).  The 160 others run gate|up (pair c - 96 + 160 j in round j < 3);
+//    the last 80 of the 560 gate/up tile pairs (round 3) run on residual CUs 0..79, ahead of their
+//    down_proj, and the attention's units (one per row and KV head) on residual CUs 0..8B-1
+//    (round 5: the 160 gate|up CUs were the frame's critical path -- 4 rounds of 6 slots each
+//    after their input arrived, 19 us per layer -- and the attention units sat on them).
 //    Every CU runs one q|k|v row tile (4096 rows = 256 tiles).  Per layer a residual CU streams
-//    3 + 4 + 17.5 slots of 16 KiB, a gate|up CU 3 + 18 (or 24).
+//    3 + 4 (+ 6) + 18 slots of 16 KiB, a gate|up CU 3 + 18.
+//  * While a gate|up CU waits for its post-attention input (the attention and o_proj run
+//    elsewhere) its consumer waves copy its first pair's 6 ring slots into registers as they land
+//    (pse.hip's SlotCache), so the loader streams 6 slots further ahead through that wait.
 //  * Hand-offs.  An op's producers store their outputs write-through (sc1), drain them
 //    (s_waitcnt vmcnt(0)), then bump the op's counter (relaxed, agent scope); a consumer polls the
 //    counter with sc1 loads and reads the data with sc1 loads (cdna_hip_programming.md Guideline
@@ -60,6 +66,9 @@ constexpr int P = 256;
 constexpr int NM = P - NR;              // gate|up CUs
 constexpr int GU_PAIRS = LI / 16, F_PAIRS = F / 16;
 constexpr int ROUND_KT = NM * 16 / 32;  // down k-tiles per act round (80)
+constexpr int R3_PAIRS = LI / 16 - 3 * NM;   // round 3's pairs (80), on residual CUs 0 .. 79
+constexpr int R3_KT0 = 3 * ROUND_KT;         // their down k-tiles 240 .. 279
+constexpr int DOWN_SLOTS_R3 = (KT_LI - R3_KT0 + 15) / 16;  // 3 (the last one half valid)
 constexpr int TILE_E = 512;             // bf16 per 1 KiB weight tile
 static_assert(QKVR / 16 == P && H / 16 == 128 && F_PAIRS == 128, "the 1.7B depth shape on 256 CUs");
 static_assert(KT_LI == 3 * ROUND_KT + 40 && GU_PAIRS == 3 * NM + 80, "down's act rounds");
@@ -102,9 +111,13 @@ constexpr int L_RED = L_X + X_BYTES;           // [CW][2][256] fp32
 constexpr int L_MISC = L_RED + CW * 2 * 256 * 4;  // r_s[NB], sq[NB][16]
 constexpr int L_END = L_MISC + (NB + NB * 16) * 4;
 static_assert(L_END <= 160 * 1024, "LDS");
-// attention scratch over the op-input region (the q|k|v input is consumed): qn [2][D], kn [D],
-// vn [D], p [2][CMAX], l [2] (fp32)
-constexpr int L_AQ = L_X, L_AK = L_AQ + 2 * D * 4, L_AV = L_AK + D * 4, L_AP = L_AV + D * 4, L_AL = L_AP + 2 * CMAX * 4;
+// attention scratch over the op-input region (the q|k|v input is consumed): the cached keys
+// K [AKEYS][D] and values V^T [D][AKEYS] bf16 (prefetched while the q|k|v hand-off is awaited),
+// qn [2][D], kn [D], vn [D], scores [2][CMAX], p [2][CMAX], l [2] (fp32)
+constexpr int AKEYS = 32;  // channel positions before the newest (<= 33 channels per frame)
+constexpr int L_AKC = L_X, L_AVC = L_AKC + AKEYS * D * 2;
+constexpr int L_AQ = L_AVC + D * AKEYS * 2, L_AK = L_AQ + 2 * D * 4, L_AV = L_AK + D * 4, L_AS = L_AV + D * 4,
+              L_AP = L_AS + 2 * CMAX * 4, L_AL = L_AP + 2 * CMAX * 4;
 static_assert(L_AL + 16 <= L_X + X_BYTES, "attention scratch");
 
 extern __shared__ __attribute__((aligned(16))) unsigned char lp_lds[];
@@ -117,7 +130,8 @@ __device__ __forceinline__ const bf16_t* lptr(int l, int k) {
 
 // trace (MTTS_PSE_TRACE=1 engines, scripts/lpse_trace.py): consumer wave 0 per layer -- 0 q|k|v input
 // ready, 1 normed, 2 q|k|v done; attention units 3 start, 4 done; residual CUs 5 o input in, 6 o done,
-// 12-15 down round j input in, 16 down done; gate|up CUs 7 input normed, 8-11 round j done
+// 11 round-3 pair done, 12-15 down round j input in, 16 down done; gate|up CUs 7 input normed, 8-10
+// round j done
 #define LP_STAMP(l, ev)                                                                          \
   do {                                                                                           \
     if (a.trace && x.w == 0 && x.lane == 0)                                                      \
@@ -170,12 +184,17 @@ constexpr int GO_STRIDE = 32;  // words: one 128-byte line per flag
 __device__ __forceinline__ uint32_t* go_flag(const Cx& x, int k, int cu) { return x.go + ((size_t)k * P + cu) * GO_STRIDE; }
 
 // wait until hand-off k is complete (sc1 polls); false on timeout / abort
-__device__ __forceinline__ bool bwait(Cx& x, int k, int target) {
+struct NoPoll {
+  __device__ void operator()() const {}
+};
+template <typename Poll = NoPoll>
+__device__ __forceinline__ bool bwait(Cx& x, int k, int target, const Poll& each_poll = Poll()) {
   for (uint32_t spins = 0; LPSE_GO ? ld32(go_flag(x, k, x.c)) != x.epoch : (int)ld32(x.cnt + k) < target; ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed() || ld32(x.err)))) {
       give_up(x.err, 2);
       return false;
     }
+    each_poll();
     __builtin_amdgcn_s_sleep(1);
   }
   // every later read of the producers' data is an sc1 load: a wavefront-scope fence keeps the
@@ -198,6 +217,11 @@ __device__ __forceinline__ void arrive(Cx& x, int k, int target) {
       for (int i = 0; i < P / 64; ++i) st32(go_flag(x, k, x.lane + 64 * i), x.epoch);
   }
 }
+
+template <bool V>
+struct RoleC {
+  static constexpr bool value = V;
+};
 
 // ---- op input staging: rows [B][K] bf16 -> X [k tile][row][32] ----
 // chunk i (8 columns) of the B x K input: row i / (K/8), columns 8 (i % (K/8)) ..
@@ -320,6 +344,57 @@ __device__ __forceinline__ bool gemv_unit(Cx& x, int& seq, f32x4 (&acc)[NRT]) {
   return true;
 }
 
+// ring slots drained into registers while the consumer waits for an input (pse.hip SlotCache):
+// slots seq0 .. seq0 + RC - 1 in order, each released to the loader once copied
+__device__ __forceinline__ bool slot_ready(int seq) {
+  return __hip_atomic_load(&LP_CTL->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > seq;
+}
+#ifndef LPSE_RC
+#define LPSE_RC 4  // a gate|up CU's ring slots drained into registers during the post-attention wait
+#endif
+template <int RC>
+struct SlotCache {
+  u32x4 rc[RC > 0 ? RC : 1][4];
+  int nd = 0;
+  __device__ __forceinline__ void drain(const Cx& x, int seq0) {
+#pragma unroll
+    for (int k = 0; k < RC; ++k)
+      if (k == nd && slot_ready(seq0 + k)) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const u32x4* sl = reinterpret_cast<const u32x4*>(lp_lds + L_RING + ((seq0 + k) % NS) * SLOT);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) rc[k][i] = sl[(x.w * 4 + i) * 64 + x.lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (x.lane == 0)
+          __hip_atomic_store(&LP_CTL->freed[x.w], seq0 + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ++nd;
+      }
+  }
+};
+// a gate|up pair (2 row tiles x 3 slots) whose first RC slots may sit in a SlotCache (RC 6 spilled 19 VGPRs)
+template <int RC>
+__device__ __forceinline__ bool gu_pair_cached(Cx& x, int& seq, SlotCache<RC>& sc, f32x4 (&acc)[2]) {
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    acc[r] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int k = r * 3 + s;
+      u32x4 t[4];
+      if (k < RC && k < sc.nd) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = sc.rc[k < RC ? k : 0][i];
+        ++seq;
+      } else if (!take4(x, seq++, t)) {
+        return false;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[r] = mfma(t[i], xfrag(x, s * 16 + x.w * 4 + i), acc[r]);
+    }
+  }
+  return true;
+}
+
 // fixed-order reduction of the CW waves' tiles: element t (< 256) of row tile r ->
 // weight row n = 4 ((t >> 2) >> 4) + (t & 3), batch row b = (t >> 2) & 15
 template <int NRT>
@@ -378,16 +453,53 @@ __device__ __forceinline__ float swiglu(float g0, float u0) {
 // q / k RMSNorm (no RoPE: MossTTSLocal's depth transformer, moss_tts_local/modeling_moss_tts.py:
 // 126-176), K / V appended at pos (TF/cache_utils.py:127-145), softmax(q k^T / sqrt(D)) v over
 // positions 0..pos (causal; every channel position is valid), probabilities rounded to bf16
-// before P.V (the reference's bf16 SDPA)
-__device__ __forceinline__ void attention(Cx& x, const LpseArgs& a, int l, int b, int g) {
+// before P.V (the reference's bf16 SDPA).
+// Round 5: the cached keys / values (positions < pos, written by earlier channels' launches) are
+// loaded into registers BEFORE the q|k|v hand-off is awaited (att_prefetch) and land in LDS behind
+// it; scores take 4 lanes per key (32 dims each) instead of one lane per key over all 128 dims.
+struct KVPre {
+  u32x4 k[2], v[2];
+};
+__device__ __forceinline__ bf16_t* att_kc(const LpseArgs& a, int l, int b, int g) {
+  return a.kc + (size_t)l * a.layer_kv + (((size_t)b * HKV + g) * CMAX) * D;  // [CMAX][D]
+}
+__device__ __forceinline__ bf16_t* att_vc(const LpseArgs& a, int l, int b, int g) {
+  return a.vc + (size_t)l * a.layer_kv + (((size_t)b * HKV + g) * D) * CMAX;  // [D][CMAX]
+}
+__device__ __forceinline__ KVPre att_prefetch(const Cx& x, const LpseArgs& a, int l, int b, int g) {
   const int pos = a.pos;
+  constexpr uint32_t OOB = 0x7ffffff0u;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(att_kc(a, l, b, g), 0, CMAX * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(att_vc(a, l, b, g), 0, CMAX * D * 2, 0x00020000);
+  KVPre r;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int i = x.tid + m * CW * 64;  // 16-byte chunk i of K [AKEYS][D] / of V^T's first AKEYS columns
+    const int key = i >> 4;             // K: 16 chunks per key
+    r.k[m] = __builtin_amdgcn_raw_buffer_load_b128(krs, key < pos ? (uint32_t)i * 16u : OOB, 0, 0);
+    const int d = i >> 2, q = i & 3;    // V^T: 4 chunks (32 keys) per dim
+    r.v[m] = __builtin_amdgcn_raw_buffer_load_b128(vrs, q * 8 < pos ? (uint32_t)(d * CMAX + q * 8) * 2u : OOB, 0, 0);
+  }
+  return r;
+}
+__device__ __forceinline__ void attention(Cx& x, const LpseArgs& a, int l, int b, int g, const KVPre& pre) {
+  const int pos = a.pos;
+  bf16_t* Ks = reinterpret_cast<bf16_t*>(lp_lds + L_AKC);  // [AKEYS][D]
+  bf16_t* Vs = reinterpret_cast<bf16_t*>(lp_lds + L_AVC);  // [D][AKEYS]
   float* qn = reinterpret_cast<float*>(lp_lds + L_AQ);
   float* kn = reinterpret_cast<float*>(lp_lds + L_AK);
   float* vn = reinterpret_cast<float*>(lp_lds + L_AV);
+  float* sc = reinterpret_cast<float*>(lp_lds + L_AS);
   float* ps = reinterpret_cast<float*>(lp_lds + L_AP);
   float* ls = reinterpret_cast<float*>(lp_lds + L_AL);
-  bf16_t* kc = a.kc + (size_t)l * a.layer_kv + (((size_t)b * HKV + g) * CMAX) * D;  // [CMAX][D]
-  bf16_t* vc = a.vc + (size_t)l * a.layer_kv + (((size_t)b * HKV + g) * D) * CMAX;  // [D][CMAX]
+  bf16_t* kc = att_kc(a, l, b, g);
+  bf16_t* vc = att_vc(a, l, b, g);
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int i = x.tid + m * CW * 64;
+    reinterpret_cast<u32x4*>(Ks)[i] = pre.k[m];
+    reinterpret_cast<u32x4*>(Vs)[(i >> 2) * (AKEYS / 8) + (i & 3)] = pre.v[m];
+  }
   {
     // wave w: vector w (0, 1: q heads 2g, 2g + 1; 2: k; 3: v), two dims per lane
     const int hd = x.w < 2 ? g * 2 + x.w : (x.w == 2 ? HQ + g : HQ + HKV + g);
@@ -413,27 +525,34 @@ __device__ __forceinline__ void attention(Cx& x, const LpseArgs& a, int l, int b
     }
   }
   cbar(x);
-  if (x.w < 2) {
-    // head x.w: lane j scores key j (keys < pos from the cache, pos = the new key)
-    const int j = x.lane;
+  {
+    // scores: thread -> head h = tid / 128, cached key j = (tid / 4) % 32, dims 32 (tid % 4) ..;
+    // the new key (pos) by the first wave of each head
+    const int h = x.tid >> 7, j = (x.tid >> 2) & (AKEYS - 1), qd = x.tid & 3;
+    const float* q = qn + h * D + qd * 32;
+    const u32x4* kr = reinterpret_cast<const u32x4*>(Ks + j * D + qd * 32);
     float s = 0.f;
-    if (j < pos) {
-      const u32x4* kr = reinterpret_cast<const u32x4*>(kc + (size_t)j * D);
-      const float* q = qn + x.w * D;
-#pragma unroll 4
-      for (int c = 0; c < D / 8; ++c) {
-        const u32x4 kv = kr[c];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          s += q[c * 8 + 2 * e] * __uint_as_float(kv[e] << 16);
-          s += q[c * 8 + 2 * e + 1] * __uint_as_float(kv[e] & 0xffff0000u);
-        }
+    for (int c = 0; c < 4; ++c) {
+      const u32x4 kv = kr[c];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        s += q[c * 8 + 2 * e] * __uint_as_float(kv[e] << 16);
+        s += q[c * 8 + 2 * e + 1] * __uint_as_float(kv[e] & 0xffff0000u);
       }
-    } else if (j == pos) {
-      const float* q = qn + x.w * D;
-      for (int d = 0; d < D; ++d) s += q[d] * kn[d];
     }
-    const float sv = j <= pos ? s * a.scale : -INFINITY;
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if (qd == 0 && j < pos) sc[h * CMAX + j] = s * a.scale;
+    if ((x.w & 1) == 0) {  // waves 0 / 2: the new key of head h
+      const float sn = wave_sum(qn[h * D + 2 * x.lane] * kn[2 * x.lane] + qn[h * D + 2 * x.lane + 1] * kn[2 * x.lane + 1]);
+      if (x.lane == 0) sc[h * CMAX + pos] = sn * a.scale;
+    }
+  }
+  cbar(x);
+  if (x.w < 2) {  // softmax of head w over keys 0..pos (lane = key)
+    const int j = x.lane;
+    const float sv = j <= pos ? sc[x.w * CMAX + j] : -INFINITY;
     const float m = wave_max(sv);
     const float p = j <= pos ? expf(sv - m) : 0.f;
     const float L = wave_sum(p);
@@ -444,10 +563,10 @@ __device__ __forceinline__ void attention(Cx& x, const LpseArgs& a, int l, int b
   {
     // output (head h, dim d) per thread: sum over keys of bf16(p) * v, in key order
     const int h = x.tid >> 7, d = x.tid & (D - 1);
-    const bf16_t* vr = vc + (size_t)d * CMAX;
+    const u32x4* vr = reinterpret_cast<const u32x4*>(Vs + d * AKEYS);
     float o = 0.f;
     for (int j0 = 0; j0 < pos; j0 += 8) {
-      const u32x4 v8 = *reinterpret_cast<const u32x4*>(vr + j0);
+      const u32x4 v8 = vr[j0 >> 3];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int j = j0 + 2 * e;
@@ -545,12 +664,14 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
       seg(lptr(l, P_QKV) + (size_t)c * KT_LH * TILE_E, 1ll << 40, KT_LH / 16);
       if (resid) {
         seg(lptr(l, P_O) + (size_t)c * KT_AT * TILE_E, 1ll << 40, KT_AT / 16);
-        seg(lptr(l, P_DOWN) + (size_t)c * KT_LI * TILE_E, (long long)(NR - c) * KT_LI * 1024, (KT_LI + 15) / 16);
+        // round 3's gate|up pair, then down_proj: round 3's k-tiles (240 .. 279: 2.5 slots, the
+        // last one half valid) first -- this CU group produces them -- then rounds 0-2 (0 .. 239)
+        if (c < R3_PAIRS) seg(lptr(l, P_GU) + (size_t)(3 * NM + c) * 2 * KT_LH * TILE_E, 1ll << 40, 2 * KT_LH / 16);
+        const bf16_t* dn = lptr(l, P_DOWN) + (size_t)c * KT_LI * TILE_E;
+        seg(dn + (size_t)R3_KT0 * TILE_E, (long long)(KT_LI - R3_KT0) * 1024, DOWN_SLOTS_R3);
+        seg(dn, (long long)R3_KT0 * 1024, R3_KT0 / 16);
       } else {
-        for (int j = 0; j < 4; ++j) {
-          const int p = c - NR + NM * j;
-          if (p < GU_PAIRS) seg(lptr(l, P_GU) + (size_t)p * 2 * KT_LH * TILE_E, 1ll << 40, 2 * KT_LH / 16);
-        }
+        for (int j = 0; j < 3; ++j) seg(lptr(l, P_GU) + (size_t)(c - NR + NM * j) * 2 * KT_LH * TILE_E, 1ll << 40, 2 * KT_LH / 16);
       }
     }
     // the adapter out: gate|up pairs on CUs 128 .., down row tiles on CUs .. 127
@@ -584,6 +705,12 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
       resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);  // res = 0: bf16(0 + bf16(y)) = bf16(y)
       arrive(x, C_MIDOWN, NR);
     }
+    // the layer loop instantiated per role (residual / gate|up CU), so that one role's registers
+    // (the gate|up CUs' drained slots, the residual CUs' down fragments) do not shape the other's
+    // allocation; attention unit (row b, KV head g) on residual CU 8 b + g
+    const bool att = resid && c < HKV * a.B;
+    auto layers = [&](auto role) __attribute__((always_inline)) {
+    constexpr bool R = decltype(role)::value;
     for (int l = 0; l < L && ok; ++l) {
       // ---- input RMSNorm + q|k|v: row tile c ----
       ok = bwait(x, l == 0 ? C_MIDOWN : c_layer(l - 1, 7), NR);
@@ -598,31 +725,46 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
         arrive(x, c_layer(l, 0), P);
         LP_STAMP(l, 2);
       }
-      // ---- attention: unit (row b, KV head g) on CU NR + 8 b + g ----
-      const int u = c - NR;
-      if (!resid && u < HKV * a.B && ok) {
-        ok = bwait(x, c_layer(l, 0), P);
-        LP_STAMP(l, 3);
-        if (ok) attention(x, a, l, u >> 3, u & 7);
-        arrive(x, c_layer(l, 1), HKV * a.B);
-        LP_STAMP(l, 4);
-      }
-      if (resid) {
+      if constexpr (R) {
+        // ---- attention (cached K / V loaded ahead of the q|k|v hand-off) ----
+        if (att && ok) {
+          const KVPre pre = att_prefetch(x, a, l, c >> 3, c & 7);
+          ok = bwait(x, c_layer(l, 0), P);
+          LP_STAMP(l, 3);
+          if (ok) attention(x, a, l, c >> 3, c & 7, pre);
+          arrive(x, c_layer(l, 1), HKV * a.B);
+          LP_STAMP(l, 4);
+        }
         // ---- o_proj + residual: row tile c ----
         ok = ok && bwait(x, c_layer(l, 1), HKV * a.B);
         stage_plain<HQ * D>(x, [&](int b) { return a.attnb + (size_t)b * HQ * D; });
         LP_STAMP(l, 5);
-        f32x4 acc[1];
-        ok = ok && gemv_unit<1, KT_AT / 16, KT_AT>(x, seq, acc);
-        red_put<1>(x, acc);
-        resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);
-        arrive(x, c_layer(l, 2), NR);
-        LP_STAMP(l, 6);
-        // ---- down_proj + residual: row tile c, its input in 4 rounds of gate|up output ----
+        {
+          f32x4 acc[1];
+          ok = ok && gemv_unit<1, KT_AT / 16, KT_AT>(x, seq, acc);
+          red_put<1>(x, acc);
+          resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);
+          arrive(x, c_layer(l, 2), NR);
+          LP_STAMP(l, 6);
+        }
+        // ---- round 3 of gate|up (pairs 480 + c, c < 80): post-attention RMSNorm + SwiGLU ----
+        if (c < R3_PAIRS) {
+          ok = ok && bwait(x, c_layer(l, 2), NR);
+          stage_norm(x, a.h, a.ss, lptr(l, P_POSTN));
+          f32x4 acc[2];
+          ok = ok && gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
+          red_put<2>(x, acc);
+          put_pair(x, a.act, LI, (3 * NM + c) * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
+          arrive(x, c_layer(l, 6), R3_PAIRS);
+          LP_STAMP(l, 11);
+        }
+        // ---- down_proj + residual: row tile c, its input in rounds 3, 0, 1, 2 of gate|up output ----
         f32x4 dacc = (f32x4){0.f, 0.f, 0.f, 0.f};
-        for (int j = 0; j < 4 && ok; ++j) {
-          ok = bwait(x, c_layer(l, 3 + j), j < 3 ? NM : GU_PAIRS - 3 * NM);
+        for (int jj = 0; jj < 4 && ok; ++jj) {
+          const int j = jj == 0 ? 3 : jj - 1;
+          ok = bwait(x, c_layer(l, 3 + j), j < 3 ? NM : R3_PAIRS);
           LP_STAMP(l, 12 + j);
+          const int kt0 = j < 3 ? j * ROUND_KT : R3_KT0, nsl = j < 3 ? ROUND_KT / 16 : DOWN_SLOTS_R3;
           // this wave's B fragments of the round's (up to) 5 slots, straight from act (sc1)
           const int b = x.lane & 15;
           const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(a.act, 0, NB * LI * 2, 0x00020000);
@@ -631,13 +773,14 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
           for (int s5 = 0; s5 < 5; ++s5)
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
-              const int kt = (5 * j + s5) * 16 + x.w * 4 + i;
+              const int kt = kt0 + s5 * 16 + x.w * 4 + i;
               fr[s5][i] = __builtin_amdgcn_raw_buffer_load_b128(
-                  rs, (b < x.B && kt < KT_LI) ? (uint32_t)(b * LI + kt * 32 + 8 * (x.lane >> 4)) * 2u : 0x7ffffff0u, 0, 16);
+                  rs, (b < x.B && s5 < nsl && kt < KT_LI) ? (uint32_t)(b * LI + kt * 32 + 8 * (x.lane >> 4)) * 2u : 0x7ffffff0u,
+                  0, 16);
             }
 #pragma unroll
           for (int s5 = 0; s5 < 5; ++s5) {
-            if (5 * j + s5 >= (KT_LI + 15) / 16) break;
+            if (s5 >= nsl) break;
             u32x4 t[4];
             if (!take4(x, seq++, t)) {
               ok = false;
@@ -645,7 +788,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
             }
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              if ((5 * j + s5) * 16 + x.w * 4 + i < KT_LI) dacc = mfma(t[i], fr[s5][i], dacc);
+              if (kt0 + s5 * 16 + x.w * 4 + i < KT_LI) dacc = mfma(t[i], fr[s5][i], dacc);
           }
         }
         f32x4 acc1[1] = {dacc};
@@ -654,22 +797,27 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
         arrive(x, c_layer(l, 7), NR);
         LP_STAMP(l, 16);
       } else {
-        // ---- post-attention RMSNorm + gate|up + SwiGLU: pairs c - NR + 160 j (round j) ----
-        ok = ok && bwait(x, c_layer(l, 2), NR);
+        // ---- post-attention RMSNorm + gate|up + SwiGLU: pairs c - NR + 160 j (rounds 0-2) ----
+        // (the first pair's 6 slots drain into registers through the wait)
+        SlotCache<LPSE_RC> sc;
+        const int seq0 = seq;
+        ok = ok && bwait(x, c_layer(l, 2), NR, [&]() { sc.drain(x, seq0); });
         stage_norm(x, a.h, a.ss, lptr(l, P_POSTN));
         LP_STAMP(l, 7);
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < 3 && ok; ++j) {
           const int p = c - NR + NM * j;
-          if (p >= GU_PAIRS) break;
           f32x4 acc[2];
-          ok = ok && gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
+          ok = j == 0 ? gu_pair_cached(x, seq, sc, acc) : gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
           red_put<2>(x, acc);
           put_pair(x, a.act, LI, p * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-          arrive(x, c_layer(l, 3 + j), j < 3 ? NM : GU_PAIRS - 3 * NM);
+          arrive(x, c_layer(l, 3 + j), NM);
           LP_STAMP(l, 8 + j);
         }
       }
     }
+    };
+    if (resid) layers(RoleC<true>{});
+    else layers(RoleC<false>{});
     // ---- local_transformer.norm + local_to_speech_embedding_mlps[i] (:402-406) ----
     if (ok && c >= 128) {
       ok = bwait(x, c_layer(L - 1, 7), NR);

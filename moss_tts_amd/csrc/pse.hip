@@ -73,6 +73,11 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_RC
 #define PSE_RC 6  // ring slots a plain CU's consumer waves drain into registers during the attention wait
 #endif
+// PSE_OGRP: o_proj slot k (the 512 attention columns of KV head k) starts once that head's units
+// have published, instead of after the whole attention output (pse4.hip PSE4_OGRP)
+#ifndef PSE_OGRP
+#define PSE_OGRP 0
+#endif
 #ifndef PSE_TRACE2
 #define PSE_TRACE2 0  // (diagnostic: the input-norm h gather's own stamps replace the loader's)
 #endif
@@ -1342,6 +1347,35 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         // ---------------- o_proj (+ residual) ----------------
         // (plain CUs: the o_proj slots drain into registers while the attention runs elsewhere)
         SlotCache<RC> co;
+        if (PSE_OGRP) {
+          constexpr int NGG = HQ_ * D_ / 2 / HKV_;  // one granule per consumer thread
+          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+          bool ok = true;
+          auto grp = [&](int k) {
+            return gather<1, false>(x, a.g_att + (size_t)k * NGG, NGG, tagof(epoch, l, OP_ATT), xs32 + k * NGG, NGG,
+                                    nullptr, NoHook(), [&]() {
+                                      if (k == 0) co.drain(x, seq);
+                                    });
+          };
+#pragma unroll
+          for (int k = 0; k < RC; ++k) {
+            ok = ok && grp(k);
+            if (ok) co.take(x, seq, k, k * 16, acc);
+          }
+#pragma unroll 1
+          for (int k = RC; k < HKV_ && ok; ++k) {
+            ok = grp(k);
+            if (ok) consume_slot(x, seq++, k * 16, acc);
+          }
+          if (!ok) break;
+          if (wave == LW) PSE_STAMP(l, 4);
+          PSE_PRIO_UP();
+          red_put(x, 0, acc);
+          cbar(x);
+          emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f, l);
+          cbar(x);
+          PSE_PRIO_DOWN();
+        } else {
         if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr, NoHook(),
                               [&]() { co.drain(x, seq); }))
           break;
@@ -1358,6 +1392,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f, l);
           cbar(x);
           PSE_PRIO_DOWN();
+        }
         }
         if (wave == LW) PSE_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------

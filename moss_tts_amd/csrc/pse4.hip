@@ -52,6 +52,11 @@ constexpr int THREADS = (LW + CW) * 64;
 #define PSE4_ATTF 0
 #endif
 #define P4_AFLAG (PSE4_HCNT == 2 && PSE4_ATTF)
+// PSE4_OGRP: o_proj slot k (k tiles 16k .. 16k + 15 = the 512 attention columns of KV head k) starts
+// once head k's 4 units (one per row) have published, instead of after the whole attention output
+#ifndef PSE4_OGRP
+#define PSE4_OGRP 1
+#endif
 constexpr int NS = PSE4_NS;
 constexpr int SLOT_KB = 16;
 constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
@@ -892,6 +897,39 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         }
         // ---------------- o_proj (+ residual) ----------------
         SlotCache<RC> co;
+        if (PSE4_OGRP && !P4_AFLAG) {
+          // per KV-head group: gather head k's 512 columns of the 4 rows (1,024 granules, contiguous in
+          // the [k tile][row][16] layout), then run o_proj slot k on them; the ring slots drain into
+          // registers only while the first group is awaited (SlotCache counts from a fixed seq)
+          constexpr int NGG = NG_ATT / HKV_;
+          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
+          bool ok = true;
+          auto grp = [&](int k) {
+            return gather<NGG / (CW * 64)>(x, a.g_att + (size_t)k * NGG, NGG, tagof(epoch, l, OP_ATT), xa32 + k * NGG,
+                                           NGG, nullptr, NoHook(), [&]() {
+                                             if (k == 0) co.drain(x, seq);
+                                           });
+          };
+          // (the register-drained slots first, at compile-time indices)
+#pragma unroll
+          for (int k = 0; k < RC; ++k) {
+            ok = ok && grp(k);
+            if (ok) co.take(x, seq, k, L_XA, k * 16, acc);
+          }
+#pragma unroll 1
+          for (int k = RC; k < HKV_ && ok; ++k) {
+            ok = grp(k);
+            if (ok) consume_slot(x, seq++, L_XA, k * 16, acc);
+          }
+          if (!ok) break;
+          if (wave == LW) P4_STAMP(l, 4);
+          __builtin_amdgcn_s_setprio(3);
+          red_put(x, 0, acc);
+          cbar(x);
+          emit_h(a.g_h[0], tagof(epoch, l, OP_O), red_get(0, ecol, erow), l * 2);
+          cbar(x);
+          __builtin_amdgcn_s_setprio(0);
+        } else {
         if (P4_AFLAG) {
           if (!hgather(x, a.hcnt, a.go, 2 * PSE_MAXL + l, HKV_ * NB, reinterpret_cast<const bf16_t*>(a.g_att), nullptr, xa32,
                        nullptr, NoHook(), [&]() { co.drain(x, seq); }))
@@ -913,6 +951,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           emit_h(a.g_h[0], tagof(epoch, l, OP_O), red_get(0, ecol, erow), l * 2);
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
+        }
         }
         if (wave == LW) P4_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------

@@ -193,3 +193,55 @@ def test_pse_greedy_trajectory_vs_oracle(setup):
         mk = np.concatenate([mk, (~st["is_stopping"])[:, None]], axis=1)
         gen = np.concatenate([gen, cur], axis=1)
     assert out.shape[1] == T + steps
+
+
+@pytest.fixture(scope="module")
+def setup_coop(setup):
+    """the same weights on an engine that launches the persistent kernel cooperatively
+    (MTTS_PSE_COOP=1, hipLaunchCooperativeKernel: the runtime refuses a grid whose workgroups
+    cannot all be resident instead of relying on the bounded waits)"""
+    from moss_tts_amd.engine import Engine, EngineConfig
+    os.environ.update(MTTS_PSE="1", MTTS_PSE_CTX=str(1 << 20), MTTS_PSE_COOP="1")
+    try:
+        eng = Engine(EngineConfig(layers=LAYERS, max_batch=1, max_ctx=768, max_prefill_tokens=1024), 0)
+    finally:
+        for k in ("MTTS_PSE", "MTTS_PSE_CTX", "MTTS_PSE_COOP"):
+            os.environ.pop(k)
+    eng.load_state_dict(weights_on_device(11))
+    torch.cuda.empty_cache()
+    yield eng, setup[0], setup[1]
+    eng.close()
+
+
+def test_pse_cooperative_launch(setup_coop):
+    """the cooperative launch of the batch-1 persistent kernel, teacher-forced
+    against the oracle (T=150, as test_pse_decode_logits_vs_oracle) and bit-identical to the
+    ordinary launch; then generate() (the launch captured into the step's hipGraph) gives the
+    ordinary launch's ids."""
+    from moss_tts_amd.engine import sampling_params
+    coop, eng, M = setup_coop
+    T, steps = 150, 4
+    ids, mask = prompt(T, steps, T, 0)
+    ctx = O._Ctx("bf16")
+    cache = O.KVCache(LAYERS)
+    M.step(ctx, ids[:, :T], mask[:, :T], cache)
+    for e in (coop, eng):
+        e.forward(torch.from_numpy(ids[:, :T].copy()), torch.from_numpy(mask[:, :T]), 0)
+    for s in range(steps):
+        p = T + s
+        text, audio = M.step(ctx, ids[:, p:p + 1], mask[:, :p + 1], cache)
+        lc, lo = [e.forward(torch.from_numpy(ids[:, p:p + 1].copy()), torch.from_numpy(mask[:, :p + 1]), p)
+                  .float().cpu().numpy()[0] for e in (coop, eng)]
+        assert np.array_equal(lc, lo), s
+        band(lc[M.sel], text, (T, s, "text"))
+        for j in range(CFG.n_vq):
+            band(lc[V + j * A:V + (j + 1) * A], audio[j], (T, s, j))
+    assert coop.pse_active()
+    gp, gm = prompt(120, 0, 23)
+    gp[0, -1, 0] = CFG.audio_start_token_id
+    forced = torch.full((24,), CFG.audio_assistant_gen_slot_token_id, dtype=torch.int32)
+    sp = sampling_params(text_temperature=0, audio_temperature=0)
+    a, b = [e.generate_ids(torch.from_numpy(gp), torch.from_numpy(gm.astype(bool)), 24, sp, forced_text=forced)
+            .cpu().numpy() for e in (coop, eng)]
+    assert np.array_equal(a, b)
+    assert coop.pse_active()
