@@ -203,14 +203,41 @@ __device__ __forceinline__ bool bwait(Cx& x, int k, int target, const Poll& each
   return !failed();
 }
 
-// this workgroup's outputs of hand-off k are stored (write-through): drain, barrier, one arrival;
-// the arrival that completes it releases every consumer CU's flag
-__device__ __forceinline__ void arrive(Cx& x, int k, int target) {
+// LPSE_HTREE: a hand-off's arrivals (the producers: CUs lo .. hi - 1) counted in two levels -- a
+// counter per group of 32 CUs (its own 128-byte line), whose completing arrival bumps the hand-off's
+// counter -- instead of up to 256 agent-scope atomics queueing on one line (pse4.hip PSE4_HTREE)
+#ifndef LPSE_HTREE
+#define LPSE_HTREE 1
+#endif
+constexpr int AGRP = 32;                 // CUs per arrival group
+constexpr int NGRP = P / AGRP;
+constexpr int GC_STRIDE = 32;            // ints per group counter line
+// workspace (bytes): counters [N_CNT] at 0, the error word and epoch behind them, the release flags
+// from WS_GO, the group counters [N_CNT][NGRP] lines behind the flags
+constexpr size_t WS_GO = 512;
+constexpr size_t WS_GC = WS_GO + (size_t)N_CNT * P * GO_STRIDE * 4;
+__device__ __forceinline__ int* grp_cnt(const Cx& x, int k, int g) {
+  return x.cnt + WS_GC / 4 + ((size_t)k * NGRP + g) * GC_STRIDE;
+}
+
+// this workgroup's outputs of hand-off k are stored (write-through): drain, barrier, one arrival
+// (producers: CUs lo .. hi - 1); the arrival that completes it releases every consumer CU's flag
+__device__ __forceinline__ void arrive(Cx& x, int k, int lo, int hi) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   cbar(x);
   if (x.w == 0) {
-    int t = 0;
-    if (x.lane == 0) t = __hip_atomic_fetch_add((gi32*)(x.cnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int t = 0, target = hi - lo;
+    if (LPSE_HTREE && LPSE_GO) {
+      const int g = x.c / AGRP;
+      const int in_g = min(hi, (g + 1) * AGRP) - max(lo, g * AGRP);
+      target = (hi - 1) / AGRP - lo / AGRP + 1;  // groups with producers
+      if (x.lane == 0) {
+        t = __hip_atomic_fetch_add((gi32*)grp_cnt(x, k, g), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        t = t == in_g - 1 ? __hip_atomic_fetch_add((gi32*)(x.cnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
+      }
+    } else if (x.lane == 0) {
+      t = __hip_atomic_fetch_add((gi32*)(x.cnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     t = __shfl(t, 0, 64);
     if (LPSE_GO && t == target - 1)
 #pragma unroll
@@ -694,7 +721,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
       ok = gemv_unit<2, KT_H / 16, KT_H>(x, seq, acc);
       red_put<2>(x, acc);
       put_pair(x, a.actF, F, p * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-      arrive(x, C_MIGU, F_PAIRS);
+      arrive(x, C_MIGU, NR, NR + F_PAIRS);
     }
     if (resid && ok) {
       ok = bwait(x, C_MIGU, F_PAIRS);
@@ -703,7 +730,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
       ok = ok && gemv_unit<1, KT_F / 16, KT_F>(x, seq, acc);
       red_put<1>(x, acc);
       resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);  // res = 0: bf16(0 + bf16(y)) = bf16(y)
-      arrive(x, C_MIDOWN, NR);
+      arrive(x, C_MIDOWN, 0, NR);
     }
     // the layer loop instantiated per role (residual / gate|up CU), so that one role's registers
     // (the gate|up CUs' drained slots, the residual CUs' down fragments) do not shape the other's
@@ -722,7 +749,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
         ok = ok && gemv_unit<1, KT_LH / 16, KT_LH>(x, seq, acc);
         red_put<1>(x, acc);
         put_pair(x, a.qkvb, QKVR, c * 16 + el_n(x.tid), rbf(red_get(x, 0)));
-        arrive(x, c_layer(l, 0), P);
+        arrive(x, c_layer(l, 0), 0, P);
         LP_STAMP(l, 2);
       }
       if constexpr (R) {
@@ -732,7 +759,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
           ok = bwait(x, c_layer(l, 0), P);
           LP_STAMP(l, 3);
           if (ok) attention(x, a, l, c >> 3, c & 7, pre);
-          arrive(x, c_layer(l, 1), HKV * a.B);
+          arrive(x, c_layer(l, 1), 0, HKV * a.B);
           LP_STAMP(l, 4);
         }
         // ---- o_proj + residual: row tile c ----
@@ -744,7 +771,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
           ok = ok && gemv_unit<1, KT_AT / 16, KT_AT>(x, seq, acc);
           red_put<1>(x, acc);
           resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);
-          arrive(x, c_layer(l, 2), NR);
+          arrive(x, c_layer(l, 2), 0, NR);
           LP_STAMP(l, 6);
         }
         // ---- round 3 of gate|up (pairs 480 + c, c < 80): post-attention RMSNorm + SwiGLU ----
@@ -755,7 +782,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
           ok = ok && gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
           red_put<2>(x, acc);
           put_pair(x, a.act, LI, (3 * NM + c) * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-          arrive(x, c_layer(l, 6), R3_PAIRS);
+          arrive(x, c_layer(l, 6), 0, R3_PAIRS);
           LP_STAMP(l, 11);
         }
         // ---- down_proj + residual: row tile c, its input in rounds 3, 0, 1, 2 of gate|up output ----
@@ -794,7 +821,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
         f32x4 acc1[1] = {dacc};
         red_put<1>(x, acc1);
         resadd_out(x, red_get(x, 0), hres, a.h, a.ss, c);
-        arrive(x, c_layer(l, 7), NR);
+        arrive(x, c_layer(l, 7), 0, NR);
         LP_STAMP(l, 16);
       } else {
         // ---- post-attention RMSNorm + gate|up + SwiGLU: pairs c - NR + 160 j (rounds 0-2) ----
@@ -810,7 +837,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
           ok = j == 0 ? gu_pair_cached(x, seq, sc, acc) : gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
           red_put<2>(x, acc);
           put_pair(x, a.act, LI, p * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-          arrive(x, c_layer(l, 3 + j), NM);
+          arrive(x, c_layer(l, 3 + j), NR, P);
           LP_STAMP(l, 8 + j);
         }
       }
@@ -826,7 +853,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
       ok = ok && gemv_unit<2, KT_LH / 16, KT_LH>(x, seq, acc);
       red_put<2>(x, acc);
       put_pair(x, a.actF, F, (c - 128) * 16 + el_n(x.tid), swiglu(red_get(x, 0), red_get(x, 1)));
-      arrive(x, C_MOGU_BASE + 8 * L, F_PAIRS);
+      arrive(x, C_MOGU_BASE + 8 * L, 128, P);
     } else if (ok) {
       ok = bwait(x, C_MOGU_BASE + 8 * L, F_PAIRS);
       stage_plain<F>(x, [&](int b) { return a.actF + (size_t)b * F; });
@@ -844,6 +871,7 @@ __global__ __launch_bounds__(THREADS) void lpse_kernel(LpseArgs a) {
     const int t = __hip_atomic_fetch_add((gi32*)(a.cnt + C_EXIT), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t == P - 1) {
       for (int k = 0; k < N_CNT; ++k) st32(a.cnt + k, 0u);
+      for (int k = 0; k < N_CNT * NGRP; ++k) st32(a.cnt + WS_GC / 4 + (size_t)k * GC_STRIDE, 0u);
       st32(a.epoch, epoch);
     }
   }
@@ -866,8 +894,7 @@ bool lpse_supported(int device, int B, int layers, int LH_, int Hq, int Hkv, int
 }
 
 // counters [N_CNT], error word, epoch, then the release flags [N_CNT][P] lines
-constexpr size_t WS_GO = 512;
-size_t lpse_ws_bytes() { return WS_GO + (size_t)N_CNT * P * GO_STRIDE * 4; }
+size_t lpse_ws_bytes() { return WS_GC + (size_t)N_CNT * NGRP * GC_STRIDE * 4; }
 
 hipError_t lpse_channel(const LpseArgs& a0, void* ws, hipStream_t s) {
   if (a0.layers < 1 || a0.layers > LPSE_MAXL || a0.B < 1 || a0.B > NB || a0.pos < 0 || a0.pos >= CMAX)

@@ -73,11 +73,6 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_RC
 #define PSE_RC 6  // ring slots a plain CU's consumer waves drain into registers during the attention wait
 #endif
-// PSE_OGRP: o_proj slot k (the 512 attention columns of KV head k) starts once that head's units
-// have published, instead of after the whole attention output (pse4.hip PSE4_OGRP)
-#ifndef PSE_OGRP
-#define PSE_OGRP 0
-#endif
 #ifndef PSE_TRACE2
 #define PSE_TRACE2 0  // (diagnostic: the input-norm h gather's own stamps replace the loader's)
 #endif
@@ -88,6 +83,12 @@ constexpr int THREADS = (LW + CW) * 64;
 // sums of squares in one round of 16-byte sc1 loads and normalises them (no consumer barrier)
 #define PSE_HCNT 0
 #endif
+// PSE_HTREE (with PSE_HCNT): the 256 arrivals counted in two levels, 8 group counters (32 CUs each,
+// one 128-byte line each) whose completing arrival bumps the hand-off's counter (pse4.hip PSE4_HTREE)
+#ifndef PSE_HTREE
+#define PSE_HTREE 1
+#endif
+constexpr int HGRP = 8, GCNT_STRIDE = 32;
 #ifndef PSE_LONG_RESUME
 // long form: every CU's loader pauses while its slice reads K / V (the reads would queue behind the
 // weight fills); 1: it resumes as soon as the slice's chunks are scored (the partial hop, the merge
@@ -180,6 +181,9 @@ constexpr int L_XS = L_RING + NS * SLOT_KB * 1024;  // op input: 12288 bf16
 constexpr int L_RED = L_XS + I_ * 2;                // [CW][2][16] fp32: column 0 of the partial tiles
 constexpr int L_MISC = L_RED + CW * 2 * 16 * 4;     // [256] gathered sums of squares
 constexpr int PSE_MAXL = 64;                        // layers (weight pointer table in LDS)
+// counters (ints from a.hcnt): [2 PSE_MAXL] hand-off counters, the release flags (PSE_HCNT 2), then
+// the group counters (PSE_HTREE)
+constexpr size_t HCNT_GC_OFF = (2 * PSE_MAXL * 4 + (PSE_HCNT == 2 ? (size_t)2 * PSE_MAXL * 256 * 128 : 0)) / 4;
 constexpr int L_PTR = L_MISC + 1024;
 constexpr int L_END = L_PTR + PSE_MAXL * 4 * 8;
 // the attention CUs' scratch overlays the op input (q|k|v's input is dead once its slots are
@@ -417,7 +421,8 @@ __device__ __forceinline__ bool hnorm_counter(Ctx& x, const int* hcnt, const uin
   hook();
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);
   // (PSE_HCNT 2: this CU's own release flag line; 1: the counter line every consumer wave polls)
-  for (uint32_t spins = 0; PSE_HCNT == 2 ? ld32(go + ((size_t)k * 256 + x.c) * 32) != x.epoch : (int)ld32(hcnt + k) < 256;
+  for (uint32_t spins = 0;
+       PSE_HCNT == 2 ? ld32(go + ((size_t)k * 256 + x.c) * 32) != x.epoch : (int)ld32(hcnt + k) < (PSE_HTREE ? HGRP : 256);
        ++spins) {
     if (spins > SPIN_MEM || ((spins & 255) == 255 && (failed(x) || ld32(x.err)))) {
       give_up(x, 2);
@@ -1248,10 +1253,21 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           if (lane < 16 && (lane & 1) == 0) st32(reinterpret_cast<bf16_t*>(a.g_h[which]) + c * 16 + lane, pack2(hv, hn));
           if (lane == 0) st32(reinterpret_cast<float*>(a.g_ss[which]) + c, __float_as_uint(s16));
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          typedef __attribute__((address_space(1))) int gi;
           int t = 0;
-          if (lane == 0)
-            t = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(a.hcnt + l * 2 + which), 1, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+          if (lane == 0) {
+            if (PSE_HTREE) {
+              int* gc = a.hcnt + HCNT_GC_OFF + ((size_t)(l * 2 + which) * HGRP + c / (256 / HGRP)) * GCNT_STRIDE;
+              t = __hip_atomic_fetch_add((gi*)gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              // the group's last arrival bumps the counter: 8 of them complete it (t = 255 - (8 - 1 - t'))
+              t = t == 256 / HGRP - 1
+                      ? __hip_atomic_fetch_add((gi*)(a.hcnt + l * 2 + which), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) +
+                            256 - HGRP
+                      : -1;
+            } else {
+              t = __hip_atomic_fetch_add((gi*)(a.hcnt + l * 2 + which), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
           t = __shfl(t, 0, 64);
           if (PSE_HCNT == 2 && t == 255)  // the last producer releases every consumer CU's flag line
 #pragma unroll
@@ -1347,35 +1363,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         // ---------------- o_proj (+ residual) ----------------
         // (plain CUs: the o_proj slots drain into registers while the attention runs elsewhere)
         SlotCache<RC> co;
-        if (PSE_OGRP) {
-          constexpr int NGG = HQ_ * D_ / 2 / HKV_;  // one granule per consumer thread
-          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-          bool ok = true;
-          auto grp = [&](int k) {
-            return gather<1, false>(x, a.g_att + (size_t)k * NGG, NGG, tagof(epoch, l, OP_ATT), xs32 + k * NGG, NGG,
-                                    nullptr, NoHook(), [&]() {
-                                      if (k == 0) co.drain(x, seq);
-                                    });
-          };
-#pragma unroll
-          for (int k = 0; k < RC; ++k) {
-            ok = ok && grp(k);
-            if (ok) co.take(x, seq, k, k * 16, acc);
-          }
-#pragma unroll 1
-          for (int k = RC; k < HKV_ && ok; ++k) {
-            ok = grp(k);
-            if (ok) consume_slot(x, seq++, k * 16, acc);
-          }
-          if (!ok) break;
-          if (wave == LW) PSE_STAMP(l, 4);
-          PSE_PRIO_UP();
-          red_put(x, 0, acc);
-          cbar(x);
-          emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f, l);
-          cbar(x);
-          PSE_PRIO_DOWN();
-        } else {
         if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr, NoHook(),
                               [&]() { co.drain(x, seq); }))
           break;
@@ -1392,7 +1379,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
           emit_h(0, tagof(epoch, l, OP_O), lane < 16 ? red_get(x, 0, lane) : 0.f, l);
           cbar(x);
           PSE_PRIO_DOWN();
-        }
         }
         if (wave == LW) PSE_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
@@ -1486,6 +1472,8 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
     if (t == (uint32_t)P - 1) {
       if (PSE_HCNT)
         for (int k = 0; k < 2 * a.layers; ++k) st32(a.hcnt + k, 0u);
+      if (PSE_HCNT && PSE_HTREE)
+        for (int k = 0; k < 2 * a.layers * HGRP; ++k) st32(a.hcnt + HCNT_GC_OFF + (size_t)k * GCNT_STRIDE, 0u);
       st32(a.exit_cnt, 0u);
       st32(a.epoch, epoch);
     }
@@ -1515,8 +1503,8 @@ int pse_grid(int device) {
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + 2 * PSE_MAXL * 4 +
-         (PSE_HCNT == 2 ? (size_t)2 * PSE_MAXL * 256 * 128 : 0) + 64;
+  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + HCNT_GC_OFF * 4 +
+         (PSE_HCNT && PSE_HTREE ? (size_t)2 * PSE_MAXL * HGRP * GCNT_STRIDE * 4 : 0) + 64;
 }
 
 hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, bool long_ctx) {

@@ -36,6 +36,13 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE4_RC
 #define PSE4_RC 2  // ring slots a plain CU's consumer waves drain into registers during the attention wait
 #endif
+// PSE4_LC: after those, ring slots drained into region B (free from the previous layer's down_proj
+// until this layer's SwiGLU rounds: 2 slots of 16 KiB), so the loader runs RC + LC slots further
+// ahead through the attention wait (a register drain past 2 slots spills: 16 / 27 VGPRs at 3 / 4)
+#ifndef PSE4_LC
+#define PSE4_LC 0
+#endif
+static_assert(PSE4_LC >= 0 && PSE4_LC <= 2, "region B holds two slots");
 // PSE4_HCNT: the residual hand-offs (h after o_proj / down, 9,216 tagged granules per consumer CU)
 // as counter + bulk load -- producers store the bf16 rows write-through and bump a per-layer counter,
 // consumers poll it and then load the 32 KiB of rows + sums of squares in one round of 16-byte sc1
@@ -52,11 +59,14 @@ constexpr int THREADS = (LW + CW) * 64;
 #define PSE4_ATTF 0
 #endif
 #define P4_AFLAG (PSE4_HCNT == 2 && PSE4_ATTF)
-// PSE4_OGRP: o_proj slot k (k tiles 16k .. 16k + 15 = the 512 attention columns of KV head k) starts
-// once head k's 4 units (one per row) have published, instead of after the whole attention output
-#ifndef PSE4_OGRP
-#define PSE4_OGRP 1
+// PSE4_HTREE: the 256 arrivals of a residual hand-off counted in two levels -- 8 group counters
+// (CUs 32 g .. 32 g + 31, each on its own 128-byte line), whose completing arrival bumps the
+// hand-off's counter (8 arrivals) -- instead of 256 agent-scope atomics queueing on one line
+#ifndef PSE4_HTREE
+#define PSE4_HTREE 1
 #endif
+constexpr int HGRP = 8;                              // arrival groups
+constexpr int GCNT_STRIDE = 32;                      // ints: one 128-byte line per group counter
 constexpr int NS = PSE4_NS;
 constexpr int SLOT_KB = 16;
 constexpr int H_ = 4096, HQ_ = 32, HKV_ = 8, D_ = 128, I_ = 12288, QKVR_ = 6144;
@@ -311,10 +321,22 @@ __device__ __forceinline__ bool hgather(Ctx& x, const int* hcnt, const uint32_t*
 // one arrival at hand-off k after this CU's stores of it drained (by every storing wave); the
 // arrival that completes it (target) releases every consumer CU's flag line (PSE4_HCNT 2)
 __device__ __forceinline__ void harrive(const Ctx& x, int* hcnt, uint32_t* go, int k, int target) {
+  typedef __attribute__((address_space(1))) int gi;
   int t = 0;
-  if (x.lane == 0)
-    t = __hip_atomic_fetch_add((__attribute__((address_space(1))) int*)(hcnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  t = __shfl(t, 0, 64);
+  if (PSE4_HTREE && target == 256) {
+    // group counter g = c / 32 (its line: hcnt + 3 PSE_MAXL + (k HGRP + g) GCNT_STRIDE); the group's
+    // 32nd arrival is the one arrival at the hand-off's counter
+    int* gc = hcnt + 3 * PSE_MAXL + ((size_t)k * HGRP + x.c / (256 / HGRP)) * GCNT_STRIDE;
+    if (x.lane == 0) {
+      t = __hip_atomic_fetch_add((gi*)gc, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = t == 256 / HGRP - 1 ? __hip_atomic_fetch_add((gi*)(hcnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : -1;
+    }
+    t = __shfl(t, 0, 64);
+    target = HGRP;
+  } else {
+    if (x.lane == 0) t = __hip_atomic_fetch_add((gi*)(hcnt + k), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    t = __shfl(t, 0, 64);
+  }
   if (PSE4_HCNT == 2 && t == target - 1)
 #pragma unroll
     for (int i = 0; i < 4; ++i) st32(go + ((size_t)k * 256 + x.lane + 64 * i) * 32, x.epoch);
@@ -412,24 +434,51 @@ __device__ __forceinline__ void consume_slot(Ctx& x, int seq, int reg, int kt0, 
 __device__ __forceinline__ bool slot_ready(int seq) {
   return __hip_atomic_load(&P4_CTL->full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) > seq;
 }
-template <int RC>
+template <int RC, int LC = 0>
 struct SlotCache {
   u32x4 rc[RC > 0 ? RC : 1][4];
   int nd = 0;
   __device__ __forceinline__ void drain(Ctx& x, int seq) {
 #pragma unroll
-    for (int k = 0; k < RC; ++k)
+    for (int k = 0; k < RC + LC; ++k)
       if (k == nd && slot_ready(seq + k)) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         const u32x4* sl = reinterpret_cast<const u32x4*>(p4_lds + L_RING + ((seq + k) % NS) * SLOT_KB * 1024);
         const int w = x.wave - LW;
+        if (k < RC) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i) rc[k][i] = sl[(w * 4 + i) * 64 + x.lane];
+          for (int i = 0; i < 4; ++i) rc[k < RC ? k : 0][i] = sl[(w * 4 + i) * 64 + x.lane];
+        } else {  // this wave's 4 tiles -> region B slot k - RC (same tile layout as a ring slot)
+          u32x4* lb = reinterpret_cast<u32x4*>(p4_lds + L_XB + (k - RC) * SLOT_KB * 1024);
+          u32x4 t[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) t[i] = sl[(w * 4 + i) * 64 + x.lane];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) lb[(w * 4 + i) * 64 + x.lane] = t[i];
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (x.lane == 0)
           __hip_atomic_store(&P4_CTL->freed[w], seq + k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         ++nd;
       }
+  }
+  // slot i (RC <= i < RC + LC) from region B, else the ring
+  __device__ __forceinline__ void take_lds(Ctx& x, int& seq, int i, int reg, int kt0, f32x4& acc) {
+    if (i < nd) {
+      const u32x4* lb = reinterpret_cast<const u32x4*>(p4_lds + L_XB + (i - RC) * SLOT_KB * 1024);
+      const u32x4* xv = reinterpret_cast<const u32x4*>(p4_lds + reg);
+      const int w = x.wave - LW;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const u32x4 wt = lb[(w * 4 + q) * 64 + x.lane];
+        const u32x4 xb = xv[((kt0 + w * 4 + q) * NB + (x.lane & (NB - 1))) * 4 + (x.lane >> 4)];
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wt), __builtin_bit_cast(bf16x8, xb), acc,
+                                                      0, 0, 0);
+      }
+      ++seq;
+    } else {
+      consume_slot(x, seq++, reg, kt0, acc);
+    }
   }
   __device__ __forceinline__ void take(Ctx& x, int& seq, int i, int reg, int kt0, f32x4& acc) {
     if (i < RC && i < nd) {
@@ -896,40 +945,8 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           if (wave == LW) P4_STAMP(l, 3);
         }
         // ---------------- o_proj (+ residual) ----------------
-        SlotCache<RC> co;
-        if (PSE4_OGRP && !P4_AFLAG) {
-          // per KV-head group: gather head k's 512 columns of the 4 rows (1,024 granules, contiguous in
-          // the [k tile][row][16] layout), then run o_proj slot k on them; the ring slots drain into
-          // registers only while the first group is awaited (SlotCache counts from a fixed seq)
-          constexpr int NGG = NG_ATT / HKV_;
-          f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
-          bool ok = true;
-          auto grp = [&](int k) {
-            return gather<NGG / (CW * 64)>(x, a.g_att + (size_t)k * NGG, NGG, tagof(epoch, l, OP_ATT), xa32 + k * NGG,
-                                           NGG, nullptr, NoHook(), [&]() {
-                                             if (k == 0) co.drain(x, seq);
-                                           });
-          };
-          // (the register-drained slots first, at compile-time indices)
-#pragma unroll
-          for (int k = 0; k < RC; ++k) {
-            ok = ok && grp(k);
-            if (ok) co.take(x, seq, k, L_XA, k * 16, acc);
-          }
-#pragma unroll 1
-          for (int k = RC; k < HKV_ && ok; ++k) {
-            ok = grp(k);
-            if (ok) consume_slot(x, seq++, L_XA, k * 16, acc);
-          }
-          if (!ok) break;
-          if (wave == LW) P4_STAMP(l, 4);
-          __builtin_amdgcn_s_setprio(3);
-          red_put(x, 0, acc);
-          cbar(x);
-          emit_h(a.g_h[0], tagof(epoch, l, OP_O), red_get(0, ecol, erow), l * 2);
-          cbar(x);
-          __builtin_amdgcn_s_setprio(0);
-        } else {
+        constexpr int LC = ATT ? 0 : PSE4_LC;
+        SlotCache<RC, LC> co;
         if (P4_AFLAG) {
           if (!hgather(x, a.hcnt, a.go, 2 * PSE_MAXL + l, HKV_ * NB, reinterpret_cast<const bf16_t*>(a.g_att), nullptr, xa32,
                        nullptr, NoHook(), [&]() { co.drain(x, seq); }))
@@ -943,15 +960,16 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
           for (int k = 0; k < RC; ++k) co.take(x, seq, k, L_XA, k * 16, acc);
+#pragma unroll
+          for (int k = RC; k < RC + LC; ++k) co.take_lds(x, seq, k, L_XA, k * 16, acc);
 #pragma unroll 1
-          for (int k = RC; k < 8; ++k) consume_slot(x, seq++, L_XA, k * 16, acc);
+          for (int k = RC + LC; k < 8; ++k) consume_slot(x, seq++, L_XA, k * 16, acc);
           __builtin_amdgcn_s_setprio(3);
           red_put(x, 0, acc);
           cbar(x);
           emit_h(a.g_h[0], tagof(epoch, l, OP_O), red_get(0, ecol, erow), l * 2);
           cbar(x);
           __builtin_amdgcn_s_setprio(0);
-        }
         }
         if (wave == LW) P4_STAMP(l, 5);
         // ---------------- gate|up (post-attention RMSNorm fused, SwiGLU) ----------------
@@ -1041,6 +1059,7 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
       if (PSE4_HCNT) {
         for (int k = 0; k < 2 * a.layers; ++k) st32(a.hcnt + k, 0u);
         for (int k = 0; k < a.layers; ++k) st32(a.hcnt + 2 * PSE_MAXL + k, 0u);
+        for (int k = 0; k < 2 * a.layers * HGRP; ++k) st32(a.hcnt + 3 * PSE_MAXL + (size_t)k * GCNT_STRIDE, 0u);
       }
       st32(a.exit_cnt, 0u);
       st32(a.epoch, epoch);
@@ -1065,8 +1084,11 @@ bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I
          per_cu >= 1;
 }
 
+// counters: [3 PSE_MAXL] hand-off counters, then the group counters of the residual hand-offs
+// [2 PSE_MAXL][HGRP] one 128-byte line each (PSE4_HTREE), then the release flags
+constexpr size_t HCNT_BYTES = ((size_t)3 * PSE_MAXL + (size_t)2 * PSE_MAXL * HGRP * GCNT_STRIDE) * 4;
 size_t pse4_ws_bytes() {
-  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + 3 * PSE_MAXL * 4 +
+  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + HCNT_BYTES +
          (PSE4_HCNT == 2 ? (size_t)3 * PSE_MAXL * 256 * 128 : 0) + 64;
 }
 
@@ -1082,7 +1104,7 @@ hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   a.g_ss[1] = a.g_h[1] + NG_H;
   a.g_act = g; g += NG_ACT;
   a.hcnt = reinterpret_cast<int*>(g);
-  a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + 3 * PSE_MAXL * 4);
+  a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + HCNT_BYTES);
   uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse4_ws_bytes() - 64);
   a.err = w; a.epoch = w + 1; a.exit_cnt = w + 2;
   if (coop) {

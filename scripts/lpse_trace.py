@@ -16,8 +16,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from moss_tts_amd import _native as N  # noqa: E402
 
 NAMES = {0: "qkv input ready", 1: "normed", 2: "qkv done", 3: "att start", 4: "att done", 5: "o input in",
-         6: "o done", 7: "gu input normed", 8: "gu r0 done", 9: "gu r1 done", 10: "gu r2 done", 11: "gu r3 done",
-         12: "down r0 in", 13: "down r1 in", 14: "down r2 in", 15: "down r3 in", 16: "down done"}
+         6: "o done", 7: "gu input normed", 8: "gu r0 done", 9: "gu r1 done", 10: "gu r2 done",
+         11: "gu r3 done (residual CUs)", 15: "down r3 in", 12: "down r0 in", 13: "down r1 in", 14: "down r2 in",
+         16: "down done"}
 B, EV = 8, 28
 
 

@@ -25,6 +25,40 @@ sys.path.insert(0, ROOT)
 
 
 TTSD_TEXT, TTSD_A, TTSD_B = 5750, 24, 56  # prompt 5,867 rows = the bench's mean TTSD context (2,117 + 7,519 / 2)
+LOCAL_A, LOCAL_B = 8, 24  # MossTTSLocal frames of the two generations (--config local_frame)
+
+
+def run_local_frame():
+    """Two greedy MossTTSLocal generations (the 1.7B shape, B = 8, bench.py's ragged prompts) of
+    LOCAL_A and LOCAL_B frames: identical prefills and first LOCAL_A frames, so the counters of the
+    second minus the first are LOCAL_B - LOCAL_A whole frames (hipGraph replays: the backbone step,
+    33 channels of depth transformer + adapters + norm + head + pick, the frame end)."""
+    import numpy as np
+    import torch
+    from bench import local_prompt
+    from moss_tts_amd.engine import Engine, EngineConfig
+    rng = np.random.default_rng(1)
+    B = 8
+    prompts = [local_prompt(rng, text_tokens=int(n)) for n in rng.integers(36, 61, B)]
+    T = max(p.shape[0] for p in prompts)
+    ids = np.full((B, T, 33), 1024, np.int64)
+    ids[..., 0] = 151643
+    mask = np.zeros((B, T), bool)
+    for b, p in enumerate(prompts):
+        ids[b, T - p.shape[0]:] = p
+        mask[b, T - p.shape[0]:] = True
+    eng = Engine(EngineConfig(hidden=2048, layers=28, n_heads=16, n_kv=8, head_dim=128, inter=6144, n_vq=32,
+                              max_batch=B, max_ctx=T + LOCAL_B + 16, max_prefill_tokens=256 * B, model_kind=1,
+                              local_hidden=1536, local_layers=4, local_inter=8960, local_mlp_ffn=2048), 0)
+    eng.init_random(0)
+    ids_d, mask_d = torch.from_numpy(ids).cuda(), torch.from_numpy(mask).cuda()
+    for n in (LOCAL_A, LOCAL_B):
+        eng.local_generate_ids(ids_d, mask_d, n, -1, chunk=32)
+        torch.cuda.synchronize()
+    kv = 28 * 2 * 8 * 128 * 2 * B * (T + (LOCAL_A + LOCAL_B) / 2)
+    print(json.dumps({"T": T, "frames": [LOCAL_A, LOCAL_B], "lpse": eng.lpse_active(),
+                      "alg_bytes_per_frame": int(eng.local_frame_bytes(-1) + kv)}))
+    eng.close()
 
 
 def run_ttsd():
@@ -55,16 +89,20 @@ def run_ttsd():
     eng.close()
 
 
-def summarize_ttsd(d):
+def summarize_ttsd(d, cfg_name="ttsd"):
     """per-step bytes = (second generation - first) / (TTSD_B - TTSD_A); a generation starts at
-    the first prefill GEMM after a decode-step kernel"""
+    the first prefill GEMM after a decode-step kernel (local_frame: per frame, LOCAL_B - LOCAL_A)"""
     rows = []
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             key = r.get("Dispatch_Id") or r.get("Correlation_Id") or str(len(rows))
             rows.append((int(key), r["Kernel_Name"], r["Counter_Name"], float(r["Counter_Value"])))
-    out = {"config": "ttsd", "unit_raw": "KiB (rocprofv3 FETCH_SIZE / WRITE_SIZE)",
-           "what": f"whole decode steps at the mean TTSD context: generation of {TTSD_B} steps minus one of {TTSD_A}"}
+    local = cfg_name == "local_frame"
+    n_a, n_b = (LOCAL_A, LOCAL_B) if local else (TTSD_A, TTSD_B)
+    out = {"config": cfg_name, "unit_raw": "KiB (rocprofv3 FETCH_SIZE / WRITE_SIZE)",
+           "what": (f"whole MossTTSLocal frames (B = 8, ragged prompts): generation of {n_b} frames minus one of {n_a}"
+                    if local else
+                    f"whole decode steps at the mean TTSD context: generation of {n_b} steps minus one of {n_a}")}
     for cname in sorted({r[2] for r in rows}):
         seq = sorted((r for r in rows if r[2] == cname), key=lambda r: r[0])
         seg, dec_seen, tot = -1, True, [0.0, 0.0]
@@ -72,12 +110,12 @@ def summarize_ttsd(d):
         for _, kname, _, v in seq:
             if "gemm" in kname and dec_seen:
                 seg, dec_seen = seg + 1, False
-            if "pse_kernel" in kname or "finalize" in kname or "attn_decode" in kname:
+            if "pse_kernel" in kname or "finalize" in kname or "attn_decode" in kname or "lpse" in kname:
                 dec_seen = True
             if 0 <= seg < 2:
                 tot[seg] += v
                 per_k[seg][kname.split("(")[0]] += v
-        steps = TTSD_B - TTSD_A
+        steps = n_b - n_a
         by_kernel = {k: round((per_k[1][k] - per_k[0].get(k, 0.0)) / steps, 1) for k in per_k[1]}
         by_kernel = dict(sorted(by_kernel.items(), key=lambda kv: -kv[1])[:8])
         out[cname] = {"segments": seg + 1, "gen_kib": tot, "per_step_kib": (tot[1] - tot[0]) / steps,
@@ -86,7 +124,8 @@ def summarize_ttsd(d):
     write = out.get("WRITE_SIZE", {}).get("per_step_kib")
     if fetch is not None and write is not None:
         out["traffic_bytes_per_launch"] = int((2 * fetch + write) * 1024)
-        out["traffic_unit"] = "bytes per decode step (hipGraph replay, every kernel)"
+        out["traffic_unit"] = ("bytes per frame (hipGraph replay, every kernel)" if local else
+                               "bytes per decode step (hipGraph replay, every kernel)")
     print(json.dumps(out, indent=1))
 
 
@@ -97,6 +136,8 @@ def run(cfg_name, iters):
     from moss_tts_amd import _native as N
     if cfg_name == "ttsd":
         return run_ttsd()
+    if cfg_name == "local_frame":
+        return run_local_frame()
     if cfg_name == "local":
         cfg = EngineConfig(hidden=2048, layers=28, n_heads=16, n_kv=8, head_dim=128, inter=6144, n_vq=32, max_batch=8,
                            max_ctx=512, model_kind=1, local_hidden=1536, local_layers=4, local_inter=8960,
@@ -120,8 +161,8 @@ def run(cfg_name, iters):
 
 
 def summarize(d, cfg_name):
-    if cfg_name == "ttsd":
-        return summarize_ttsd(d)
+    if cfg_name in ("ttsd", "local_frame"):
+        return summarize_ttsd(d, cfg_name)
     vals = {}
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
@@ -144,7 +185,7 @@ def summarize(d, cfg_name):
 
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", choices=["clone", "local", "pse", "pse4", "ttsd"], default="clone")
+    ap.add_argument("--config", choices=["clone", "local", "local_frame", "pse", "pse4", "ttsd"], default="clone")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--summarize", default=None)
     a = ap.parse_args()
