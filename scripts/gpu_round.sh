@@ -3,15 +3,15 @@
 # kernel-trace summaries of the default and Local benches.  Writes gpurun_out/round/.
 set -u
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/round
+O=gpurun_out/${ROUND_TAG:-round}
 mkdir -p $O
 export TMPDIR=/tmp
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc"; tail -3 $O/smoke.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/pytest_gpu.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
 rc=$?; echo "bench rc=$rc"; cat $O/bench.json
 if [ $rc -ne 0 ]; then exit $rc; fi
