@@ -25,7 +25,8 @@ sys.path.insert(0, ROOT)
 
 
 TTSD_TEXT, TTSD_A, TTSD_B = 5750, 24, 56  # prompt 5,867 rows = the bench's mean TTSD context (2,117 + 7,519 / 2)
-LOCAL_A, LOCAL_B = 8, 24  # MossTTSLocal frames of the two generations (--config local_frame)
+LOCAL_A, LOCAL_B = 2, 6  # MossTTSLocal frames of the two generations (--config local_frame; ~1,050 dispatches a frame:
+# rocprofv3 --pmc crashed on the host collecting 2 x 24 frames of graph replays)
 
 
 def run_local_frame():
@@ -37,6 +38,7 @@ def run_local_frame():
     import torch
     from bench import local_prompt
     from moss_tts_amd.engine import Engine, EngineConfig
+    os.environ.setdefault("MTTS_LOCAL_NO_GRAPH", "1")  # direct launches (the same kernels) for the profiler
     rng = np.random.default_rng(1)
     B = 8
     prompts = [local_prompt(rng, text_tokens=int(n)) for n in rng.integers(36, 61, B)]
