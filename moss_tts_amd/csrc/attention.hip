@@ -328,9 +328,274 @@ __global__ __launch_bounds__(G * 64) void attn_prefill_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Long prompts (round 5): 32-token query tiles with the K / V^T chunks staged ONCE per block in
+// LDS.  The 16-token form above has each of its G waves load the chunk's K / V^T fragments itself
+// (16 KiB per wave per 32-key chunk, 16 MFMAs), and re-reads every key once per 16 tokens: at the
+// TTSD script's 2,117 tokens the attention took 445 us a layer (36.7 GFLOP: 3 % of the MFMA peak,
+// profiles/r05_h_prefill_*).  Here the block's 256 threads copy a 32-key chunk (K [32][D] and
+// V^T [D][32], 16 KiB) global -> LDS by LDS-DMA into one of two buffers while the waves run the
+// other, and each wave (one query head) computes 2 tiles of 16 tokens from those LDS tiles.
+//
+// The products run transposed, S^T = K . Q^T and O^T = V^T . P^T, so that every lane owns ONE
+// token column of each tile and 8 of the chunk's keys: the softmax statistics are per-lane scalars
+// (in-lane max over 8 keys + 2 cross-lane steps, one alpha per token), the probabilities feed the
+// P.V MFMA straight from the S^T accumulators, and chunks wholly below the diagonal with no
+// padding skip the mask arithmetic.  K rows enter the S^T tiles permuted (tile t, row r <- key
+// 8 (r >> 2) + 4 t + (r & 3)) so that lane (g4, c16) ends up holding keys 8 g4 .. 8 g4 + 7: the
+// contiguous k-slice the P^T B operand and the V^T A operand (one 16-B LDS read) need.  A first straight form (scores per token row, P through LDS) measured ~1,100 VALU
+// instructions per chunk against 32 MFMAs and ran at 310 us a layer.
+// Arithmetic as above: scores and statistics fp32 (exp via exp2 of log2e-scaled scores),
+// probabilities rounded to bf16 before P.V, the row sum over the unrounded ones.
+// max / sum of a value over lanes l, l ^ 16, l ^ 32, l ^ 48 (gfx950 row swaps, no LDS round trip)
+__device__ __forceinline__ float pf_max3(float a, float b, float c) {
+  float r;  // (fmaxf would canonicalise every MFMA / permlane result first)
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+__device__ __forceinline__ float pf_xmax(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = pf_max3(__uint_as_float(r[0]), __uint_as_float(r[1]), __uint_as_float(r[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return pf_max3(__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float pf_xsum(float v) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+__device__ __forceinline__ uint32_t pf_pack(float a, float b) {  // one v_cvt_pk_bf16_f32 (RNE)
+  typedef __attribute__((ext_vector_type(2))) float f2;
+  typedef __attribute__((ext_vector_type(2))) __bf16 h2;
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f2){a, b}, h2));
+}
+
+template <int G, int D>
+__global__ __launch_bounds__(G * 64, 2) void attn_prefill32_kernel(AttnArgs a) {
+  static_assert(D == 128 && G == 4, "the 8B / 1.7B head shape: 4 waves copy 16 KiB chunks in 1 KiB rows");
+  typedef __attribute__((address_space(3))) void lvoid;
+  constexpr int QS = D / 32, DT = D / 16, TQ = 32, RT = TQ / 16;
+  // the causal tiles' work grows with qt: dispatch the longest first
+  const int qt = gridDim.x - 1 - blockIdx.x, kvh = blockIdx.y, b = blockIdx.z;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int g4 = lane >> 4, c16 = lane & 15;
+  const int hq = kvh * G + wave;
+  const int s0 = qt * TQ;
+  const int pos0 = *a.pos_base + s0;
+  const int last = min(a.S - 1, s0 + TQ - 1);
+  const int kend = *a.pos_base + last;  // last key any token of the tile sees
+  const int Cmax = a.Cmax;
+  // one dynamic LDS block (PF32_LDS bytes): with static arrays the compiler cannot tell the two
+  // buffers apart and waits for the prefetch in flight before every LDS read of the chunk in use
+  extern __shared__ __attribute__((aligned(16))) unsigned char pf_lds[];
+  auto ks = reinterpret_cast<bf16_t(*)[32][D]>(pf_lds);                   // [buf][key][dim]
+  auto vs = reinterpret_cast<bf16_t(*)[D][32]>(pf_lds + 2 * 32 * D * 2);  // [buf][dim][key]
+  auto ms = reinterpret_cast<uint32_t(*)[64]>(pf_lds + 4 * 32 * D * 2);   // [buf] mask bytes
+  const bf16_t* kbase = a.kc + ((size_t)b * a.Hkv + kvh) * Cmax * D;
+  const bf16_t* vbase = a.vc + ((size_t)b * a.Hkv + kvh) * D * Cmax;
+  const uint8_t* mrow = a.mask + (size_t)b * Cmax;
+  const __amdgpu_buffer_rsrc_t krs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(kbase), 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<bf16_t*>(vbase), 0, Cmax * D * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mrow), 0, Cmax, 0x00020000);
+  constexpr uint32_t OOBA = 0x7ffffff0u;
+  // chunk k0 -> LDS buffer buf: each wave 2 KiB of K (keys 8 w .. 8 w + 7) and 2 KiB of V^T (dims
+  // 32 w .. 32 w + 31, 64 B each), 1 KiB per LDS-DMA instruction (lane l: 16 B at lds + 16 l).
+  // Bank swizzle on the SOURCE side (the LDS-DMA destination is fixed per lane): K row r holds
+  // its 16-B piece j at slot j ^ kswz(r), V^T row d its piece j at slot j ^ ((d >> 2) & 3), so
+  // the fragment reads below (16 rows per 16 lanes) spread over all 64 banks.
+  // distinct over each S^T tile's 16 keys (bits 0, 1, 3, 4 of the key's row in the chunk)
+  auto kswz = [](int r) { return (r & 3) | ((r >> 1) & 12); };
+  auto issue = [&](int k0, int buf) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int kr = wave * 8 + i * 4 + (lane >> 4);        // 4 keys (256 B each) per instruction
+      const int key = k0 + kr;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          krs, (lvoid*)&ks[buf][wave * 8 + i * 4][0], 16,
+          (key < Cmax) ? (uint32_t)(key * D * 2 + ((lane & 15) ^ kswz(kr)) * 16) : OOBA, 0, 0, 0);
+      const int d = wave * 32 + i * 16 + (lane >> 2);       // 16 dims (64 B each) per instruction
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          vrs, (lvoid*)&vs[buf][wave * 32 + i * 16][0], 16,
+          (k0 + 32 <= Cmax) ? (uint32_t)((d * Cmax + k0) * 2 + ((lane & 3) ^ ((d >> 2) & 3)) * 16) : OOBA, 0, 0, 0);
+    }
+    // the chunk's 32 mask bytes ride with it (a register load here would make the waitcnt before
+    // its first use also wait for the chunk prefetched after it)
+    if (wave == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(mrs, (lvoid*)&ms[buf][0], 4,
+                                               lane < 8 ? (uint32_t)(k0 + 4 * lane) : OOBA, 0, 0, 0);
+  };
+  // Q B-operand fragments of the 2 token tiles: token s0 + 16 rt + c16, dims 32 st + 8 g4 ..
+  bf16x8 qf[RT][QS];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int tq = min(s0 + rt * 16 + c16, a.S - 1);
+    const bf16_t* qrow = a.q + ((size_t)b * a.S + tq) * a.Hq * D + (size_t)hq * D;
+#pragma unroll
+    for (int st = 0; st < QS; ++st) qf[rt][st] = *reinterpret_cast<const bf16x8*>(qrow + st * 32 + 8 * g4);
+  }
+  const float sc2 = a.scale * 1.4426950408889634f;  // scores in log2 units
+  // this lane's token of tile rt sees keys <= pq[rt] (capped at kend: keys past the prompt are
+  // never written before the read)
+  int pq[RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) pq[rt] = min(pos0 + rt * 16 + c16, kend);
+  // m: running max (log2 units; -1e30 stands for "none yet" so fully masked tokens stay finite
+  // and end with l = 0), l: this lane's partial of the row sum (reduced over g4 at the end)
+  float m_run[RT], l_run[RT];
+  f32x4 o_run[DT][RT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    m_run[rt] = -1e30f;
+    l_run[rt] = 0.f;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) o_run[dt][rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  }
+  const int nch = kend / 32 + 1;
+  issue(0, 0);
+  for (int c = 0; c < nch; ++c) {
+    const int k0 = c * 32, buf = c & 1;
+    // chunk c has landed for every wave; buffer buf ^ 1 was last read in iteration c - 1
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+    if (c + 1 < nch) issue(k0 + 32, buf ^ 1);
+    // ---- S^T = K . Q^T: K A-operand row c16 of tile t = key 8 (c16 >> 2) + 4 t + (c16 & 3) of
+    // the chunk, dims 32 st + 8 g4 .. ----
+    f32x4 sacc[2][RT];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int kr = 8 * (c16 >> 2) + 4 * t + (c16 & 3);
+      u32x4 kf[QS];
+#pragma unroll
+      for (int st = 0; st < QS; ++st) kf[st] = *reinterpret_cast<const u32x4*>(&ks[buf][kr][((st * 4 + g4) ^ kswz(kr)) * 8]);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        sacc[t][rt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < QS; ++st)
+          sacc[t][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, kf[st]), qf[rt][st],
+                                                                sacc[t][rt], 0, 0, 0);
+      }
+    }
+    // lane (g4, c16) holds scores of keys k0 + 8 g4 + 4 t + i for token tile rt column c16
+    const uint32_t mw0 = ms[buf][2 * g4], mw1 = ms[buf][2 * g4 + 1];  // mask bytes of its 8 keys
+    auto has_zero = [](uint32_t w) { return ((w - 0x01010101u) & ~w & 0x80808080u) != 0u; };
+    const bool full = (k0 + 31 <= pos0) && !__builtin_amdgcn_ballot_w64(has_zero(mw0) || has_zero(mw1));
+    // (the asm markers keep the two rare paths below as wave-uniform branches: without them the
+    // compiler speculates the masking into selects on every chunk)
+    // statistics in raw score units (the scale is > 0); exp2 of fma(s, sc2, -m sc2)
+    float alpha[RT];
+    bf16x8 pf[RT];
+    if (!full) {  // diagonal / padded chunks
+      asm volatile("; masked chunk");
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int key = k0 + 8 * g4 + 4 * t + i;
+            const uint32_t mb = ((t ? mw1 : mw0) >> (8 * i)) & 0xffu;
+            if (!(key <= pq[rt] && mb)) sacc[t][rt][i] = -INFINITY;
+          }
+    }
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const float m1 = pf_max3(sacc[0][rt][0], sacc[0][rt][1], sacc[0][rt][2]);
+      const float m2 = pf_max3(sacc[0][rt][3], sacc[1][rt][0], sacc[1][rt][1]);
+      const float mc = pf_xmax(pf_max3(m1, m2, pf_max3(sacc[1][rt][2], sacc[1][rt][3], m_run[rt])));
+      const float mn = mc;  // (m_run folded into the max)
+      alpha[rt] = __builtin_amdgcn_exp2f((m_run[rt] - mn) * sc2);
+      m_run[rt] = mn;
+      const float nm = -mn * sc2;
+      float lc = 0.f;
+      uint32_t pw[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[k >> 1][rt][2 * (k & 1)], sc2, nm));
+        const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[k >> 1][rt][2 * (k & 1) + 1], sc2, nm));
+        lc += p0 + p1;
+        pw[k] = pf_pack(p0, p1);  // bf16-rounded probabilities
+      }
+      l_run[rt] = l_run[rt] * alpha[rt] + lc;
+      pf[rt] = __builtin_bit_cast(bf16x8, (u32x4){pw[0], pw[1], pw[2], pw[3]});
+    }
+    // the running max rarely moves once a few chunks are in: rescale O only when it did
+    if (__builtin_amdgcn_ballot_w64(alpha[0] != 1.f || alpha[1] != 1.f)) {
+      asm volatile("; rescale");
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) o_run[dt][rt][i] *= alpha[rt];
+    }
+    // ---- O^T += V^T . P^T; V^T A-operand (dim dt*16 + c16, keys 8 g4 .. 8 g4 + 7: 16-B piece
+    // g4, stored at slot g4 ^ ((d >> 2) & 3)); in the chunk holding kend, keys past it zeroed
+    // (cache rows not yet written: 0 * NaN in the MFMA would be NaN) ----
+    const bool tail = k0 + 31 > kend;
+    uint32_t vm[4] = {~0u, ~0u, ~0u, ~0u};
+    if (tail) {
+      asm volatile("; tail mask");
+      const int nv = kend + 1 - (k0 + 8 * g4);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vm[q] = (2 * q < nv ? 0x0000ffffu : 0u) | (2 * q + 1 < nv ? 0xffff0000u : 0u);
+    }
+    const int vslot = (g4 ^ ((c16 >> 2) & 3)) * 8;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      u32x4 vt = *reinterpret_cast<const u32x4*>(&vs[buf][dt * 16 + c16][vslot]);
+      if (tail) {
+        asm volatile("; tail chunk");
+#pragma unroll
+        for (int q = 0; q < 4; ++q) vt[q] &= vm[q];
+      }
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+        o_run[dt][rt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, vt), pf[rt], o_run[dt][rt], 0, 0, 0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // ---- normalise and store: token s0 + 16 rt + c16, dims dt*16 + 4 g4 + i ----
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const float l = pf_xsum(l_run[rt]);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    const int tq = s0 + rt * 16 + c16;
+    if (tq >= a.S) continue;
+    const int mrow_ = b * a.S + tq;
+    bf16_t* dst = a.out + (size_t)mrow_ * a.Hq * D + (size_t)hq * D;
+#pragma unroll
+    for (int dt = 0; dt < DT; ++dt) {
+      const int d0 = dt * 16 + 4 * g4;
+      const f32x4 o4 = o_run[dt][rt];
+      if (a.out_tiles) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a.out[xpkT_index(mrow_, hq * D + d0 + i, a.out_tiles)] = f2bf(o4[i] * inv);
+      } else {
+        *reinterpret_cast<uint2*>(dst + d0) = make_uint2(pack2(o4[0] * inv, o4[1] * inv), pack2(o4[2] * inv, o4[3] * inv));
+      }
+    }
+  }
+}
+
+// query tokens per row from which the 32-token LDS-staged form runs (MTTS_ATTN_PF32_MIN, A/B;
+// 0: never)
+static int attn_pf32_min() {
+  static const int v = getenv("MTTS_ATTN_PF32_MIN") ? atoi(getenv("MTTS_ATTN_PF32_MIN")) : 64;
+  return v;
+}
+
 template <int D>
 static hipError_t attn_prefill_d(const AttnArgs& a, int G, hipStream_t st) {
   const int B = a.M / a.S;
+  if constexpr (D == 128) {
+    if (G == 4 && attn_pf32_min() > 0 && a.S >= attn_pf32_min()) {
+      constexpr size_t PF32_LDS = 4 * 32 * D * 2 + 2 * 256;
+      hipLaunchKernelGGL((attn_prefill32_kernel<4, D>), dim3((a.S + 31) / 32, a.Hkv, B), dim3(256), PF32_LDS, st, a);
+      return hipGetLastError();
+    }
+  }
   dim3 grid((a.S + 15) / 16, a.Hkv, B);
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_prefill_kernel<1, D>), grid, dim3(64), 0, st, a); break;

@@ -426,6 +426,38 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
         assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), (CH, err.max())
 
 
+@pytest.mark.parametrize("S,past,B,Cmax", [(512, 0, 1, 512), (600, 37, 2, 704), (1100, 0, 1, 1152), (777, 300, 1, 1088)])
+def test_attention_prefill_long(N, S, past, B, Cmax):
+    """Long prompts take the 32-token LDS-staged flash kernel (attention.hip attn_prefill32_kernel,
+    S >= MTTS_ATTN_PF32_MIN = 512 query tokens, 4 query heads per KV head, D = 128): ragged tail
+    tiles, a cached prefix, left padding on row 1 and uninitialised (NaN) cache rows past the prompt."""
+    rng = np.random.default_rng(S + past)
+    ctx = O._Ctx("bf16")
+    D, Hq, Hkv = 128, 32, 8
+    M = B * S
+    q = rand_bf16(rng, (B, S, Hq, D), 2.0)
+    kc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
+    vc0 = rand_bf16(rng, (B, Hkv, D, Cmax))
+    end = past + S
+    kc0[:, :, end:] = np.nan  # rows no query may read: must not leak through 0 * NaN
+    vc0[:, :, :, end:] = np.nan
+    mask = np.ones((B, Cmax), np.uint8)
+    if B > 1:
+        mask[1, :45] = 0
+    qd, kc, vc = dev_bf16(q.reshape(M, Hq * D)), dev_bf16(kc0), dev_bf16(vc0)
+    md = torch.from_numpy(mask).cuda()
+    pos = torch.tensor([past], dtype=torch.int32, device="cuda")
+    out = torch.zeros(M, Hq * D, dtype=torch.bfloat16, device="cuda")
+    N.call("mtts_k_attention_prefill", P(qd), P(kc), P(vc), P(md), P(pos), P(out), M, S, Hq, Hkv, D, Cmax, None)
+    torch.cuda.synchronize()
+    want = O.attention(ctx, q.transpose(0, 2, 1, 3), kc0[:, :, :end], vc0.transpose(0, 1, 3, 2)[:, :, :end],
+                       mask[:, :end].astype(bool), np.arange(past, end), D ** -0.5)
+    got = host(out).reshape(B, S, Hq, D).transpose(0, 2, 1, 3)
+    err = np.abs(got - want)
+    assert np.isfinite(got).all()
+    assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), err.max()
+
+
 @pytest.mark.parametrize("past,D,Hq,Hkv,B", [(10, 128, 32, 8, 1), (0, 16, 4, 2, 3), (300, 128, 8, 2, 2), (700, 64, 4, 1, 2),
                                              (127, 128, 32, 8, 1), (128, 128, 32, 8, 2), (1023, 16, 8, 1, 1),
                                              (389, 128, 32, 8, 4), (3000, 128, 32, 8, 1), (8100, 64, 8, 2, 1)])
