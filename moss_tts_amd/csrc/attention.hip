@@ -569,12 +569,9 @@ __global__ __launch_bounds__(G * 64, 2) void attn_prefill32_kernel(AttnArgs a) {
     for (int dt = 0; dt < DT; ++dt) {
       const int d0 = dt * 16 + 4 * g4;
       const f32x4 o4 = o_run[dt][rt];
-      if (a.out_tiles) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) a.out[xpkT_index(mrow_, hq * D + d0 + i, a.out_tiles)] = f2bf(o4[i] * inv);
-      } else {
-        *reinterpret_cast<uint2*>(dst + d0) = make_uint2(pack2(o4[0] * inv, o4[1] * inv), pack2(o4[2] * inv, o4[3] * inv));
-      }
+      // dims d0 .. d0 + 3 stay contiguous in the packed layout too (k & 7 = 0..3 or 4..7)
+      const uint2 o = make_uint2(pf_pack(o4[0] * inv, o4[1] * inv), pf_pack(o4[2] * inv, o4[3] * inv));
+      *reinterpret_cast<uint2*>(a.out_tiles ? a.out + xpkT_index(mrow_, hq * D + d0, a.out_tiles) : dst + d0) = o;
     }
   }
 }

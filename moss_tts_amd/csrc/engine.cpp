@@ -934,7 +934,7 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   e->gen_B = B; e->gen_T = T; e->gen_max_new = max_new; e->forced = forced;
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemsetAsync(e->seen, 0, 2 * e->audio_rows, s));
-  HIPCHK(gen_init(e->bufs(), ids, mask, s));
+  HIPCHK(gen_init(e->bufs(), ids, mask, B, T, c.n_vq + 1, s));
   e->pse_choose(T);  // (a prefill takes the launch only as a one-token prompt)
   e->long_now = e->attn_long_ctx > 0 && T > e->attn_long_ctx;
   int rc = forward_chunked(e, ids, B, T, 0, e->logits, s);

@@ -707,7 +707,37 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // (profiles/r04_p_gemm5_long_ab.txt)
   static const int g5l = getenv("MTTS_GEMM5_LONG") ? atoi(getenv("MTTS_GEMM5_LONG")) : 1;
   if (g5l) {
-    if (a.n_row_tiles >= wide_min) return gemm5_launch<2, 4, 8, 4, 2, EPI>(a, 128, 16, s);
+    // token tiles per wave chosen as below for the 256-row blocks too (4 or 5; MTTS_GEMM5_WWN forces)
+    if (a.n_row_tiles >= wide_min) {
+      static const int force_wwn = getenv("MTTS_GEMM5_WWN") ? atoi(getenv("MTTS_GEMM5_WWN")) : 0;
+      int wn = force_wwn;
+      if (wn < 4 || wn > 5) {
+        const long rb = (a.n_row_tiles + 15) / 16;
+        const long c4 = (rb * ((a.pk_tiles + 15) / 16) + 255) / 256 * 4;
+        const long c5 = (rb * ((a.pk_tiles + 19) / 20) + 255) / 256 * 5;
+        wn = c5 < c4 ? 5 : 4;
+      }
+      if (wn == 5) return gemm5_launch<2, 4, 8, 5, 2, EPI>(a, 128, 16, s);
+      return gemm5_launch<2, 4, 8, 4, 2, EPI>(a, 128, 16, s);
+    }
+    // 128-row blocks: token tiles per wave WN = 4, 5 or 6 by the launch's rounds over the CUs x
+    // per-block work (ceil(blocks / 256) x WN).  WN = 4 alone gave the TTSD script's 2,117-row o_proj
+    // and down projections 288 blocks (32 CUs holding two): 118 / 345 us against hipBLASLt's 96 / 229
+    // (scripts/blas_ref.py, profiles/r05_j_*); WN = 5 deals 224 blocks, one a CU.  MTTS_GEMM5_WN
+    // forces one (A/B).
+    static const int force_wn = getenv("MTTS_GEMM5_WN") ? atoi(getenv("MTTS_GEMM5_WN")) : 0;
+    int wn = force_wn;
+    if (wn < 4 || wn > 6) {
+      const int rb = (a.n_row_tiles + 7) / 8;
+      long best = 1L << 40;
+      for (int w = 4; w <= 6; ++w) {
+        const long blocks = (long)rb * ((a.pk_tiles + 4 * w - 1) / (4 * w));
+        const long cost = (blocks + 255) / 256 * w;
+        if (cost < best) { best = cost; wn = w; }
+      }
+    }
+    if (wn == 5) return gemm5_launch<2, 4, 4, 5, 2, EPI>(a, 128, 16, s);
+    if (wn == 6) return gemm5_launch<2, 4, 4, 6, 2, EPI>(a, 128, 16, s);
     return gemm5_launch<2, 4, 4, 4, 2, EPI>(a, 128, 16, s);
   }
   if (a.n_row_tiles >= wide_min) return gemm3_launch<2, 4, 8, 4, G3_NST, EPI>(a, 128, 16, s);

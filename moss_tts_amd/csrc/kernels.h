@@ -335,7 +335,7 @@ size_t lpse_ws_bytes();  // zero-filled once by the owner
 hipError_t lpse_channel(const LpseArgs& a, void* ws, hipStream_t s);
 uint32_t* lpse_err_word(void* ws);
 // sample.hip
-hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s);
+hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, int B, int T, int C, hipStream_t s);
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s);
 // local.hip (MossTTSLocal depth stage)
 hipError_t moss_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int H, float eps, hipStream_t s);

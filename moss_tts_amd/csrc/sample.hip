@@ -19,6 +19,8 @@
 //   finalize      (1 block)      state update, next input ids, generation buffer, mask, stop
 // Draws: Philox(seed; step, row, channel) uniforms through torch's bf16 softmax / cumsum
 // arithmetic (torch_draw); distribution-level parity, torch's RNG stream is not reproduced.
+#include <algorithm>
+
 #include "kernels.h"
 #include "topk.h"
 
@@ -298,48 +300,61 @@ __global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
 
 // generate() prologue (modeling_moss_tts.py:417-440): per-row continuation state,
 // copy of the prompt into the generation buffer / mask, audio history bitmaps.
+// Blocks [0, B): row b's state (the block scans the row for its last audio_start together -- one
+// thread walking a 2,117-token prompt backwards took 0.6 ms); blocks from B: grid-stride copies.
 __global__ __launch_bounds__(256) void gen_init_kernel(GenBufs g, const int64_t* ids, const uint8_t* mask_in) {
   GenDev& st = *g.st;
   const MttsIds& d = st.ids;
-  const int T = st.T0, C = st.C;
-  // copies (grid-stride over all threads of the one block)
-  for (size_t i = threadIdx.x; i < (size_t)st.B * T * C; i += blockDim.x) {
-    const size_t b = i / ((size_t)T * C), r = i % ((size_t)T * C);
-    g.gen_ids[b * st.Ltot * C + r] = ids[i];
-    const int c = (int)(r % C);
-    if (c >= 1) {
-      const int64_t tok = ids[i];
-      if (tok >= 0 && tok < st.audio_rows) g.seen[(c == 1 ? 0 : st.audio_rows) + tok] = 1;
-    }
-  }
-  for (size_t i = threadIdx.x; i < (size_t)st.B * T; i += blockDim.x) {
-    const size_t b = i / T, t = i % T;
-    g.mask[b * st.Cmax + t] = mask_in ? mask_in[i] : 1;
-  }
-  for (int b = threadIdx.x; b < st.B; b += blockDim.x) {
+  const int T = st.T0, C = st.C, B = st.B;
+  if ((int)blockIdx.x < B) {
+    const int b = blockIdx.x;
     const int64_t* row = ids + (size_t)b * T * C;
-    const int64_t last = row[(size_t)(T - 1) * C];
-    const bool cont = last == d.audio_start || last == d.gen_slot;
+    __shared__ int last_as;
+    if (threadIdx.x == 0) last_as = -1;
+    __syncthreads();
     int as = -1;
-    for (int t = T - 1; t >= 0; --t)
-      if (row[(size_t)t * C] == d.audio_start) { as = t; break; }  // find_last_equal_C
-    const bool am = cont && as != -1;
-    g.audio_len[b] = am ? (int64_t)(T - as) : 0;
-    g.is_audio[b] = am;
-    g.is_stopping[b] = 0;
-    g.delayed[b] = I64MAX;
+    for (int t = threadIdx.x; t < T; t += blockDim.x)
+      if (row[(size_t)t * C] == d.audio_start) as = t;  // find_last_equal_C
+    if (as >= 0) atomicMax(&last_as, as);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int64_t last = row[(size_t)(T - 1) * C];
+      const bool cont = last == d.audio_start || last == d.gen_slot;
+      const bool am = cont && last_as != -1;
+      g.audio_len[b] = am ? (int64_t)(T - last_as) : 0;
+      g.is_audio[b] = am;
+      g.is_stopping[b] = 0;
+      g.delayed[b] = I64MAX;
+      if (b == 0) {
+        st.step = 0;
+        st.done_step = -1;
+        st.fwd_pos = 0;
+        st.need_text = 1;  // step 0 samples from the prefill's full logits
+        st.text_head_steps = 0;
+      }
+    }
+    return;
   }
-  if (threadIdx.x == 0) {
-    st.step = 0;
-    st.done_step = -1;
-    st.fwd_pos = 0;
-    st.need_text = 1;  // step 0 samples from the prefill's full logits
-    st.text_head_steps = 0;
+  // copies (grid-stride over the copy blocks)
+  const int nthr = (gridDim.x - B) * blockDim.x;
+  const int tid = (blockIdx.x - B) * blockDim.x + threadIdx.x;
+  const int TC = T * C;
+  for (int i = tid; i < B * TC; i += nthr) {
+    const int b = i / TC, r = i - b * TC;
+    const int64_t tok = ids[i];
+    g.gen_ids[(size_t)b * st.Ltot * C + r] = tok;
+    const int c = r % C;
+    if (c >= 1 && tok >= 0 && tok < st.audio_rows) g.seen[(c == 1 ? 0 : st.audio_rows) + tok] = 1;
+  }
+  for (int i = tid; i < B * T; i += nthr) {
+    const int b = i / T, t = i - b * T;
+    g.mask[(size_t)b * st.Cmax + t] = mask_in ? mask_in[i] : 1;
   }
 }
 
-hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, hipStream_t s) {
-  hipLaunchKernelGGL(gen_init_kernel, dim3(1), dim3(256), 0, s, g, ids, mask);
+hipError_t gen_init(const GenBufs& g, const int64_t* ids, const uint8_t* mask, int B, int T, int C, hipStream_t s) {
+  const int copy_blocks = std::max(1, std::min(512, (B * T * C + 255) / 256));
+  hipLaunchKernelGGL(gen_init_kernel, dim3(B + copy_blocks), dim3(256), 0, s, g, ids, mask);
   return hipGetLastError();
 }
 

@@ -200,7 +200,9 @@ def xpk_indices(M, K):
 
 @pytest.mark.parametrize("M,Nr,K,epi", [(181, 6144, 4096, 0), (181, 4096, 4096, 1), (181, 12288, 4096, 2),
                                         (181, 4096, 12288, 1), (130, 1000, 512, 1), (192, 96, 1024, 2),
-                                        (2048, 4096, 4096, 1), (2048, 1536, 2048, 2), (1024, 12288, 4096, 2)])
+                                        (2048, 4096, 4096, 1), (2048, 1536, 2048, 2), (1024, 12288, 4096, 2),
+                                        (2117, 4096, 4096, 1), (1500, 6144, 4096, 0), (3000, 1024, 512, 1),
+                                        (2117, 12288, 4096, 2)])
 def test_gemm_packed_prefill(N, M, Nr, K, epi):
     """Prefill GEMM on fragment-packed activations (the engine's >= 128-row prompts) at the 8B
     projections' shapes: 181 rows take gemm3's one-token-block form (split K for q|k|v, o_proj,
@@ -319,17 +321,19 @@ def test_rmsnorm(N, M, H):
     assert np.mean(got == want) > 0.99
 
 
-@pytest.mark.parametrize("H,n_vq", [(64, 4), (320, 32), (4096, 32)])
-def test_embed_exact(N, H, n_vq):
+@pytest.mark.parametrize("H,n_vq,M", [(64, 4, 6), (320, 32, 6), (4096, 32, 6), (320, 5, 100), (4096, 16, 70),
+                                      (6144, 32, 64)])
+def test_embed_exact(N, H, n_vq, M):
+    """M >= 64 rows take the prompt form (norm_rope.hip embed_wide_kernel); bit-exact either way."""
     cfg = O.tiny_cfg(n_vq=n_vq)
-    rng = np.random.default_rng(H + n_vq)
+    rng = np.random.default_rng(H + n_vq + M)
     et = rand_bf16(rng, (cfg.vocab, H))
     ea = rand_bf16(rng, (cfg.n_vq, 1025, H))
-    ids = np.concatenate([rng.integers(0, cfg.vocab, (6, 1)), rng.integers(0, 1025, (6, cfg.n_vq))], 1).astype(np.int64)
-    h = torch.zeros(6, H, dtype=torch.bfloat16, device="cuda")
+    ids = np.concatenate([rng.integers(0, cfg.vocab, (M, 1)), rng.integers(0, 1025, (M, cfg.n_vq))], 1).astype(np.int64)
+    h = torch.zeros(M, H, dtype=torch.bfloat16, device="cuda")
     idd = torch.from_numpy(ids).cuda()
     etd, ead = dev_bf16(et), dev_bf16(ea)
-    N.call("mtts_k_embed", P(idd), cfg.n_vq + 1, P(etd), P(ead), 1025, H, P(h), 6, None)
+    N.call("mtts_k_embed", P(idd), cfg.n_vq + 1, P(etd), P(ead), 1025, H, P(h), M, None)
     torch.cuda.synchronize()
     W = {"language_model.embed_tokens.weight": et}
     for j in range(cfg.n_vq):
