@@ -258,7 +258,7 @@ int mtts_k_gemv_splitk(const uint16_t* wpacked, const uint16_t* x, int ldx, uint
  * add + per-16-column sums of squares into ss_out when non-NULL, 2 swiglu) */
 int mtts_k_gemm(const uint16_t* wpacked, const uint16_t* x, int ldx, uint16_t* y, int ldy, const uint16_t* res,
                 int ldres, int M, int N, int K, int epi, float* ss_out, int ld_ss_out, void* stream);
-/* the prefill projections' packed-activation form (the engine's >= 128-row prompts): x_packed holds
+/* the prefill projections' packed-activation form (the engine's >= 33-row prompts; M >= 33): x_packed holds
  * ceil(M / 16) token tiles in the fragment order xpkT_index (kernels.h: u16 index
  * ((((k / 32) T + m / 16) 64 + m % 16 + 16 ((k % 32) / 8)) 8 + k % 8), T = ceil(M / 16)); y row-major
  * (epi 0 / 1) or, y_packed = 1 (epi 2 only, the down projection's input), packed the same way over

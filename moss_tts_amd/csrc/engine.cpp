@@ -572,7 +572,8 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   // prefills of >= 128 token rows (the 128 x 128 GEMM's range): packed GEMM inputs.  B=1 clone
   // prompt (181 rows) 12.6 -> 9.5 ms with the split-K partial launches reading them packed
   // (MTTS_PK_MIN / MTTS_PK_SPLIT=0 for A/B)
-  static const int pk_min = getenv("MTTS_PK_MIN") ? atoi(getenv("MTTS_PK_MIN")) : 128;
+  // (from 33 rows since round 5: the <= 192-row GEMM form takes 3-12 token tiles)
+  static const int pk_min = getenv("MTTS_PK_MIN") ? atoi(getenv("MTTS_PK_MIN")) : 33;
   const int pkT = (S > 1 && M >= pk_min && e->xpack && !e->gemv_prefill && !e->old_prefill_attn &&
                    M >= gemm_min_rows() && (M + 15) / 16 * 16 <= st.rows) ? (M + 15) / 16 : 0;
   const int ntiles = xpk ? 2 : pkT;  // packed activations of this call (0: row-major)
@@ -1321,7 +1322,7 @@ extern "C" int mtts_k_gemm(const uint16_t* w, const uint16_t* x, int ldx, uint16
 extern "C" int mtts_k_gemm_packed(const uint16_t* w, const uint16_t* x, uint16_t* y, int ldy, int y_packed,
                                   const uint16_t* res, int ldres, int M, int N, int K, int epi, float* ss_out,
                                   int ld_ss_out, float* ws, size_t ws_floats, void* stream) {
-  if (K % 64 || M < 128) return fail(MTTS_E_INVALID, "packed prefill GEMM: K % 64 == 0 and M >= 128");
+  if (K % 64 || M < 33) return fail(MTTS_E_INVALID, "packed prefill GEMM: K % 64 == 0 and M >= 33");
   if (epi != EPI_STORE && epi != EPI_RESADD && epi != EPI_SWIGLU) return fail(MTTS_E_INVALID, "epi 0/1/2 only");
   if (y_packed && epi != EPI_SWIGLU) return fail(MTTS_E_INVALID, "packed outputs: epi 2 only");
   GemvArgs a = gemv_args(w, x, K, y, ldy, M, N, K);

@@ -536,6 +536,9 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm3_kernel(GemvArgs a) {
 // Shape <NWR, NWN, WR, WN>: NWR x NWN waves, each WR weight row tiles x WN token tiles; the block's
 // BR = NWR WR weight tiles per k step are split over the waves' LDS-DMA loads, each wave loads its own
 // WN activation fragments.  <1, 6, 6, 2> for <= 192 rows.
+#ifndef G5S_R
+#define G5S_R 4  // k steps in flight of the <= 192-row form (A/B)
+#endif
 template <int NWR, int NWN, int WR, int R>
 constexpr size_t gemm5_lds_bytes() { return (size_t)(R + 1) * NWR * WR * 1024; }
 template <int NWR, int NWN, int WR, int WN, int R, int EPI, bool SPLIT = false>
@@ -700,7 +703,9 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // slower: 181 rows 7.97 -> 8.20 ms, 32 utterances 91.9 -> 95.7 ms, profiles/r04_j_*)
   // MTTS_GEMM5 (A/B): the split-path form for <= 12 token tiles
   static const int g5 = getenv("MTTS_GEMM5") ? atoi(getenv("MTTS_GEMM5")) : 1;
-  if (a.pk_tiles <= small_max && g5) return gemm5_launch<1, 6, 6, 2, 4, EPI>(a, 256, small_mink, s);
+  // MTTS_GEMM5_SMALL_COVER (A/B): workgroups the split-K aims for
+  static const int small_cover = getenv("MTTS_GEMM5_SMALL_COVER") ? atoi(getenv("MTTS_GEMM5_SMALL_COVER")) : 256;
+  if (a.pk_tiles <= small_max && g5) return gemm5_launch<1, 6, 6, 2, G5S_R, EPI>(a, small_cover, small_mink, s);
   if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, G3S_NST, EPI>(a, 256, small_mink, s);
   // MTTS_GEMM5_LONG (A/B, 0: gemm3): the long-prompt shapes with split paths as well -- batch-4 prefill
   // 18.6 -> 17.5 ms, 1,024 rows 27.7 -> 26.6, TTSD long form 75.2 -> 71.6, 32 utterances unchanged
@@ -771,7 +776,11 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   const int n_tiles = (a0.N + 15) / 16;
   static const int big = getenv("MTTS_GEMM_SMALL") && getenv("MTTS_GEMM_SMALL")[0] == '1' ? 1 << 30 : 128;
   // the packed layout is read / written by the 128 x 128 form only
-  if ((a0.x_packed || a0.y_packed) && (a0.B < big || a0.K % 64 || a0.pk_tiles * 16 < a0.B)) return hipErrorInvalidValue;
+  // (and, from round 5, 33-127 rows: the <= 192-row gemm5 form below; a 120-token prompt's row-major
+  // GEMMs had run 12.8 ms against 7.0 for 181 packed ones, profiles/r05_l_*)
+  if ((a0.x_packed || a0.y_packed) && ((a0.B < big && (a0.pk_tiles < 3 || a0.pk_tiles > 12)) || a0.K % 64 ||
+                                       a0.pk_tiles * 16 < a0.B))
+    return hipErrorInvalidValue;
   // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged form (0: off, A/B).  From
   // 512 rows since its k loop keeps NST - 1 stages in flight (a __syncthreads per k step had waited
   // them all out): 724-row prefill 20.5 -> 18.7 ms, 1,024-row 29.2 -> 28.0 (profiles/r04_i_*); at
@@ -788,6 +797,7 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
       default: return hipErrorInvalidValue;
     }
   }
+  if ((a.x_packed || a.y_packed) && a.B < big) return hipErrorInvalidValue;  // (gemm3 small form off)
   if (a.B >= big && a.K % 64 == 0) {  // 128 x 128 block tiles
     switch (epi) {
       case EPI_STORE: gemm2_launch<4, 4, EPI_STORE>(a, s); break;

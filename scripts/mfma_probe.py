@@ -30,19 +30,31 @@ def run():
     from bench import direct_prompt, synthetic_prompt
     from moss_tts_amd.engine import Engine, EngineConfig
     from moss_tts_amd.processing_moss_tts import left_pad
-    eng = Engine(EngineConfig(layers=LAYERS, max_batch=32, max_ctx=512, max_prefill_tokens=8192), 0)
+    # MFMA_SHAPES: b1 (the clone prompt), b32 (32 ragged utterances), ttsd (one 2,117-token prompt)
+    shapes = os.environ.get("MFMA_SHAPES", "b1,b32").split(",")
+    eng = Engine(EngineConfig(layers=LAYERS, max_batch=32, max_ctx=2304, max_prefill_tokens=8192), 0)
     eng.init_random(0)
     rng = np.random.default_rng(1)
-    one = torch.from_numpy(synthetic_prompt(dict(n_vq=32), rng)[None]).cuda()
-    lens = np.random.default_rng(0).integers(100, 131, 32)
-    p = left_pad([torch.from_numpy(direct_prompt(rng, int(T))) for T in lens], 151643, 1024)
-    ids32, mask32 = p["input_ids"].cuda(), p["attention_mask"].cuda()
-    for _ in range(3):
-        eng.forward(one, torch.ones(1, one.shape[1], dtype=torch.uint8, device="cuda"), 0)
-    for _ in range(2):
-        eng.forward(ids32, mask32, 0)
+    out = {}
+    if "b1" in shapes:
+        one = torch.from_numpy(synthetic_prompt(dict(n_vq=32), rng)[None]).cuda()
+        for _ in range(3):
+            eng.forward(one, torch.ones(1, one.shape[1], dtype=torch.uint8, device="cuda"), 0)
+        out["B1_tokens"] = int(one.shape[1])
+    if "b32" in shapes:
+        lens = np.random.default_rng(0).integers(100, 131, 32)
+        p = left_pad([torch.from_numpy(direct_prompt(rng, int(T))) for T in lens], 151643, 1024)
+        ids32, mask32 = p["input_ids"].cuda(), p["attention_mask"].cuda()
+        for _ in range(2):
+            eng.forward(ids32, mask32, 0)
+        out["B32_tokens"] = int(ids32.shape[0] * ids32.shape[1])
+    if "ttsd" in shapes:
+        long = torch.from_numpy(direct_prompt(rng, 2117)[None]).cuda()
+        for _ in range(2):
+            eng.forward(long, torch.ones(1, long.shape[1], dtype=torch.uint8, device="cuda"), 0)
+        out["ttsd_tokens"] = int(long.shape[1])
     torch.cuda.synchronize()
-    print(json.dumps({"B1_tokens": int(one.shape[1]), "B32_tokens": int(ids32.shape[0] * ids32.shape[1])}))
+    print(json.dumps(out))
     eng.close()
 
 
@@ -51,7 +63,7 @@ def summarize(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
             k = r["Kernel_Name"].split("(")[0]
-            if "gemm" not in k:
+            if "gemm" not in k and "attn_prefill" not in k:
                 continue
             key = (k, r.get("Dispatch_Id", r.get("Correlation_Id", "")))
             per.setdefault(key, {})[r["Counter_Name"]] = per.setdefault(key, {}).get(r["Counter_Name"], 0.0) + \

@@ -202,9 +202,10 @@ def xpk_indices(M, K):
                                         (181, 4096, 12288, 1), (130, 1000, 512, 1), (192, 96, 1024, 2),
                                         (2048, 4096, 4096, 1), (2048, 1536, 2048, 2), (1024, 12288, 4096, 2),
                                         (2117, 4096, 4096, 1), (1500, 6144, 4096, 0), (3000, 1024, 512, 1),
-                                        (2117, 12288, 4096, 2)])
+                                        (2117, 12288, 4096, 2), (40, 4096, 4096, 1), (100, 6144, 4096, 0),
+                                        (120, 12288, 4096, 2), (64, 4096, 12288, 1)])
 def test_gemm_packed_prefill(N, M, Nr, K, epi):
-    """Prefill GEMM on fragment-packed activations (the engine's >= 128-row prompts) at the 8B
+    """Prefill GEMM on fragment-packed activations (the engine's >= 33-row prompts) at the 8B
     projections' shapes: 181 rows take gemm3's one-token-block form (split K for q|k|v, o_proj,
     down), 2,048 the 256 / 128-row blocks; the gate|up output packed for the down projection.
     Oracle linear + epilogues within 2 bf16 ulp (rows' scale / 4 floor), the residual epilogue's
