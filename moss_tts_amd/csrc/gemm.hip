@@ -539,6 +539,7 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm3_kernel(GemvArgs a) {
 #ifndef G5S_R
 #define G5S_R 4  // k steps in flight of the <= 192-row form (A/B)
 #endif
+
 template <int NWR, int NWN, int WR, int R>
 constexpr size_t gemm5_lds_bytes() { return (size_t)(R + 1) * NWR * WR * 1024; }
 template <int NWR, int NWN, int WR, int WN, int R, int EPI, bool SPLIT = false>
@@ -625,16 +626,23 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm5_kernel(GemvArgs a) {
   gemm_tile_epilogue<WR, WN, EPI, SPLIT>(a, acc, rb0 + wr * WR, tb0 + wn * WN, lane);
 }
 
+// split-K ways of a gemm5 launch of `blocks` workgroups: doubled until the grid covers `cover` or a
+// split would drop below `mink` k tiles (row-major outputs with a partials workspace only)
+static int gemm5_splits(const GemvArgs& a, int blocks, int cover, int mink) {
+  int S = 1;
+  if (!a.y_packed && a.ws) {
+    while (blocks * S < cover && a.KT / (2 * S) >= mink) S *= 2;
+    while (S > 1 && (a.KT % S || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
+  }
+  return S;
+}
+
 template <int NWR, int NWN, int WR, int WN, int R, int EPI>
 static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
   constexpr int BR = NWR * WR, BT = NWN * WN;
   const size_t lds = gemm5_lds_bytes<NWR, NWN, WR, R>();
   const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
-  int S = 1;
-  if (!a.y_packed && a.ws) {
-    while ((int)(grid.x * grid.y) * S < cover && a.KT / (2 * S) >= mink) S *= 2;
-    while (S > 1 && (a.KT % S || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
-  }
+  const int S = gemm5_splits(a, (int)(grid.x * grid.y), cover, mink);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm5_kernel<NWR, NWN, WR, WN, R, EPI, false>,
@@ -644,8 +652,8 @@ static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
     attr = true;
   }
   if (S > 1) {
-    hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>), dim3(grid.x, grid.y, S), dim3(NWR * NWN * 64),
-                       lds, s, a);
+    hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>), dim3(grid.x, grid.y, S),
+                       dim3(NWR * NWN * 64), lds, s, a);
     const int n = a.B * ((a.N + 15) / 16) * 4;
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
   } else {
@@ -705,7 +713,22 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   static const int g5 = getenv("MTTS_GEMM5") ? atoi(getenv("MTTS_GEMM5")) : 1;
   // MTTS_GEMM5_SMALL_COVER (A/B): workgroups the split-K aims for
   static const int small_cover = getenv("MTTS_GEMM5_SMALL_COVER") ? atoi(getenv("MTTS_GEMM5_SMALL_COVER")) : 256;
-  if (a.pk_tiles <= small_max && g5) return gemm5_launch<1, 6, 6, 2, G5S_R, EPI>(a, small_cover, small_mink, s);
+  // two shapes: 6 waves x 2 token tiles on 96-row blocks, or 4 waves x 3 on 128-row blocks (one wave a
+  // SIMD: the same MFMA time per k step for 8 row tiles instead of 6).  Taken by rounds over the
+  // CUs x k steps per block (ties: the 96-row form); the 128-row form gives o_proj / down 256 split
+  // blocks where the 96-row form had 344: 181-row prompt 33.2 -> 23.5 us (profiles/r05_m_*).
+  // MTTS_GEMM5_SMALL_SHAPE=1 / 2 forces one (A/B).
+  static const int small_shape = getenv("MTTS_GEMM5_SMALL_SHAPE") ? atoi(getenv("MTTS_GEMM5_SMALL_SHAPE")) : 0;
+  if (a.pk_tiles <= small_max && g5) {
+    auto cost = [&](int br) {
+      const int rb = (a.n_row_tiles + br - 1) / br;
+      const int S = gemm5_splits(a, rb, small_cover, small_mink);
+      return (long)((rb * S + 255) / 256) * (a.KT / S);
+    };
+    const bool four = small_shape ? small_shape == 2 : cost(8) < cost(6);
+    if (four) return gemm5_launch<1, 4, 8, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
+    return gemm5_launch<1, 6, 6, 2, G5S_R, EPI>(a, small_cover, small_mink, s);
+  }
   if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, G3S_NST, EPI>(a, 256, small_mink, s);
   // MTTS_GEMM5_LONG (A/B, 0: gemm3): the long-prompt shapes with split paths as well -- batch-4 prefill
   // 18.6 -> 17.5 ms, 1,024 rows 27.7 -> 26.6, TTSD long form 75.2 -> 71.6, 32 utterances unchanged
