@@ -51,12 +51,12 @@ def test_errors_map_to_reference_exceptions():
 
 def test_packed_gemm_argument_checks():
     """mtts_k_gemm_packed refuses shapes its kernels do not take, before any device call:
-    K % 64 != 0, fewer than 128 rows, a packed output for a non-SwiGLU epilogue."""
+    K % 64 != 0, fewer than 33 rows, a packed output for a non-SwiGLU epilogue."""
     from moss_tts_amd import _native
     if not os.path.exists(_native.lib_path()):
         pytest.skip("libmtts.so not built")
     L = _native.load()
-    for M, K, epi, ypk in [(181, 96, 0, 0), (100, 4096, 0, 0), (181, 4096, 1, 1), (181, 4096, 7, 0)]:
+    for M, K, epi, ypk in [(181, 96, 0, 0), (32, 4096, 0, 0), (181, 4096, 1, 1), (181, 4096, 7, 0)]:
         with pytest.raises(ValueError):
             _native.check(L.mtts_k_gemm_packed(None, None, None, 16, ypk, None, 16, M, 16, K, epi, None, 1, None, 0,
                                                None), "gemm_packed")
