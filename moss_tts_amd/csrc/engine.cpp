@@ -577,12 +577,28 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
   const int pkT = (S > 1 && M >= pk_min && e->xpack && !e->gemv_prefill && !e->old_prefill_attn &&
                    M >= gemm_min_rows() && (M + 15) / 16 * 16 <= st.rows) ? (M + 15) / 16 : 0;
   const int ntiles = xpk ? 2 : pkT;  // packed activations of this call (0: row-major)
+  // packed split prefills: the residual GEMMs' split-K reduce also writes the next op's normed,
+  // packed input (GemvArgs::pn_w; MTTS_FUSE_PN=0 for A/B), and that op skips its rmsnorm_ss
+  static const bool fuse_pn = !getenv("MTTS_FUSE_PN") || getenv("MTTS_FUSE_PN")[0] != '0';
+  int xn_ready = 0;  // st.xn holds the next op's normed packed input
+  auto input = [&](GemvArgs& g, const bf16_t* nw) -> int {
+    if (xn_ready) {
+      g.x = st.xn; g.ldx = H; g.x_packed = 1; g.pk_tiles = pkT;
+      xn_ready = 0;
+      return 0;
+    }
+    return normed_input(e, st, g, nw, M, s, ntiles);
+  };
+  auto fuse_next = [&](GemvArgs& g, const bf16_t* nw) {
+    if (!fuse_pn || pkT <= 2 || !nw) return;
+    g.pn_w = nw; g.pn_y = st.xn; g.pn_tiles = pkT; g.pn_eps = eps; g.pn_done = &xn_ready;
+  };
   for (int l = 0; l < st.layers; ++l) {
     const LayerW& w = st.L[l];
     bf16_t* kc = st.kc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     bf16_t* vc = st.vc + l * st.layer_kv + (size_t)b0 * Hkv * st.Cmax * D;
     GemvArgs g = gemv_args(w.qkv, st.xn, H, st.qkvb, st.qkv_rows, M, st.qkv_rows, H);
-    if (int rc = normed_input(e, st, g, w.in_norm, M, s, ntiles)) return rc;
+    if (int rc = input(g, w.in_norm)) return rc;
     g.force_nw = e->nw[0]; g.force_u = e->nu[0];
     DecAttnArgs da{};
     da.qkv = st.qkvb; da.qn_w = w.q_norm; da.kn_w = w.k_norm; da.cos_t = st.cos_t; da.sin_t = st.sin_t;
@@ -624,15 +640,17 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
       g.attn.ns = (st.Cmax + g.attn.kb - 1) / g.attn.kb;
       g.attn.po_max = attn_publish_max_splits();
     }
+    fuse_next(g, w.post_norm);
     HIPCHK(proj(e, g, EPI_RESADD, s));
     g = gemv_args(w.gu, st.xn, H, st.act, I, M, I, H);
-    if (int rc = normed_input(e, st, g, w.post_norm, M, s, ntiles)) return rc;
+    if (int rc = input(g, w.post_norm)) return rc;
     g.force_nw = e->nw[2]; g.force_u = e->nu[2];
     g.y_packed = ntiles ? 1 : 0;
     HIPCHK(proj(e, g, EPI_SWIGLU, s));
     g = gemv_args(w.down, st.act, I, st.h, H, M, H, I);
     g.res = st.h; g.ldres = H; g.ss_out = st.ss; g.ld_ss_out = NT; g.force_nw = e->nw[3]; g.force_u = e->nu[3];
     g.x_packed = ntiles ? 1 : 0; g.pk_tiles = pkT;
+    if (l + 1 < st.layers) fuse_next(g, st.L[l + 1].in_norm);
     HIPCHK(proj(e, g, EPI_RESADD, s));
   }
   return 0;

@@ -324,6 +324,66 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
   }
 }
 
+// The residual split-K reduce fused with the next op's input RMSNorm (GemvArgs::pn_w): one block
+// per token row, thread t owns columns 8t .. 8t + 7.  Bit-identical to gemm_splitk_reduce<EPI_RESADD>
+// followed by rmsnorm_ss_kernel: the partials are summed in split order per column, the 16-column
+// sums of squares are formed as the reduce forms them ((c0^2 + c1^2) + (c2^2 + c3^2) per quad, quads
+// added pairwise), and the row statistic is rmsnorm_ss's (4 tiles per lane, then wave_sum).  Saves
+// the norm's launch after o_proj and after down_proj of every packed split prefill layer.
+__global__ __launch_bounds__(512) void gemm_splitk_reduce_norm(GemvArgs a, int S) {
+  __shared__ float tss[256];
+  const int m = blockIdx.x, t = threadIdx.x, lane = t & 63;
+  const int H = a.N, n0 = 8 * t;
+  const bool ok = n0 < H;
+  const size_t ld = (size_t)a.n_row_tiles * 16;
+  const float* p = a.ws + (size_t)m * ld + n0;
+  const size_t zs = (size_t)a.B * ld;
+  f32x4 g0 = (f32x4){0.f, 0.f, 0.f, 0.f}, g1 = g0;
+  if (ok)
+    for (int z = 0; z < S; ++z) {
+      g0 += *reinterpret_cast<const f32x4*>(p + z * zs);
+      g1 += *reinterpret_cast<const f32x4*>(p + z * zs + 4);
+    }
+  float v[8], w[8];
+  if (ok) {
+    float r8[8];
+    unpack8(*reinterpret_cast<const uint4*>(a.res + (size_t)m * a.ldres + n0), r8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[i] = rbf(r8[i] + rbf(g0[i]));
+      v[4 + i] = rbf(r8[4 + i] + rbf(g1[i]));
+    }
+    unpack8(*reinterpret_cast<const uint4*>(a.pn_w + n0), w);
+    uint4 o;
+    o.x = pack2(v[0], v[1]); o.y = pack2(v[2], v[3]); o.z = pack2(v[4], v[5]); o.w = pack2(v[6], v[7]);
+    *reinterpret_cast<uint4*>(a.y + (size_t)m * a.ldy + n0) = o;
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = w[i] = 0.f;
+  }
+  // 16-column tile sums of squares: quads as the reduce forms them, the two halves of a tile
+  // in threads 2u, 2u + 1
+  float s4 = ((v[0] * v[0] + v[1] * v[1]) + (v[2] * v[2] + v[3] * v[3])) +
+             ((v[4] * v[4] + v[5] * v[5]) + (v[6] * v[6] + v[7] * v[7]));
+  s4 += __shfl_xor(s4, 1, 64);
+  if (ok && (t & 1) == 0) {
+    tss[t >> 1] = s4;
+    if (a.ss_out) a.ss_out[(size_t)m * a.ld_ss_out + (t >> 1)] = s4;
+  }
+  __syncthreads();
+  float sw = 0.f;
+  for (int t4 = lane * 4; t4 < (H >> 4); t4 += 256) sw += (tss[t4] + tss[t4 + 1]) + (tss[t4 + 2] + tss[t4 + 3]);
+  sw = wave_sum(sw);
+  const float r = 1.0f / sqrtf(sw / (float)H + a.pn_eps);
+  if (!ok) return;
+  float q[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) q[i] = w[i] * rbf(v[i] * r);
+  uint4 o;
+  o.x = pack2(q[0], q[1]); o.y = pack2(q[2], q[3]); o.z = pack2(q[4], q[5]); o.w = pack2(q[6], q[7]);
+  *reinterpret_cast<uint4*>(a.pn_y + xpkT_index(m, n0, a.pn_tiles)) = o;
+}
+
 // split count for a short prompt: the GEMM's per-workgroup latency is ~constant in N, so
 // split K until the grid covers the CUs (cdna_hip_programming.md "Projection GEMM at M = 256"),
 // keeping >= 16 k-tiles per split and the partials inside the workspace
@@ -654,6 +714,11 @@ static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
   if (S > 1) {
     hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>), dim3(grid.x, grid.y, S),
                        dim3(NWR * NWN * 64), lds, s, a);
+    if (EPI == EPI_RESADD && a.pn_w && a.N % 16 == 0 && a.N <= 4096 && a.ldres % 8 == 0 && a.ldy % 8 == 0) {
+      hipLaunchKernelGGL(gemm_splitk_reduce_norm, dim3(a.B), dim3(a.N / 8), 0, s, a, S);
+      if (a.pn_done) *a.pn_done = 1;
+      return hipGetLastError();
+    }
     const int n = a.B * ((a.N + 15) / 16) * 4;
     hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
   } else {

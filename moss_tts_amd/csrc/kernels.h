@@ -76,6 +76,15 @@ struct GemvArgs {
   // next adapter's gate|up directly (no separate embed launch); nullptr: x rows are contiguous
   const int64_t* xtok;
   int ld_xtok;
+  // prefill split-K residual GEMM (EPI_RESADD, packed): when pn_w != nullptr and the launch splits
+  // K, its reduce also applies the NEXT op's input Qwen3RMSNorm (weight pn_w, eps pn_eps) to the
+  // new residual rows and writes them packed (xpkT_index, pn_tiles token tiles) to pn_y, and sets
+  // the host flag *pn_done = 1 (the caller then skips its rmsnorm_ss launch)
+  const bf16_t* pn_w;
+  bf16_t* pn_y;
+  int pn_tiles;
+  float pn_eps;
+  int* pn_done;
 };
 
 // Fragment-packed activations of the 17-32 row decode GEMVs: the MFMA B-operand order of
