@@ -611,17 +611,25 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
     da.out_packed = xpk ? 1 : 0;
     da.nwv_force = dec_nwv;
     da.Hq = Hq; da.Hkv = Hkv; da.D = D; da.Cmax = st.Cmax; da.eps = eps; da.scale = 1.0f / std::sqrt((float)D);
+    QKRopeArgs qa{};
+    qa.qkv = st.qkvb; qa.q_out = st.qb; qa.kc = kc; qa.vc = vc;
+    qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = st.cos_t; qa.sin_t = st.sin_t;
+    qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = st.Cmax; qa.eps = eps; qa.M = M;
+    qa.rope_off = st.rope_off ? st.rope_off + b0 : nullptr;
+    // packed split prefills: the q|k|v reduce runs the q/k norm + RoPE + KV append itself
+    // (MTTS_FUSE_QKR=0 for A/B)
+    static const bool fuse_qkr = !getenv("MTTS_FUSE_QKR") || getenv("MTTS_FUSE_QKR")[0] != '0';
+    int qk_done = 0;
+    if (fuse_qkr && S > 1 && pkT > 2 && D == 128 && st.cos_t) {
+      g.qkr = &qa;
+      g.qkr_done = &qk_done;
+    }
     HIPCHK(proj(e, g, EPI_STORE, s));
     if (S == 1) {
       HIPCHK(attn_decode(da, B, s));
     } else {
       if (!st.cos_t) return fail(MTTS_E_UNSUPPORTED, "multi-token forward of a stack without positions");
-      QKRopeArgs qa;
-      qa.qkv = st.qkvb; qa.q_out = st.qb; qa.kc = kc; qa.vc = vc;
-      qa.qn_w = w.q_norm; qa.kn_w = w.k_norm; qa.cos_t = st.cos_t; qa.sin_t = st.sin_t;
-      qa.pos_base = pos_base; qa.S = S; qa.Hq = Hq; qa.Hkv = Hkv; qa.D = D; qa.Cmax = st.Cmax; qa.eps = eps; qa.M = M;
-      qa.rope_off = st.rope_off ? st.rope_off + b0 : nullptr;
-      HIPCHK(qk_norm_rope(qa, s));
+      if (!qk_done) HIPCHK(qk_norm_rope(qa, s));
       AttnArgs aa;
       aa.q = st.qb; aa.kc = kc; aa.vc = vc; aa.mask = st.mask + (size_t)b0 * st.Cmax; aa.pos_base = pos_base;
       aa.part_o = st.part; aa.part_ml = st.part + (size_t)M * n_split * Hq * D; aa.out = st.attnb;

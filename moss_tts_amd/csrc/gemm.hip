@@ -15,6 +15,7 @@
 #include <cstdlib>
 
 #include "kernels.h"
+#include "qk_item.h"
 
 namespace mtts {
 
@@ -384,6 +385,31 @@ __global__ __launch_bounds__(512) void gemm_splitk_reduce_norm(GemvArgs a, int S
   *reinterpret_cast<uint4*>(a.pn_y + xpkT_index(m, n0, a.pn_tiles)) = o;
 }
 
+// The q|k|v split-K reduce fused with the q/k norm + RoPE + KV append (GemvArgs::qkr, D = 128):
+// one block per token row, 16 threads per head (thread t: head t / 16, dims 8 (t % 16) ..), the
+// partials summed in split order and rounded to bf16 as gemm_splitk_reduce<EPI_STORE> writes them,
+// then qk_item_d128 exactly as qk_norm_rope's per-item form runs it on those values.  Saves the
+// separate q|k|v write + read and one launch per packed split prefill layer.
+__global__ __launch_bounds__(1024) void gemm_splitk_reduce_qkrope(GemvArgs a, int S, QKRopeArgs q) {
+  const int m = blockIdx.x, t = threadIdx.x;
+  const int hd = t >> 4, l16 = t & 15, n0 = 8 * t;
+  const size_t ld = (size_t)a.n_row_tiles * 16;
+  const float* p = a.ws + (size_t)m * ld + n0;
+  const size_t zs = (size_t)a.B * ld;
+  f32x4 g0 = (f32x4){0.f, 0.f, 0.f, 0.f}, g1 = g0;
+  for (int z = 0; z < S; ++z) {
+    g0 += *reinterpret_cast<const f32x4*>(p + z * zs);
+    g1 += *reinterpret_cast<const f32x4*>(p + z * zs + 4);
+  }
+  float x[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    x[i] = rbf(g0[i]);
+    x[4 + i] = rbf(g1[i]);
+  }
+  qk_item_d128(q, m, hd, l16, x, true);
+}
+
 // split count for a short prompt: the GEMM's per-workgroup latency is ~constant in N, so
 // split K until the grid covers the CUs (cdna_hip_programming.md "Projection GEMM at M = 256"),
 // keeping >= 16 k-tiles per split and the partials inside the workspace
@@ -714,6 +740,11 @@ static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
   if (S > 1) {
     hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>), dim3(grid.x, grid.y, S),
                        dim3(NWR * NWN * 64), lds, s, a);
+    if (EPI == EPI_STORE && a.qkr && a.qkr->D == 128 && a.N == (a.qkr->Hq + 2 * a.qkr->Hkv) * 128 && a.N <= 8192) {
+      hipLaunchKernelGGL(gemm_splitk_reduce_qkrope, dim3(a.B), dim3(a.N / 8), 0, s, a, S, *a.qkr);
+      if (a.qkr_done) *a.qkr_done = 1;
+      return hipGetLastError();
+    }
     if (EPI == EPI_RESADD && a.pn_w && a.N % 16 == 0 && a.N <= 4096 && a.ldres % 8 == 0 && a.ldy % 8 == 0) {
       hipLaunchKernelGGL(gemm_splitk_reduce_norm, dim3(a.B), dim3(a.N / 8), 0, s, a, S);
       if (a.pn_done) *a.pn_done = 1;

@@ -85,6 +85,11 @@ struct GemvArgs {
   int pn_tiles;
   float pn_eps;
   int* pn_done;
+  // prefill split-K q|k|v GEMM (EPI_STORE, D = 128): when qkr != nullptr (host pointer) and the
+  // launch splits K, its reduce runs the q/k norm + RoPE + KV append of *qkr straight from the
+  // partials (y is not written) and sets the host flag *qkr_done = 1
+  const struct QKRopeArgs* qkr;
+  int* qkr_done;
 };
 
 // Fragment-packed activations of the 17-32 row decode GEMVs: the MFMA B-operand order of
