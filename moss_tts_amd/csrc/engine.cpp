@@ -712,7 +712,7 @@ int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const
 // row at a time in position chunks of max_prefill_tokens (each chunk attends to the cache the
 // previous ones wrote; only the last chunk evaluates the heads) -- the long-form (TTSD) path.
 int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s,
-                    bf16_t* hidden, int n_embed) {
+                    bf16_t* hidden, int n_embed, const int* text_gate) {
   const mtts_config& c = e->c;
   const int C = c.n_vq + 1;
   const int CH = S == 1 ? CH_DECODE : CH_PREFILL;
@@ -725,7 +725,7 @@ int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, 
         const int n_split = (past + s0 + len + CH - 1) / CH;
         const bool last = s0 + len == S;
         int rc = forward_rows(e, ids + ((size_t)b * S + s0) * C, b, 1, len, e->d_pos, CH, n_split,
-                              logits_out ? logits_out + (size_t)b * e->heads_ld : nullptr, s, nullptr,
+                              logits_out ? logits_out + (size_t)b * e->heads_ld : nullptr, s, text_gate,
                               last && !hidden, last && hidden ? hidden + (size_t)b * c.hidden : nullptr, n_embed);
         if (rc) return rc;
       }
@@ -738,7 +738,7 @@ int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, 
   for (int b0 = 0; b0 < B; b0 += rows_per) {
     const int nb = std::min(rows_per, B - b0);
     int rc = forward_rows(e, ids + (size_t)b0 * S * C, b0, nb, S, e->d_pos, CH, n_split,
-                          logits_out ? logits_out + (size_t)b0 * e->heads_ld : nullptr, s, nullptr, !hidden,
+                          logits_out ? logits_out + (size_t)b0 * e->heads_ld : nullptr, s, text_gate, !hidden,
                           hidden ? hidden + (size_t)b0 * c.hidden : nullptr, n_embed);
     if (rc) return rc;
   }
@@ -964,7 +964,8 @@ extern "C" int mtts_generate_begin(mtts_engine* e, const int64_t* ids, const uin
   HIPCHK(gen_init(e->bufs(), ids, mask, B, T, c.n_vq + 1, s));
   e->pse_choose(T);  // (a prefill takes the launch only as a one-token prompt)
   e->long_now = e->attn_long_ctx > 0 && T > e->attn_long_ctx;
-  int rc = forward_chunked(e, ids, B, T, 0, e->logits, s);
+  // the step-0 text rows only when some row continues in text mode (gen_init sets need_text)
+  int rc = forward_chunked(e, ids, B, T, 0, e->logits, s, nullptr, 0, e->full_text_head ? nullptr : &e->st->need_text);
   if (rc) return rc;
   HIPCHK(sample_step(e->bufs(), B, c.n_vq, TEXT_PARTS, s));
   e->steps_issued = 1;

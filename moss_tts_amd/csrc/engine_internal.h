@@ -209,8 +209,10 @@ int run_layers(mtts_engine* e, const Stack& st, int b0, int B, int S, const int*
 int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const int* pos_base, int CH, int n_split,
                  bf16_t* logits_out, hipStream_t s, const int* text_gate = nullptr, bool heads = true,
                  bf16_t* hidden = nullptr, int n_embed = 0);
+// text_gate: device flag gating the heads' text rows below the special ids (generate_begin's
+// prefill: GenDev::need_text); nullptr: every head row
 int forward_chunked(mtts_engine* e, const int64_t* ids, int B, int S, int past, bf16_t* logits_out, hipStream_t s,
-                    bf16_t* hidden = nullptr, int n_embed = 0);
+                    bf16_t* hidden = nullptr, int n_embed = 0, const int* text_gate = nullptr);
 hipStream_t enter(mtts_engine* e, void* user);
 bool pse_tripped(mtts_engine* e, hipStream_t s);
 void leave(mtts_engine* e, void* user);

@@ -325,11 +325,15 @@ __global__ __launch_bounds__(256) void gen_init_kernel(GenBufs g, const int64_t*
       g.is_audio[b] = am;
       g.is_stopping[b] = 0;
       g.delayed[b] = I64MAX;
+      // step 0: every row samples its text channel; an audio-mode row reads only gen_slot /
+      // delay_slot (the special-id tiles), so the prefill's full text head is needed only when
+      // some row continues in text mode (need_text starts at 0, host-initialised; it gates the
+      // prefill heads' text rows as it gates each decode step's)
+      if (!am) atomicOr(&st.need_text, 1);
       if (b == 0) {
         st.step = 0;
         st.done_step = -1;
         st.fwd_pos = 0;
-        st.need_text = 1;  // step 0 samples from the prefill's full logits
         st.text_head_steps = 0;
       }
     }
