@@ -431,11 +431,12 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
         assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), (CH, err.max())
 
 
-@pytest.mark.parametrize("S,past,B,Cmax", [(512, 0, 1, 512), (600, 37, 2, 704), (1100, 0, 1, 1152), (777, 300, 1, 1088)])
+@pytest.mark.parametrize("S,past,B,Cmax", [(512, 0, 1, 512), (600, 37, 2, 704), (1100, 0, 1, 1152), (777, 300, 1, 1088),
+                                          (181, 0, 1, 256), (100, 29, 2, 192), (64, 0, 1, 64)])
 def test_attention_prefill_long(N, S, past, B, Cmax):
-    """Long prompts take the 32-token LDS-staged flash kernel (attention.hip attn_prefill32_kernel,
-    S >= MTTS_ATTN_PF32_MIN = 512 query tokens, 4 query heads per KV head, D = 128): ragged tail
-    tiles, a cached prefix, left padding on row 1 and uninitialised (NaN) cache rows past the prompt."""
+    """Prompts of >= MTTS_ATTN_PF32_MIN = 64 query tokens take the 32-token LDS-staged flash kernel
+    (attention.hip attn_prefill32_kernel, 4 query heads per KV head, D = 128): ragged tail tiles,
+    a cached prefix, left padding on row 1 and uninitialised (NaN) cache rows past the prompt."""
     rng = np.random.default_rng(S + past)
     ctx = O._Ctx("bf16")
     D, Hq, Hkv = 128, 32, 8
