@@ -795,12 +795,15 @@ static hipError_t gemm3_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
   return hipGetLastError();
 }
 
-// gemm3 shape by prompt rows: <= 192 token rows (12 tiles) one token block of 96-row blocks, split
-// to >= 256 workgroups (q|k|v 4, o_proj / down 8 ways); longer prompts 256-row blocks for the wide
-// matrices, 128 for N 4,096 (o_proj / down), split to >= 128 workgroups
+// gemm3 shape by prompt rows: <= 384 token rows (24 tiles) token blocks of 192 rows on 96- / 128-row
+// weight blocks, split to >= 256 workgroups (q|k|v 4, o_proj / down 8 ways); longer prompts 256-row
+// blocks for the wide matrices, 128 for N 4,096 (o_proj / down), split to >= 128 workgroups
 template <int EPI>
 static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
-  static const int small_max = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 12;
+  // (24 since round 5: 193-384 rows as two token blocks of the small form rather than the long forms:
+  // 300 rows 10.9 -> 9.0 ms, 2 x 181 11.0 -> 9.4, 384 rows 11.1 -> 9.7; 32 tiles slower,
+  // profiles/r05_r_*)
+  static const int small_max = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 24;
   static const int small_mink = getenv("MTTS_GEMM3_SMALL_MINK") ? atoi(getenv("MTTS_GEMM3_SMALL_MINK")) : 8;  // A/B
   static const int wide_min = getenv("MTTS_GEMM3_WIDE") ? atoi(getenv("MTTS_GEMM3_WIDE")) : 1024;  // A/B
   // (a register-staged variant -- global -> VGPRs -> ds_write_b128, two LDS stages -- measured
@@ -816,10 +819,11 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // MTTS_GEMM5_SMALL_SHAPE=1 / 2 forces one (A/B).
   static const int small_shape = getenv("MTTS_GEMM5_SMALL_SHAPE") ? atoi(getenv("MTTS_GEMM5_SMALL_SHAPE")) : 0;
   if (a.pk_tiles <= small_max && g5) {
+    const int ty = (a.pk_tiles + 11) / 12;  // token blocks (both shapes take 12 token tiles)
     auto cost = [&](int br) {
       const int rb = (a.n_row_tiles + br - 1) / br;
-      const int S = gemm5_splits(a, rb, small_cover, small_mink);
-      return (long)((rb * S + 255) / 256) * (a.KT / S);
+      const int S = gemm5_splits(a, rb * ty, small_cover, small_mink);
+      return (long)((rb * ty * S + 255) / 256) * (a.KT / S);
     };
     const bool four = small_shape ? small_shape == 2 : cost(8) < cost(6);
     if (four) return gemm5_launch<1, 4, 8, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
@@ -900,13 +904,13 @@ hipError_t gemm_ex(const GemvArgs& a0, int epi, hipStream_t s) {
   if ((a0.x_packed || a0.y_packed) && ((a0.B < big && (a0.pk_tiles < 3 || a0.pk_tiles > 12)) || a0.K % 64 ||
                                        a0.pk_tiles * 16 < a0.B))
     return hipErrorInvalidValue;
-  // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged form (0: off, A/B).  From
-  // 512 rows since its k loop keeps NST - 1 stages in flight (a __syncthreads per k step had waited
-  // them all out): 724-row prefill 20.5 -> 18.7 ms, 1,024-row 29.2 -> 28.0 (profiles/r04_i_*); at
-  // 2,048 rows the 32-utterance prefill 127 -> 105 ms (profiles/r04_e_*)
-  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 512;
-  // (and prompts of <= 192 rows: gemm3's one-token-block form, MTTS_GEMM3_SMALL tiles, 0: off)
-  static const int g3small = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 12;
+  // packed activations of >= MTTS_GEMM3_MIN token rows: the LDS-staged forms (0: off, A/B).  Round 4
+  // took them from 512 rows (gemm3: 724-row prefill 20.5 -> 18.7 ms, profiles/r04_i_*); with the
+  // gemm5 forms from 193 (the 4 x 126-row batch prefill ran gemm2_kernel: 13.7 -> 11.1 ms,
+  // profiles/r05_r_*)
+  static const int g3min = getenv("MTTS_GEMM3_MIN") ? atoi(getenv("MTTS_GEMM3_MIN")) : 193;
+  // (and prompts of <= 384 rows: the small forms, MTTS_GEMM3_SMALL tiles, 0: off)
+  static const int g3small = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 24;
   if (g3min > 0 && a.x_packed && a.pk_tiles > 2 && (a.B >= g3min || a.pk_tiles <= g3small) && a.K % 64 == 0) {
     a.n_row_tiles = (epi == EPI_SWIGLU ? 2 : 1) * n_tiles;
     switch (epi) {
