@@ -12,6 +12,7 @@
 // its NBW activation fragments (B operands), then issues RT x NBW
 // v_mfma_f32_16x16x32_bf16.  The epilogue runs from registers: lane holds 4 consecutive
 // output columns of one token (MFMA C layout), so stores are 8-byte row segments.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels.h"
@@ -816,17 +817,27 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // SIMD: the same MFMA time per k step for 8 row tiles instead of 6).  Taken by rounds over the
   // CUs x k steps per block (ties: the 96-row form); the 128-row form gives o_proj / down 256 split
   // blocks where the 96-row form had 344: 181-row prompt 33.2 -> 23.5 us (profiles/r05_m_*).
-  // MTTS_GEMM5_SMALL_SHAPE=1 / 2 forces one (A/B).
+  // MTTS_GEMM5_SMALL_SHAPE=1 / 2 / 3 forces one (A/B).
   static const int small_shape = getenv("MTTS_GEMM5_SMALL_SHAPE") ? atoi(getenv("MTTS_GEMM5_SMALL_SHAPE")) : 0;
   if (a.pk_tiles <= small_max && g5) {
-    const int ty = (a.pk_tiles + 11) / 12;  // token blocks (both shapes take 12 token tiles)
-    auto cost = [&](int br) {
+    // cost = rounds of workgroups over the CUs x k steps per workgroup x MFMA cycles per k step on
+    // the busiest SIMD (relative): shape 1 <1,6,6,2> 96-row x 12-token blocks (2 waves x 12 MFMAs
+    // on two SIMDs: 2), shape 2 <1,4,8,3> 128 x 12 (1 x 24: 2), shape 3 <1,6,6,3> 96 x 18 (2 x 18:
+    // 3) -- one token block where 13-18 tiles needed two of 12
+    auto cost = [&](int br, int bt, int step) {
+      const int ty = (a.pk_tiles + bt - 1) / bt;
       const int rb = (a.n_row_tiles + br - 1) / br;
       const int S = gemm5_splits(a, rb * ty, small_cover, small_mink);
-      return (long)((rb * ty * S + 255) / 256) * (a.KT / S);
+      return (long)((rb * ty * S + 255) / 256) * (a.KT / S) * step;
     };
-    const bool four = small_shape ? small_shape == 2 : cost(8) < cost(6);
-    if (four) return gemm5_launch<1, 4, 8, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
+    int shape = small_shape;
+    if (shape < 1 || shape > 3) {
+      const long c1 = cost(6, 12, 2), c2 = cost(8, 12, 2), c3 = cost(6, 18, 3);
+      shape = c2 < c1 ? 2 : 1;
+      if (c3 < std::min(c1, c2)) shape = 3;
+    }
+    if (shape == 3) return gemm5_launch<1, 6, 6, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
+    if (shape == 2) return gemm5_launch<1, 4, 8, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
     return gemm5_launch<1, 6, 6, 2, G5S_R, EPI>(a, small_cover, small_mink, s);
   }
   if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, G3S_NST, EPI>(a, 256, small_mink, s);

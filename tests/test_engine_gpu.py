@@ -270,7 +270,7 @@ def test_packed_activations_17_32_rows(gpu, golden, unfused_norm):
         assert (np.abs(got[fin] - want[fin]) <= tol[fin]).all(), (s, float(np.abs(got[fin] - want[fin]).max()))
 
 
-@pytest.mark.parametrize("rows", [48, 100, 160, 300, 500, 1024])
+@pytest.mark.parametrize("rows", [48, 100, 160, 250, 300, 500, 1024])
 def test_packed_activations_long_prefill(gpu, golden, rows):
     """Prefills of >= 33 token rows keep the GEMM inputs fragment-packed (xpkT_index with
     T = M / 16 token tiles; split-K partial launches read them packed): logits bit-identical to
