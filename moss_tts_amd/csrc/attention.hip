@@ -373,7 +373,7 @@ __device__ __forceinline__ uint32_t pf_pack(float a, float b) {  // one v_cvt_pk
 
 template <int G, int D>
 __global__ __launch_bounds__(G * 64, 2) void attn_prefill32_kernel(AttnArgs a) {
-  static_assert(D == 128 && G == 4, "the 8B / 1.7B head shape: 4 waves copy 16 KiB chunks in 1 KiB rows");
+  static_assert(D == 128 && (G == 4 || G == 2), "the 8B (4 q heads per KV head) / 1.7B (2) head shapes");
   typedef __attribute__((address_space(3))) void lvoid;
   constexpr int QS = D / 32, DT = D / 16, TQ = 32, RT = TQ / 16;
   // the causal tiles' work grows with qt: dispatch the longest first
@@ -407,17 +407,18 @@ __global__ __launch_bounds__(G * 64, 2) void attn_prefill32_kernel(AttnArgs a) {
   // the fragment reads below (16 rows per 16 lanes) spread over all 64 banks.
   // distinct over each S^T tile's 16 keys (bits 0, 1, 3, 4 of the key's row in the chunk)
   auto kswz = [](int r) { return (r & 3) | ((r >> 1) & 12); };
+  // (G waves split the chunk: 32 / G keys and 128 / G V^T rows each, 8 / G instructions of each)
   auto issue = [&](int k0, int buf) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int kr = wave * 8 + i * 4 + (lane >> 4);        // 4 keys (256 B each) per instruction
+    for (int i = 0; i < 8 / G; ++i) {
+      const int kr = wave * (32 / G) + i * 4 + (lane >> 4);  // 4 keys (256 B each) per instruction
       const int key = k0 + kr;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          krs, (lvoid*)&ks[buf][wave * 8 + i * 4][0], 16,
+          krs, (lvoid*)&ks[buf][wave * (32 / G) + i * 4][0], 16,
           (key < Cmax) ? (uint32_t)(key * D * 2 + ((lane & 15) ^ kswz(kr)) * 16) : OOBA, 0, 0, 0);
-      const int d = wave * 32 + i * 16 + (lane >> 2);       // 16 dims (64 B each) per instruction
+      const int d = wave * (D / G) + i * 16 + (lane >> 2);  // 16 dims (64 B each) per instruction
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          vrs, (lvoid*)&vs[buf][wave * 32 + i * 16][0], 16,
+          vrs, (lvoid*)&vs[buf][wave * (D / G) + i * 16][0], 16,
           (k0 + 32 <= Cmax) ? (uint32_t)((d * Cmax + k0) * 2 + ((lane & 3) ^ ((d >> 2) & 3)) * 16) : OOBA, 0, 0, 0);
     }
     // the chunk's 32 mask bytes ride with it (a register load here would make the waitcnt before
@@ -587,9 +588,11 @@ template <int D>
 static hipError_t attn_prefill_d(const AttnArgs& a, int G, hipStream_t st) {
   const int B = a.M / a.S;
   if constexpr (D == 128) {
-    if (G == 4 && attn_pf32_min() > 0 && a.S >= attn_pf32_min()) {
+    if ((G == 4 || G == 2) && attn_pf32_min() > 0 && a.S >= attn_pf32_min()) {
       constexpr size_t PF32_LDS = 4 * 32 * D * 2 + 2 * 256;
-      hipLaunchKernelGGL((attn_prefill32_kernel<4, D>), dim3((a.S + 31) / 32, a.Hkv, B), dim3(256), PF32_LDS, st, a);
+      const dim3 grid((a.S + 31) / 32, a.Hkv, B);
+      if (G == 4) hipLaunchKernelGGL((attn_prefill32_kernel<4, D>), grid, dim3(256), PF32_LDS, st, a);
+      else hipLaunchKernelGGL((attn_prefill32_kernel<2, D>), grid, dim3(128), PF32_LDS, st, a);
       return hipGetLastError();
     }
   }

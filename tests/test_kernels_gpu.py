@@ -433,15 +433,17 @@ def test_qk_norm_rope_and_attention(N, S, past, D, Hq, Hkv):
         assert (err <= 4 * 2.0 ** -8 * np.maximum(np.abs(want), 1.0)).all(), (CH, err.max())
 
 
-@pytest.mark.parametrize("S,past,B,Cmax", [(512, 0, 1, 512), (600, 37, 2, 704), (1100, 0, 1, 1152), (777, 300, 1, 1088),
-                                          (181, 0, 1, 256), (100, 29, 2, 192), (64, 0, 1, 64)])
-def test_attention_prefill_long(N, S, past, B, Cmax):
+@pytest.mark.parametrize("S,past,B,Cmax,Hq", [(512, 0, 1, 512, 32), (600, 37, 2, 704, 32), (1100, 0, 1, 1152, 32),
+                                             (777, 300, 1, 1088, 32), (181, 0, 1, 256, 32), (100, 29, 2, 192, 32),
+                                             (64, 0, 1, 64, 32), (300, 0, 2, 320, 16), (130, 60, 1, 192, 16)])
+def test_attention_prefill_long(N, S, past, B, Cmax, Hq):
     """Prompts of >= MTTS_ATTN_PF32_MIN = 64 query tokens take the 32-token LDS-staged flash kernel
-    (attention.hip attn_prefill32_kernel, 4 query heads per KV head, D = 128): ragged tail tiles,
-    a cached prefix, left padding on row 1 and uninitialised (NaN) cache rows past the prompt."""
-    rng = np.random.default_rng(S + past)
+    (attention.hip attn_prefill32_kernel, D = 128): ragged tail tiles, a cached prefix, left padding
+    on row 1 and uninitialised (NaN) cache rows past the prompt.  Hq 32 / 16 over 8 KV heads: the 8B
+    and the MossTTSLocal 1.7B backbone shapes (4 / 2 waves a block)."""
+    rng = np.random.default_rng(S + past + Hq)
     ctx = O._Ctx("bf16")
-    D, Hq, Hkv = 128, 32, 8
+    D, Hkv = 128, 8
     M = B * S
     q = rand_bf16(rng, (B, S, Hq, D), 2.0)
     kc0 = rand_bf16(rng, (B, Hkv, Cmax, D))
