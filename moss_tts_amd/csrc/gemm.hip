@@ -806,7 +806,7 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // profiles/r05_r_*)
   static const int small_max = getenv("MTTS_GEMM3_SMALL") ? atoi(getenv("MTTS_GEMM3_SMALL")) : 24;
   static const int small_mink = getenv("MTTS_GEMM3_SMALL_MINK") ? atoi(getenv("MTTS_GEMM3_SMALL_MINK")) : 8;  // A/B
-  static const int wide_min = getenv("MTTS_GEMM3_WIDE") ? atoi(getenv("MTTS_GEMM3_WIDE")) : 1024;  // A/B
+  static const int wide_min = getenv("MTTS_GEMM3_WIDE") ? atoi(getenv("MTTS_GEMM3_WIDE")) : 512;  // A/B (1024 until round 5: the Local backbone gate|up, 768 row tiles, 14.4 -> 14.2 ms prefill)
   // (a register-staged variant -- global -> VGPRs -> ds_write_b128, two LDS stages -- measured
   // slower: 181 rows 7.97 -> 8.20 ms, 32 utterances 91.9 -> 95.7 ms, profiles/r04_j_*)
   // MTTS_GEMM5 (A/B): the split-path form for <= 12 token tiles

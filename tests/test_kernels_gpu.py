@@ -205,7 +205,7 @@ def xpk_indices(M, K):
                                         (2117, 12288, 4096, 2), (40, 4096, 4096, 1), (100, 6144, 4096, 0),
                                         (120, 12288, 4096, 2), (64, 4096, 12288, 1), (300, 4096, 4096, 1),
                                         (384, 12288, 4096, 2), (250, 6144, 4096, 0), (504, 4096, 12288, 1),
-                                        (288, 12288, 4096, 2), (210, 4096, 12288, 1)])
+                                        (288, 12288, 4096, 2), (210, 4096, 12288, 1), (600, 6144, 2048, 2)])
 def test_gemm_packed_prefill(N, M, Nr, K, epi):
     """Prefill GEMM on fragment-packed activations (the engine's >= 33-row prompts) at the 8B
     projections' shapes: 181 rows take gemm3's one-token-block form (split K for q|k|v, o_proj,
