@@ -692,7 +692,10 @@ int forward_rows(mtts_engine* e, const int64_t* ids, int b0, int B, int S, const
                       e->final_norm, e->xn, B, H, eps, s));
   }
   g.pad_start = c.vocab; g.pad_period = e->audio_rows; g.pad_off = e->audio_rows - 1;
-  g.force_nw = e->nw[4]; g.force_u = e->nu[4];
+  // decode at <= 16 rows: 4-wave blocks for the heads (B=4 3.052 -> 3.034 ms/step, B=1 even;
+  // profiles/r05_v_ab_heads_nw.txt); MTTS_NW's fifth entry overrides
+  g.force_nw = e->nw[4] ? e->nw[4] : (S == 1 && B <= 16 ? 4 : 0);
+  g.force_u = e->nu[4];
   if (text_gate && e->text_tile_lo > 0) {
     // decode: text rows below the special ids only when some row samples text freely.
     // Audio-mode rows see every text logit except gen_slot / delay_slot masked to -inf

@@ -32,7 +32,16 @@ size_t norm_lds_bytes(int B, int K) { return (size_t)(B + 1) * K * 2; }
 
 template <int NB, int RT, int EPI, int PRO, int NW, bool PIPE = false>
 __global__ __launch_bounds__(NW * 64) void gemv_kernel(GemvArgs a) {
-  if (a.gate && *a.gate == 0) return;
+  if (a.gate) {
+    // gated launch (the decode text head, off on most steps): a capped grid walks the tiles, so
+    // an off step dispatches a few hundred blocks instead of ~9,500 (7 us of dispatch per step)
+    if (*a.gate == 0) return;
+    for (int t = blockIdx.x; t < a.gate_tiles; t += gridDim.x) {
+      if (t != (int)blockIdx.x) __syncthreads();  // the previous tile's LDS reads are done
+      gemv_body<NB, RT, EPI, PRO, NW, PIPE>(a, t + a.tile0, [] {});
+    }
+    return;
+  }
   gemv_body<NB, RT, EPI, PRO, NW, PIPE>(a, (int)blockIdx.x + a.tile0, [] {});
 }
 
@@ -58,8 +67,17 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
+// gated launches (gemv_kernel): grid cap, MTTS_GATE_GRID (0: one block per tile)
+static int gate_grid(int n_tiles) {
+  static const int cap = getenv("MTTS_GATE_GRID") ? atoi(getenv("MTTS_GATE_GRID")) : 1024;
+  return cap > 0 ? std::min(n_tiles, cap) : n_tiles;
+}
+
 template <int NB, int RT, int EPI, int PRO>
-static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
+static void launch_nw(const GemvArgs& a0, int n_tiles, hipStream_t s) {
+  GemvArgs a = a0;
+  a.gate_tiles = n_tiles;
+  const int grid = a.gate ? gate_grid(n_tiles) : n_tiles;
   constexpr bool NORM = PRO == PRO_NORM || PRO == PRO_NORM_PRE || PRO == PRO_NORM_PREROW || PRO == PRO_NORM_DMA;
   // waves per block from the B=1/B=4 sweep (scripts/sweep_gemv.py, profiles/): 8 for the
   // large matrices (gate|up 6.1 TB/s, heads 7.0 TB/s), 16 for the <= 6144-row ones
@@ -82,14 +100,14 @@ static void launch_nw(const GemvArgs& a, int n_tiles, hipStream_t s) {
   if (EPI == EPI_SWIGLU && NB == 1 && a.KT <= 64 && !(pipe & 1)) u4 = true;
   if (a.force_u == 4 || a.force_u == 8) u4 = a.force_u == 4;
   if (u4) {
-    if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4, true>), dim3(n_tiles), dim3(256), lds, s, a);
-    if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8, true>), dim3(n_tiles), dim3(512), lds, s, a);
-    if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16, true>), dim3(n_tiles), dim3(1024), lds, s, a);
+    if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4, true>), dim3(grid), dim3(256), lds, s, a);
+    if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8, true>), dim3(grid), dim3(512), lds, s, a);
+    if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16, true>), dim3(grid), dim3(1024), lds, s, a);
     return;
   }
-  if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4>), dim3(n_tiles), dim3(256), lds, s, a);
-  if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8>), dim3(n_tiles), dim3(512), lds, s, a);
-  if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16>), dim3(n_tiles), dim3(1024), lds, s, a);
+  if (nw == 4) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 4>), dim3(grid), dim3(256), lds, s, a);
+  if (nw == 8) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 8>), dim3(grid), dim3(512), lds, s, a);
+  if (nw == 16) hipLaunchKernelGGL((gemv_kernel<NB, RT, EPI, PRO, 16>), dim3(grid), dim3(1024), lds, s, a);
 }
 
 // RT = 2 output tiles per block for the plain projections once the x fragments (B rows per

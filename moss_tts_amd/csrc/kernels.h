@@ -64,6 +64,7 @@ struct GemvArgs {
   int force_u;         // 0: automatic load-batch depth; 4/8 k-tiles per batch: forced (tuning)
   int tile0;           // first output row tile of this launch (row ranges of one matrix)
   const int* gate;     // device flag: the launch does nothing when *gate == 0 (nullptr: always on)
+  int gate_tiles;      // gated launch: output tiles, walked block-stride by a capped grid (set by launch_nw)
   int n_row_tiles;     // packed 16-row weight tiles (set by the GEMM launcher)
   AttnPartView attn;   // PRO_ATTN (o_proj): x is merged from these partials; attn.part == nullptr: off
   float* ws;           // prefill GEMM split-K workspace (gemm_ex; nullptr: no split)
@@ -199,6 +200,7 @@ struct GenDev {
   unsigned long long seed;
   MttsIds ids;
   int topk_overflow;  // a sampler cut threshold ties at TOPK_CAP (reported by poll)
+  int tsel_arrive;    // text_select blocks done this step (the last one runs the state update)
   ChSampling lch[LOCAL_MAXC];  // MossTTSLocal: per-channel processors
 };
 
