@@ -67,9 +67,11 @@ __global__ void pack_kernel(const bf16_t* __restrict__ src, bf16_t* __restrict__
 }
 
 // ---------------------------------------------------------------------------
-// gated launches (gemv_kernel): grid cap, MTTS_GATE_GRID (0: one block per tile)
+// gated launches (gemv_kernel): grid cap, MTTS_GATE_GRID (0: one block per tile; read per launch
+// so a test can make the small parity configs walk several tiles per block)
 static int gate_grid(int n_tiles) {
-  static const int cap = getenv("MTTS_GATE_GRID") ? atoi(getenv("MTTS_GATE_GRID")) : 1024;
+  const char* v = getenv("MTTS_GATE_GRID");
+  const int cap = v ? atoi(v) : 1024;
   return cap > 0 ? std::min(n_tiles, cap) : n_tiles;
 }
 

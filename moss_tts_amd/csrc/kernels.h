@@ -200,7 +200,6 @@ struct GenDev {
   unsigned long long seed;
   MttsIds ids;
   int topk_overflow;  // a sampler cut threshold ties at TOPK_CAP (reported by poll)
-  int tsel_arrive;    // text_select blocks done this step (the last one runs the state update)
   ChSampling lch[LOCAL_MAXC];  // MossTTSLocal: per-channel processors
 };
 

@@ -16,8 +16,7 @@
 //   text_select   (B)            greedy: merge slice argmaxes + allowed special ids under the
 //                                 step's masks; sampled: top-k over the whole masked row
 //                                 (topk.h radix select), top-p, draw
-//   finalize      (the last text_select block to finish) state update, next input ids,
-//                                 generation buffer, mask, stop
+//   finalize      (1 block)      state update, next input ids, generation buffer, mask, stop
 // Draws: Philox(seed; step, row, channel) uniforms through torch's bf16 softmax / cumsum
 // arithmetic (torch_draw); distribution-level parity, torch's RNG stream is not reproduced.
 #include <algorithm>
@@ -120,9 +119,9 @@ __device__ __forceinline__ bool samples_text(const GenBufs& g, int b) {
 //   sampled, audio mode: the two allowed ids {gen_slot, delay_slot} (delay banned at step 0);
 //   sampled, text mode: top-k over the whole masked row (radix select), then top-p + draw.
 constexpr int TSEL_NT = 1024;
-__device__ void text_select_body(const GenBufs& g, const int b) {
+__global__ __launch_bounds__(TSEL_NT) void text_select_kernel(GenBufs g) {
   const GenDev& st = *g.st;
-  const int t = threadIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x;
   if (!samples_text(g, b)) return;  // finalize does not read text_cand for this row
   const MttsIds& d = st.ids;
   const int step = st.step;
@@ -230,7 +229,7 @@ __device__ void audio_select_body(const GenBufs& g, int b, int j) {
 // updates the row's scalars; phase 2: one thread per (row, channel) writes the next input
 // ids, the generation buffer and the repetition-penalty history.
 constexpr int FIN_MAXB = 256;
-__device__ void finalize_body(const GenBufs& g) {
+__global__ __launch_bounds__(256) void finalize_kernel(GenBufs g) {
   GenDev& st = *g.st;
   const MttsIds& d = st.ids;
   const int n_vq = st.n_vq, C = st.C;
@@ -297,29 +296,6 @@ __device__ void finalize_body(const GenBufs& g) {
     st.fwd_pos = st.T0 + step;
     st.step = step + 1;
   }
-}
-
-// text decisions (one block per row), then the state update in the block that finishes last
-// (one launch fewer per step: the separate 1-block finalize launch cost ~5 us of a 3 ms step).
-// Release / acquire at agent scope: each row's text_cand is written by another block, possibly
-// on another XCD (its own L2).
-__global__ __launch_bounds__(TSEL_NT) void text_select_kernel(GenBufs g) {
-  text_select_body(g, blockIdx.x);
-  __shared__ int last;
-  __syncthreads();  // this block's text_cand store (thread 0) precedes its arrival
-  if (gridDim.x == 1) {  // batch 1: no arrival count (the block barrier orders its own stores)
-    finalize_body(g);
-    return;
-  }
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(&g.st->tsel_arrive, 1) == (int)gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;
-  __threadfence();
-  finalize_body(g);
-  if (threadIdx.x == 0) g.st->tsel_arrive = 0;  // the next step's (graph replay) count
 }
 
 // generate() prologue (modeling_moss_tts.py:417-440): per-row continuation state,
@@ -395,7 +371,8 @@ __global__ __launch_bounds__(256) void score_kernel(GenBufs g, int P) {
 hipError_t sample_step(const GenBufs& g, int B, int n_vq, int P, hipStream_t s) {
   if (B > FIN_MAXB) return hipErrorInvalidValue;
   hipLaunchKernelGGL(score_kernel, dim3(B, P + n_vq), dim3(256), 0, s, g, P);
-  hipLaunchKernelGGL(text_select_kernel, dim3(B), dim3(TSEL_NT), 0, s, g);  // + the state update
+  hipLaunchKernelGGL(text_select_kernel, dim3(B), dim3(TSEL_NT), 0, s, g);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, s, g);
   return hipGetLastError();
 }
 

@@ -112,7 +112,7 @@ def summarize_ttsd(d, cfg_name="ttsd"):
         for _, kname, _, v in seq:
             if "gemm" in kname and dec_seen:
                 seg, dec_seen = seg + 1, False
-            if "pse_kernel" in kname or "finalize" in kname or "text_select" in kname or "attn_decode" in kname or "lpse" in kname:
+            if "pse_kernel" in kname or "finalize" in kname or "attn_decode" in kname or "lpse" in kname:
                 dec_seen = True
             if 0 <= seg < 2:
                 tot[seg] += v

@@ -189,7 +189,9 @@ def test_decode_bitwise_deterministic(gpu, golden):
 def test_text_head_gating_is_exact(gpu, golden):
     """Decode evaluates the full text head only when some row samples text outside audio
     mode; generate() output must be bit-identical to evaluating it every step
-    (MTTS_FULL_TEXT_HEAD is read when an engine is created)."""
+    (MTTS_FULL_TEXT_HEAD is read when an engine is created).  The gated launch walks its tiles
+    from a capped grid (gemv.hip gate_grid): MTTS_GATE_GRID=3 makes each block of these small
+    configs take several tiles, as the 8B text head does at the default cap."""
     import os
     from moss_tts_amd.engine import sampling_params
     outs = []
@@ -197,16 +199,20 @@ def test_text_head_gating_is_exact(gpu, golden):
         g, c, cfg, W = case(golden, name)
         ids, mask = g[name + "/input_ids"], g[name + "/mask"]
         res = []
-        for flag in ("0", "1"):
+        for flag, grid in (("0", None), ("1", None), ("0", "3")):
             os.environ["MTTS_FULL_TEXT_HEAD"] = flag
+            if grid:
+                os.environ["MTTS_GATE_GRID"] = grid
             try:
                 eng = make_engine(cfg, W)
+                res.append(eng.generate_ids(torch.from_numpy(ids), torch.from_numpy(mask), 40,
+                                            sampling_params(text_temperature=0, audio_temperature=0)).cpu().numpy())
+                eng.close()
             finally:
                 os.environ.pop("MTTS_FULL_TEXT_HEAD")
-            res.append(eng.generate_ids(torch.from_numpy(ids), torch.from_numpy(mask), 40,
-                                        sampling_params(text_temperature=0, audio_temperature=0)).cpu().numpy())
-            eng.close()
-        assert res[0].shape == res[1].shape and (res[0] == res[1]).all(), name
+                os.environ.pop("MTTS_GATE_GRID", None)
+        for r in res[1:]:
+            assert r.shape == res[0].shape and (r == res[0]).all(), name
 
 
 @pytest.mark.parametrize("unfused_norm", ["0", "1"])
