@@ -274,8 +274,11 @@ static void gemm_launch(const GemvArgs& a, int n_tiles, hipStream_t s) {
 // 181-row o_proj / down reduce is 185 K threads, one f32x4 load per split each; one thread per tile
 // ran 12 us on 46 K latency-bound threads); the residual epilogue's per-tile sum of squares adds
 // the groups as the GEMM epilogue does, (s0 + s1) + (s2 + s3), across the 4 adjacent lanes.
-template <int EPI>
+// SS > 0: the split count as a compile-time constant, so every partial's load issues before the
+// first add (a runtime trip count kept one load pair in flight per round trip); 0: runtime S
+template <int EPI, int SS = 0>
 __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
+  if constexpr (SS > 0) S = SS;
   const int n_ot = (a.N + 15) / 16;
   const int id = blockIdx.x * 256 + threadIdx.x;
   const bool live = id < a.B * n_ot * 4;
@@ -286,6 +289,7 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
   const size_t zs = (size_t)a.B * ld;
   f32x4 g = (f32x4){0.f, 0.f, 0.f, 0.f}, u = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int c = (EPI == EPI_SWIGLU ? 2 * ot : ot) * 16 + q * 4;
+#pragma unroll
   for (int z = 0; z < S; ++z) {
     g += *reinterpret_cast<const f32x4*>(p + z * zs + c);
     if constexpr (EPI == EPI_SWIGLU) u += *reinterpret_cast<const f32x4*>(p + z * zs + c + 16);
@@ -332,7 +336,9 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
 // sums of squares are formed as the reduce forms them ((c0^2 + c1^2) + (c2^2 + c3^2) per quad, quads
 // added pairwise), and the row statistic is rmsnorm_ss's (4 tiles per lane, then wave_sum).  Saves
 // the norm's launch after o_proj and after down_proj of every packed split prefill layer.
+template <int SS = 0>
 __global__ __launch_bounds__(512) void gemm_splitk_reduce_norm(GemvArgs a, int S) {
+  if constexpr (SS > 0) S = SS;
   __shared__ float tss[256];
   const int m = blockIdx.x, t = threadIdx.x, lane = t & 63;
   const int H = a.N, n0 = 8 * t;
@@ -342,6 +348,7 @@ __global__ __launch_bounds__(512) void gemm_splitk_reduce_norm(GemvArgs a, int S
   const size_t zs = (size_t)a.B * ld;
   f32x4 g0 = (f32x4){0.f, 0.f, 0.f, 0.f}, g1 = g0;
   if (ok)
+#pragma unroll
     for (int z = 0; z < S; ++z) {
       g0 += *reinterpret_cast<const f32x4*>(p + z * zs);
       g1 += *reinterpret_cast<const f32x4*>(p + z * zs + 4);
@@ -391,13 +398,16 @@ __global__ __launch_bounds__(512) void gemm_splitk_reduce_norm(GemvArgs a, int S
 // partials summed in split order and rounded to bf16 as gemm_splitk_reduce<EPI_STORE> writes them,
 // then qk_item_d128 exactly as qk_norm_rope's per-item form runs it on those values.  Saves the
 // separate q|k|v write + read and one launch per packed split prefill layer.
+template <int SS = 0>
 __global__ __launch_bounds__(1024) void gemm_splitk_reduce_qkrope(GemvArgs a, int S, QKRopeArgs q) {
+  if constexpr (SS > 0) S = SS;
   const int m = blockIdx.x, t = threadIdx.x;
   const int hd = t >> 4, l16 = t & 15, n0 = 8 * t;
   const size_t ld = (size_t)a.n_row_tiles * 16;
   const float* p = a.ws + (size_t)m * ld + n0;
   const size_t zs = (size_t)a.B * ld;
   f32x4 g0 = (f32x4){0.f, 0.f, 0.f, 0.f}, g1 = g0;
+#pragma unroll
   for (int z = 0; z < S; ++z) {
     g0 += *reinterpret_cast<const f32x4*>(p + z * zs);
     g1 += *reinterpret_cast<const f32x4*>(p + z * zs + 4);
@@ -713,6 +723,18 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm5_kernel(GemvArgs a) {
   gemm_tile_epilogue<WR, WN, EPI, SPLIT>(a, acc, rb0 + wr * WR, tb0 + wn * WN, lane);
 }
 
+// launch KERNEL<..., SS> with the split count S as a compile-time constant when it is 2 / 4 / 8 / 16
+#define MTTS_SPLIT_DISPATCH(S, LAUNCH) \
+  do {                                 \
+    switch (S) {                       \
+      case 2: LAUNCH(2); break;        \
+      case 4: LAUNCH(4); break;        \
+      case 8: LAUNCH(8); break;        \
+      case 16: LAUNCH(16); break;      \
+      default: LAUNCH(0); break;       \
+    }                                  \
+  } while (0)
+
 // split-K ways of a gemm5 launch of `blocks` workgroups: doubled until the grid covers `cover` or a
 // split would drop below `mink` k tiles (row-major outputs with a partials workspace only)
 static int gemm5_splits(const GemvArgs& a, int blocks, int cover, int mink) {
@@ -742,17 +764,23 @@ static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
     hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, true>), dim3(grid.x, grid.y, S),
                        dim3(NWR * NWN * 64), lds, s, a);
     if (EPI == EPI_STORE && a.qkr && a.qkr->D == 128 && a.N == (a.qkr->Hq + 2 * a.qkr->Hkv) * 128 && a.N <= 8192) {
-      hipLaunchKernelGGL(gemm_splitk_reduce_qkrope, dim3(a.B), dim3(a.N / 8), 0, s, a, S, *a.qkr);
+#define L_(SS) hipLaunchKernelGGL(gemm_splitk_reduce_qkrope<SS>, dim3(a.B), dim3(a.N / 8), 0, s, a, S, *a.qkr)
+      MTTS_SPLIT_DISPATCH(S, L_);
+#undef L_
       if (a.qkr_done) *a.qkr_done = 1;
       return hipGetLastError();
     }
     if (EPI == EPI_RESADD && a.pn_w && a.N % 16 == 0 && a.N <= 4096 && a.ldres % 8 == 0 && a.ldy % 8 == 0) {
-      hipLaunchKernelGGL(gemm_splitk_reduce_norm, dim3(a.B), dim3(a.N / 8), 0, s, a, S);
+#define L_(SS) hipLaunchKernelGGL(gemm_splitk_reduce_norm<SS>, dim3(a.B), dim3(a.N / 8), 0, s, a, S)
+      MTTS_SPLIT_DISPATCH(S, L_);
+#undef L_
       if (a.pn_done) *a.pn_done = 1;
       return hipGetLastError();
     }
     const int n = a.B * ((a.N + 15) / 16) * 4;
-    hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
+#define L_(SS) hipLaunchKernelGGL((gemm_splitk_reduce<EPI, SS>), dim3((n + 255) / 256), dim3(256), 0, s, a, S)
+    MTTS_SPLIT_DISPATCH(S, L_);
+#undef L_
   } else {
     hipLaunchKernelGGL((gemm5_kernel<NWR, NWN, WR, WN, R, EPI, false>), grid, dim3(NWR * NWN * 64), lds, s, a);
   }
@@ -788,7 +816,9 @@ static hipError_t gemm3_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
     hipError_t e = hipLaunchKernel(k_split, dim3(grid.x, grid.y, S), block, args, lds, s);
     if (e != hipSuccess) return e;
     const int n = a.B * ((a.N + 15) / 16) * 4;
-    hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
+#define L_(SS) hipLaunchKernelGGL((gemm_splitk_reduce<EPI, SS>), dim3((n + 255) / 256), dim3(256), 0, s, a, S)
+    MTTS_SPLIT_DISPATCH(S, L_);
+#undef L_
   } else {
     hipError_t e = hipLaunchKernel(k_full, grid, block, args, lds, s);
     if (e != hipSuccess) return e;
@@ -894,7 +924,9 @@ static void gemm2_launch(GemvArgs a, hipStream_t s) {
   if (S > 1) {
     hipLaunchKernelGGL((gemm2_kernel<WR, WN, EPI, 4, true>), dim3(grid.x, grid.y, S), dim3(256), 0, s, a);
     const int n = a.B * ((a.N + 15) / 16) * 4;
-    hipLaunchKernelGGL((gemm_splitk_reduce<EPI>), dim3((n + 255) / 256), dim3(256), 0, s, a, S);
+#define L_(SS) hipLaunchKernelGGL((gemm_splitk_reduce<EPI, SS>), dim3((n + 255) / 256), dim3(256), 0, s, a, S)
+    MTTS_SPLIT_DISPATCH(S, L_);
+#undef L_
     return;
   }
   static const int u = getenv("MTTS_GEMM_U") ? atoi(getenv("MTTS_GEMM_U")) : 4;
