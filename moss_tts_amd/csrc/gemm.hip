@@ -309,7 +309,19 @@ __global__ __launch_bounds__(256) void gemm_splitk_reduce(GemvArgs a, int S) {
     }
     o[i] = v;
   }
-  if (live) {
+  if (EPI == EPI_SWIGLU && live && a.y_packed) {  // the packed down-projection input (xpkT_index)
+    const int n = ot * 16 + q * 4;  // 4 columns inside one 8-column group: contiguous there
+    if (n + 3 < a.N) {
+      uint2 pk;
+      pk.x = pack2(o[0], o[1]);
+      pk.y = pack2(o[2], o[3]);
+      *reinterpret_cast<uint2*>(a.y + xpkT_index(m, n, a.pk_tiles)) = pk;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (n + i < a.N) a.y[xpkT_index(m, n + i, a.pk_tiles)] = f2bf(o[i]);
+    }
+  } else if (live) {
     bf16_t* yr = a.y + (size_t)m * a.ldy + ot * 16 + q * 4;
     if (ot * 16 + q * 4 + 3 < a.N && (a.ldy % 4) == 0) {
       uint2 pk;
@@ -737,9 +749,10 @@ __global__ __launch_bounds__(NWR * NWN * 64) void gemm5_kernel(GemvArgs a) {
 
 // split-K ways of a gemm5 launch of `blocks` workgroups: doubled until the grid covers `cover` or a
 // split would drop below `mink` k tiles (row-major outputs with a partials workspace only)
-static int gemm5_splits(const GemvArgs& a, int blocks, int cover, int mink) {
+// (a packed SwiGLU output -- the down projection's input -- is written packed by the reduce too)
+static int gemm5_splits(const GemvArgs& a, int blocks, int cover, int mink, bool packed_ok = false) {
   int S = 1;
-  if (!a.y_packed && a.ws) {
+  if ((!a.y_packed || packed_ok) && a.ws) {
     while (blocks * S < cover && a.KT / (2 * S) >= mink) S *= 2;
     while (S > 1 && (a.KT % S || (size_t)S * a.B * a.n_row_tiles * 16 > a.ws_floats)) S /= 2;
   }
@@ -747,11 +760,11 @@ static int gemm5_splits(const GemvArgs& a, int blocks, int cover, int mink) {
 }
 
 template <int NWR, int NWN, int WR, int WN, int R, int EPI>
-static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s) {
+static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s, bool packed_split = false) {
   constexpr int BR = NWR * WR, BT = NWN * WN;
   const size_t lds = gemm5_lds_bytes<NWR, NWN, WR, R>();
   const dim3 grid((a.n_row_tiles + BR - 1) / BR, (a.pk_tiles + BT - 1) / BT);
-  const int S = gemm5_splits(a, (int)(grid.x * grid.y), cover, mink);
+  const int S = gemm5_splits(a, (int)(grid.x * grid.y), cover, mink, packed_split);
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)gemm5_kernel<NWR, NWN, WR, WN, R, EPI, false>,
@@ -842,7 +855,11 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // MTTS_GEMM5 (A/B): the split-path form for <= 12 token tiles
   static const int g5 = getenv("MTTS_GEMM5") ? atoi(getenv("MTTS_GEMM5")) : 1;
   // MTTS_GEMM5_SMALL_COVER (A/B): workgroups the split-K aims for
-  static const int small_cover = getenv("MTTS_GEMM5_SMALL_COVER") ? atoi(getenv("MTTS_GEMM5_SMALL_COVER")) : 256;
+  static const int small_cover0 = getenv("MTTS_GEMM5_SMALL_COVER") ? atoi(getenv("MTTS_GEMM5_SMALL_COVER")) : 256;
+  // MTTS_GEMM5_SWIGLU_COVER (A/B): the same for gate|up (its split reduce applies SwiGLU and writes
+  // the packed down input)
+  static const int swiglu_cover = getenv("MTTS_GEMM5_SWIGLU_COVER") ? atoi(getenv("MTTS_GEMM5_SWIGLU_COVER")) : 256;
+  const int small_cover = EPI == EPI_SWIGLU ? swiglu_cover : small_cover0;
   // two shapes: 6 waves x 2 token tiles on 96-row blocks, or 4 waves x 3 on 128-row blocks (one wave a
   // SIMD: the same MFMA time per k step for 8 row tiles instead of 6).  Taken by rounds over the
   // CUs x k steps per block (ties: the 96-row form); the 128-row form gives o_proj / down 256 split
@@ -857,7 +874,7 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
     auto cost = [&](int br, int bt, int step) {
       const int ty = (a.pk_tiles + bt - 1) / bt;
       const int rb = (a.n_row_tiles + br - 1) / br;
-      const int S = gemm5_splits(a, rb * ty, small_cover, small_mink);
+      const int S = gemm5_splits(a, rb * ty, small_cover, small_mink, EPI == EPI_SWIGLU);
       return (long)((rb * ty * S + 255) / 256) * (a.KT / S) * step;
     };
     int shape = small_shape;
@@ -866,9 +883,9 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
       shape = c2 < c1 ? 2 : 1;
       if (c3 < std::min(c1, c2)) shape = 3;
     }
-    if (shape == 3) return gemm5_launch<1, 6, 6, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
-    if (shape == 2) return gemm5_launch<1, 4, 8, 3, G5S_R, EPI>(a, small_cover, small_mink, s);
-    return gemm5_launch<1, 6, 6, 2, G5S_R, EPI>(a, small_cover, small_mink, s);
+    if (shape == 3) return gemm5_launch<1, 6, 6, 3, G5S_R, EPI>(a, small_cover, small_mink, s, EPI == EPI_SWIGLU);
+    if (shape == 2) return gemm5_launch<1, 4, 8, 3, G5S_R, EPI>(a, small_cover, small_mink, s, EPI == EPI_SWIGLU);
+    return gemm5_launch<1, 6, 6, 2, G5S_R, EPI>(a, small_cover, small_mink, s, EPI == EPI_SWIGLU);
   }
   if (a.pk_tiles <= small_max) return gemm3_launch<3, 2, 2, 6, G3S_NST, EPI>(a, 256, small_mink, s);
   // MTTS_GEMM5_LONG (A/B, 0: gemm3): the long-prompt shapes with split paths as well -- batch-4 prefill
