@@ -892,6 +892,10 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
   // 18.6 -> 17.5 ms, 1,024 rows 27.7 -> 26.6, TTSD long form 75.2 -> 71.6, 32 utterances unchanged
   // (profiles/r04_p_gemm5_long_ab.txt)
   static const int g5l = getenv("MTTS_GEMM5_LONG") ? atoi(getenv("MTTS_GEMM5_LONG")) : 1;
+  // MTTS_GEMM5_LONG_COVER (A/B): workgroups the long forms split K for (128 until late round 5: the
+  // batch-4 prompts' o_proj / q|k|v then ran 128 / 192 blocks on 256 CUs; 256: 4 x 126 rows 11.3 ->
+  // 10.2 ms, 8 x 126 21.0 -> 17.7, 1,024 rows 21.8 -> 18.5, 2,117 even; profiles/r05_z_ab_long_cover.txt)
+  static const int long_cover = getenv("MTTS_GEMM5_LONG_COVER") ? atoi(getenv("MTTS_GEMM5_LONG_COVER")) : 256;
   if (g5l) {
     // token tiles per wave chosen as below for the 256-row blocks too (4 or 5; MTTS_GEMM5_WWN forces)
     if (a.n_row_tiles >= wide_min) {
@@ -903,8 +907,8 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
         const long c5 = (rb * ((a.pk_tiles + 19) / 20) + 255) / 256 * 5;
         wn = c5 < c4 ? 5 : 4;
       }
-      if (wn == 5) return gemm5_launch<2, 4, 8, 5, 2, EPI>(a, 128, 16, s);
-      return gemm5_launch<2, 4, 8, 4, 2, EPI>(a, 128, 16, s);
+      if (wn == 5) return gemm5_launch<2, 4, 8, 5, 2, EPI>(a, long_cover, 16, s);
+      return gemm5_launch<2, 4, 8, 4, 2, EPI>(a, long_cover, 16, s);
     }
     // 128-row blocks: token tiles per wave WN = 4, 5 or 6 by the launch's rounds over the CUs x
     // per-block work (ceil(blocks / 256) x WN).  WN = 4 alone gave the TTSD script's 2,117-row o_proj
@@ -922,9 +926,9 @@ static hipError_t gemm3_pick(GemvArgs a, hipStream_t s) {
         if (cost < best) { best = cost; wn = w; }
       }
     }
-    if (wn == 5) return gemm5_launch<2, 4, 4, 5, 2, EPI>(a, 128, 16, s);
-    if (wn == 6) return gemm5_launch<2, 4, 4, 6, 2, EPI>(a, 128, 16, s);
-    return gemm5_launch<2, 4, 4, 4, 2, EPI>(a, 128, 16, s);
+    if (wn == 5) return gemm5_launch<2, 4, 4, 5, 2, EPI>(a, long_cover, 16, s);
+    if (wn == 6) return gemm5_launch<2, 4, 4, 6, 2, EPI>(a, long_cover, 16, s);
+    return gemm5_launch<2, 4, 4, 4, 2, EPI>(a, long_cover, 16, s);
   }
   if (a.n_row_tiles >= wide_min) return gemm3_launch<2, 4, 8, 4, G3_NST, EPI>(a, 128, 16, s);
   return gemm3_launch<2, 4, 4, 4, G3_NST, EPI>(a, 128, 16, s);
