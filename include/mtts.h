@@ -74,6 +74,9 @@ typedef struct mtts_sampling {
 
 const char* mtts_last_error(void);
 int mtts_version(void);
+/* sha256 (hex) of the sources this library was built from (moss_tts_amd/_buildid.py): ties a
+ * prebuilt binary to its tree; the Python binding refuses a mismatch. */
+const char* mtts_build_id(void);
 
 /* ---- engine lifecycle --------------------------------------------------- */
 /* replaces AutoModel.from_pretrained(...).to(device) (clis/moss_tts_app.py:95-107) */

@@ -8,7 +8,8 @@ runtime failures).
 import ctypes
 import os
 
-_LIB_PATH = os.environ.get("MTTS_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmtts.so")
+_DEFAULT_LIB = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libmtts.so")
+_LIB_PATH = os.environ.get("MTTS_LIB") or _DEFAULT_LIB
 
 MTTS_OK = 0
 MTTS_E_INVALID = -1
@@ -66,6 +67,7 @@ U64 = ctypes.c_uint64
 _SIGS = {
     "mtts_last_error": (ctypes.c_char_p, []),
     "mtts_version": (I, []),
+    "mtts_build_id": (ctypes.c_char_p, []),
     "mtts_engine_create": (I, [ctypes.POINTER(MttsConfig), I, ctypes.POINTER(P)]),
     "mtts_engine_destroy": (I, [P]),
     "mtts_engine_reserve": (I, [P, I, I, I]),
@@ -155,8 +157,20 @@ def load():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if _LIB_PATH == _DEFAULT_LIB:
+        # the in-tree library must have been built from this tree's sources (moss_tts_amd/_buildid.py)
+        from . import _buildid
+        built, tree = lib.mtts_build_id().decode(), _buildid.tree_hash("lib")
+        if built != tree:
+            raise RuntimeError(f"stale {_LIB_PATH}: built from sources {built[:16]}, the tree's are {tree[:16]}; "
+                               "rebuild with `python -c 'import __graft_entry__ as g; g.build()'`")
     _lib = lib
     return lib
+
+
+def build_id():
+    """the source hash compiled into the loaded libmtts.so"""
+    return load().mtts_build_id().decode()
 
 
 class PseTimeout(RuntimeError):

@@ -80,8 +80,8 @@ struct mtts_engine {
   float* part = nullptr;
   size_t part_floats = 0;
   bf16_t* logits = nullptr;
-  int* d_pos = nullptr;
-  int* rope_off = nullptr;  // [max_batch]: MossTTSLocal backbone rows' left-pad counts (Stack::rope_off)  // pos_base for teacher-forced forwards / prefill
+  int* d_pos = nullptr;     // pos_base for teacher-forced forwards / prefill
+  int* rope_off = nullptr;  // [max_batch]: MossTTSLocal backbone rows' left-pad counts (Stack::rope_off)
   int* att_cnt = nullptr;  // decode-attention arrival tickets [Bmax][Hkv] (zero between launches)
   int text_tile_lo = 0;    // first 16-row text-head tile holding a special id the sampler reads
   bool full_text_head = false;    // MTTS_FULL_TEXT_HEAD=1: evaluate the whole text head every step (A/B)

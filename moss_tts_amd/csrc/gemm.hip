@@ -783,7 +783,9 @@ static hipError_t gemm5_launch(GemvArgs a, int cover, int mink, hipStream_t s, b
       if (a.qkr_done) *a.qkr_done = 1;
       return hipGetLastError();
     }
-    if (EPI == EPI_RESADD && a.pn_w && a.N % 16 == 0 && a.N <= 4096 && a.ldres % 8 == 0 && a.ldy % 8 == 0) {
+    // (N / 8 threads: whole waves for its wave_sum, and its sums-of-squares pass reads 4 tiles a
+    // lane, so H % 64 == 0; N % 512 covers both -- other widths take the plain reduce + rmsnorm_ss)
+    if (EPI == EPI_RESADD && a.pn_w && a.N % 512 == 0 && a.N <= 4096 && a.ldres % 8 == 0 && a.ldy % 8 == 0) {
 #define L_(SS) hipLaunchKernelGGL(gemm_splitk_reduce_norm<SS>, dim3(a.B), dim3(a.N / 8), 0, s, a, S)
       MTTS_SPLIT_DISPATCH(S, L_);
 #undef L_

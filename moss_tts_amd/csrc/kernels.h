@@ -319,6 +319,10 @@ uint32_t* pse4_err_word(void* ws);
 // LH 1536, 16 / 8 heads x 128, I 8960, adapters F 2048 to H 2048; B <= 8 rows, 256 CUs)
 constexpr int LPSE_MAXL = 6;
 constexpr int LPSE_MAXB = 8;
+// the attention stages the keys of at most this many earlier channel positions in LDS (lpse.hip
+// AKEYS), so the launch serves frames of <= LPSE_MAX_CHANNELS channels (1 + n_vq <= 33); wider
+// configs keep the per-op depth loop
+constexpr int LPSE_MAX_CHANNELS = 33;
 struct LpseLayer {
   const bf16_t *qkv, *o, *gu, *down, *in_norm, *post_norm, *q_norm, *k_norm;
 };
@@ -357,7 +361,7 @@ hipError_t moss_rmsnorm(const bf16_t* x, const bf16_t* w, bf16_t* y, int M, int 
 hipError_t argmax_rows(const bf16_t* logits, int ld, int V, int64_t* out, int ld_out, int B, hipStream_t s);
 // per-row count of masked (pad) columns among the first n of a [B][ld] key mask: the offset
 // between a row's cache slots and its RoPE positions (kernels.h QKRopeArgs::rope_off)
-hipError_t row_pad_count(const uint8_t* mask, int ld, int n, int B, int* out, hipStream_t s);
+hipError_t row_pad_count(const uint8_t* mask, int ld, int n, int B, int* out, int* bad, hipStream_t s);
 hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, int C, int64_t* gen_ids, int Ltot,
                       uint8_t* mask, int Cmax, int* finished, uint8_t* seen, int audio_rows, hipStream_t s);
 hipError_t local_finalize(GenDev* st, int64_t* next, int* finished, int64_t* gen_ids, uint8_t* mask, uint8_t* seen,

@@ -49,6 +49,7 @@ struct LocalParts {
   bool lpse = false, lpse_ok = false;
   void* lpse_ws = nullptr;  // lpse_ws_bytes(), zero-filled
   int lpse_timeouts = 0;
+  int* mask_bad = nullptr;  // row_pad_count's flag: some row of the mask is not left-padded
 };
 
 static Stack local_stack(mtts_engine* e) {
@@ -110,10 +111,11 @@ int local_create(mtts_engine* e) {
     hipMemset(p.mo_down[i], 0, packed_bytes(H, F));
   }
   hipMemset(p.mi_down, 0, packed_bytes(LH, F));
+  if ((rc = e->alloc(&p.mask_bad, 1))) return rc;
   // weight bytes one frame streams: backbone once, then per channel the depth stack, its norm,
   // both adapters, the channel norm and the channel head
   p.lpse_ok = lpse_supported(e->device, 1, p.LL, LH, Hq, Hkv, D, LI, F, H, LOCAL_CMAX) &&
-              p.qkv_rows == (Hq + 2 * Hkv) * D;
+              p.qkv_rows == (Hq + 2 * Hkv) * D && C <= LPSE_MAX_CHANNELS;
   if (p.lpse_ok) {
     if ((rc = e->alloc(reinterpret_cast<unsigned char**>(&p.lpse_ws), lpse_ws_bytes()))) return rc;
     HIPCHK(hipMemset(p.lpse_ws, 0, lpse_ws_bytes()));
@@ -506,6 +508,24 @@ static int n_channels(const mtts_engine* e, int n_vq_inf) {
   return n_vq_inf < 0 ? C : std::min(C, 1 + n_vq_inf);
 }
 
+// The backbone rows' RoPE offsets from e->mask's first n columns (the rows' left pads).
+// GenerationMixin's positions are cumsum(mask) - 1 (transformers/generation/utils.py:751-773),
+// which is slot - pads only for a left-padded row, so any other mask is refused (one host sync,
+// outside stream capture) rather than decoded with shifted positions.
+static int left_pad_offsets(mtts_engine* e, int n, int B, hipStream_t s) {
+  LocalParts& p = *e->lp;
+  HIPCHK(hipMemsetAsync(p.mask_bad, 0, sizeof(int), s));
+  HIPCHK(row_pad_count(e->mask, e->c.max_ctx, n, B, e->rope_off, p.mask_bad, s));
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  HIPCHK(hipStreamIsCapturing(s, &cs));
+  if (cs != hipStreamCaptureStatusNone) return 0;
+  int bad = 0;
+  HIPCHK(hipMemcpyAsync(&bad, p.mask_bad, sizeof(int), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (bad) return fail(MTTS_E_INVALID, "attention_mask must be left-padded (MossTTSLocal positions are cumsum(mask) - 1)");
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // C ABI (include/mtts.h)
 extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, const uint8_t* mask, int B, int T,
@@ -551,8 +571,8 @@ extern "C" int mtts_local_generate_begin(mtts_engine* e, const int64_t* ids, con
   p.n_ch = n_channels(e, n_vq_for_inference);
   HIPCHK(hipMemcpyAsync(e->st, &g, sizeof(g), hipMemcpyHostToDevice, s));
   HIPCHK(local_init(ids, mask, B, T, p.C, e->gen_ids, c.max_ctx, e->mask, c.max_ctx, p.finished, p.seen, e->audio_rows, s));
-  HIPCHK(row_pad_count(e->mask, c.max_ctx, T, B, e->rope_off, s));  // left pads: RoPE offsets
-  int rc = forward_chunked(e, ids, B, T, 0, nullptr, s, p.hid, p.n_ch);
+  int rc = left_pad_offsets(e, T, B, s);
+  if (!rc) rc = forward_chunked(e, ids, B, T, 0, nullptr, s, p.hid, p.n_ch);
   if (!rc) rc = local_depth(e, B, p.n_ch, nullptr, 0, nullptr, 0, s);
   if (!rc) rc = local_frame_end(e, s);
   if (rc) return rc;
@@ -650,8 +670,8 @@ extern "C" int mtts_local_forward(mtts_engine* e, const int64_t* ids, const uint
   const int n_ch = n_channels(e, n_vq_for_inference);
   hipStream_t s = enter(e, stream);
   HIPCHK(hipMemcpy2DAsync(e->mask, c.max_ctx, mask, past + S, past + S, B, hipMemcpyDeviceToDevice, s));
-  HIPCHK(row_pad_count(e->mask, c.max_ctx, past + S, B, e->rope_off, s));  // left pads: RoPE offsets
-  int rc = forward_chunked(e, ids, B, S, past, nullptr, s, p.hid, n_ch);
+  int rc = left_pad_offsets(e, past + S, B, s);
+  if (!rc) rc = forward_chunked(e, ids, B, S, past, nullptr, s, p.hid, n_ch);
   if (!rc) rc = local_depth(e, B, n_ch, forced, p.C, reinterpret_cast<bf16_t*>(logits), ld_logits, s);
   if (!rc && local_lpse_takes(e, B)) {
     // (a teacher-forced frame is the parity entry: checked here, and on a timed-out launch the

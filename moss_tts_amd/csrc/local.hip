@@ -280,22 +280,33 @@ hipError_t local_init(const int64_t* ids, const uint8_t* mask_in, int B, int T, 
   return hipGetLastError();
 }
 
+// out[b] = masked columns of row b; a row whose masked columns do not all precede its first
+// unmasked one (an interior or right pad) sets *bad: GenerationMixin's positions cumsum(mask) - 1
+// equal slot - out[b] only for left padding
 __global__ __launch_bounds__(256) void row_pad_count_kernel(const uint8_t* __restrict__ mask, int ld, int n,
-                                                            int* __restrict__ out) {
+                                                            int* __restrict__ out, int* __restrict__ bad) {
   const int b = blockIdx.x;
-  int z = 0;
-  for (int t = threadIdx.x; t < n; t += blockDim.x) z += mask[(size_t)b * ld + t] == 0;
-  __shared__ int tot;
-  if (threadIdx.x == 0) tot = 0;
+  int z = 0, first = n;
+  for (int t = threadIdx.x; t < n; t += blockDim.x) {
+    const bool m = mask[(size_t)b * ld + t] != 0;
+    z += !m;
+    if (m) first = min(first, t);
+  }
+  __shared__ int tot, fst;
+  if (threadIdx.x == 0) { tot = 0; fst = n; }
   __syncthreads();
   atomicAdd(&tot, z);
+  atomicMin(&fst, first);
   __syncthreads();
-  if (threadIdx.x == 0) out[b] = tot;
+  if (threadIdx.x == 0) {
+    out[b] = tot;
+    if (bad && tot != fst && !(fst == n && tot == n)) atomicOr(bad, 1);
+  }
 }
 
-hipError_t row_pad_count(const uint8_t* mask, int ld, int n, int B, int* out, hipStream_t s) {
+hipError_t row_pad_count(const uint8_t* mask, int ld, int n, int B, int* out, int* bad, hipStream_t s) {
   if (B <= 0 || n < 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(row_pad_count_kernel, dim3(B), dim3(256), 0, s, mask, ld, n, out);
+  hipLaunchKernelGGL(row_pad_count_kernel, dim3(B), dim3(256), 0, s, mask, ld, n, out, bad);
   return hipGetLastError();
 }
 

@@ -115,6 +115,7 @@ static_assert(L_END <= 160 * 1024, "LDS");
 // K [AKEYS][D] and values V^T [D][AKEYS] bf16 (prefetched while the q|k|v hand-off is awaited),
 // qn [2][D], kn [D], vn [D], scores [2][CMAX], p [2][CMAX], l [2] (fp32)
 constexpr int AKEYS = 32;  // channel positions before the newest (<= 33 channels per frame)
+static_assert(AKEYS + 1 == LPSE_MAX_CHANNELS, "local.cpp gates the launch on 1 + n_vq <= LPSE_MAX_CHANNELS");
 constexpr int L_AKC = L_X, L_AVC = L_AKC + AKEYS * D * 2;
 constexpr int L_AQ = L_AVC + D * AKEYS * 2, L_AK = L_AQ + 2 * D * 4, L_AV = L_AK + D * 4, L_AS = L_AV + D * 4,
               L_AP = L_AS + 2 * CMAX * 4, L_AL = L_AP + 2 * CMAX * 4;

@@ -131,6 +131,37 @@ def make_weights(cfg: Cfg, seed: int, dtype="fp32", emb_scale=1.0, text_boost=4.
     return out
 
 
+def weight_fill_plan(cfg: Cfg, seed: int, text_boost=4.0, text_damp=0.25, special_boost=1.0):
+    """`make_weights(cfg, seed, "bf16", ...)` restated as device fills, for shapes too large to
+    build on the host (the 8B-shape reference fixtures, tests/golden/make_golden_8b.py).
+
+    Returns [(name, shape, tensor_id, scale, offset, patch)]: fill the tensor with the portable
+    PRNG (`mtts_k_fill_uniform`: bf16(offset + scale * (2u - 1))), then overwrite the rows in
+    `patch` ({row: float32 values before bf16 rounding}).  Equal to make_weights bit for bit:
+    the text head's damping is a power of two (text_damp 0.25), so folding it into `scale`
+    changes no rounding, and the boosted rows are recomputed on the host with make_weights'
+    own float32 arithmetic (checked by tests/test_oracle_golden.py at the tiny shape)."""
+    plan = []
+    for tid, (name, shape, kind) in enumerate(weight_specs(cfg)):
+        sc, off = scale_for(kind, shape)
+        patch = {}
+        if name == "lm_heads.0.weight" and text_boost is not None:
+            assert text_damp in (0.5, 0.25, 0.125), "the damping must be a power of two"
+            H = shape[1]
+            idx = [t for t in BOOST_TOKENS if t < shape[0]]
+            f = np.float32(0.75) + np.float32(0.5) * prng.uniform(seed, 10_000, len(idx))
+            f[:2] *= np.float32(special_boost)
+            fac = np.float32(text_boost / text_damp) * f
+            for r, t in enumerate(idx):
+                u = prng.uniform(seed, tid, H, start=t * H)
+                v = np.float32(off) + np.float32(sc) * (np.float32(2.0) * u - np.float32(1.0))
+                v = v.astype(np.float32) * np.float32(text_damp)
+                patch[t] = (v * fac[r]).astype(np.float32)
+            sc = float(np.float32(sc) * np.float32(text_damp))
+        plan.append((name, shape, tid, sc, off, patch))
+    return plan
+
+
 # ----------------------------------------------------------------------------
 # backbone ops
 # ----------------------------------------------------------------------------

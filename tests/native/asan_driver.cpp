@@ -346,7 +346,13 @@ static void kernels() {
   for (void* p : {(void*)w, (void*)wp, (void*)x, (void*)y}) hipFree(p);
 }
 
-int main() {
+int main(int argc, char** argv) {
+  // --build-id: the source hash compiled into this driver (moss_tts_amd/_buildid.py --scope asan),
+  // checked against the tree before any GPU test runs (tests/conftest.py); touches no GPU
+  if (argc > 1 && strcmp(argv[1], "--build-id") == 0) {
+    printf("%s\n", mtts_build_id());
+    return 0;
+  }
   const char* lp = getenv("MTTS_ASAN_LOG");
   g_log = lp && *lp ? fopen(lp, "a") : nullptr;
   if (!g_log) g_log = stderr;

@@ -77,3 +77,13 @@ def test_rope_table_host_path():
                  sn.ctypes.data_as(ctypes.c_void_p))
     c, s = O.rope_cos_sin(O._Ctx("bf16"), O.tiny_cfg(), np.arange(n))
     assert np.mean(B16.from_bits(cs) == c) > 0.999 and np.mean(B16.from_bits(sn) == s) > 0.999
+
+
+def test_build_id_matches_tree():
+    """the library's compiled-in source hash is this tree's (moss_tts_amd/_buildid.py); a
+    stale prebuilt binary is refused by the binding and by tests/conftest.py"""
+    from moss_tts_amd import _buildid, _native
+    if not os.path.exists(_native.lib_path()):
+        pytest.skip("libmtts.so not built")
+    assert _native.build_id() == _buildid.tree_hash("lib")
+    assert len(_native.build_id()) == 64

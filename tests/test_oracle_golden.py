@@ -130,3 +130,20 @@ def test_ops(golden, dt):
     o = O.attention(ctx, g[p + "q"], g[p + "k"], g[p + "v"], g[p + "key_mask"], g[p + "q_pos"], 16 ** -0.5)
     ref = g[p + "out"].transpose(0, 2, 1, 3)
     np.testing.assert_allclose(o, ref, rtol=0, atol=(1.0 / 64 if dt == "bf16" else 1e-5))
+
+
+@pytest.mark.parametrize("n_vq,seed,boost", [(4, 11, 2.0), (32, 31, 2.0), (16, 33, 1.0)])
+def test_weight_fill_plan_equals_make_weights(n_vq, seed, boost):
+    """oracle.moss_delay.weight_fill_plan (the device-side recipe of the 8B-shape fixtures:
+    mtts_k_fill_uniform per tensor, then the boosted text-head rows) is make_weights bit for bit
+    (tiny shape; the device fill's arithmetic is pinned by test_fill_uniform_matches_oracle_prng)"""
+    from oracle import prng
+    cfg = O.tiny_cfg(n_vq=n_vq)
+    W = O.make_weights(cfg, seed, dtype="bf16", special_boost=boost)
+    plan = O.weight_fill_plan(cfg, seed, special_boost=boost)
+    assert [p[0] for p in plan] == list(W)
+    for name, shape, tid, sc, off, patch in plan:
+        w = B16.rnd(prng.tensor(seed, tid, shape, np.float32(sc), off))  # what the device fill writes
+        for r, v in patch.items():
+            w[r] = B16.rnd(v)
+        assert np.array_equal(w, W[name]), name
