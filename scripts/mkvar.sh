@@ -11,5 +11,5 @@ mkdir -p build/var ../lib/var
 /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wno-unused-result -Wno-unused-value -ffp-contract=fast \
   -I. $defs -x hip -c $file -o build/var/${src}_$name.o
 objs=$(for s in $(sed -n "s/^SRCS = //p" Makefile); do [ "$s" = "$src" ] || echo build/$s.o; done)
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/var/libmtts_$name.so $objs build/var/${src}_$name.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o ../lib/var/libmtts_$name.so $objs build/build_id.o build/var/${src}_$name.o
 echo "built moss_tts_amd/lib/var/libmtts_$name.so"

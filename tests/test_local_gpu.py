@@ -374,3 +374,31 @@ def test_local_per_channel_processors(gpu, gl):
         f0 = T - int(starts[r])  # first generated row of this row's output
         assert torch.equal(a[r][f0, :j0], greedy[r][f0, :j0]) and torch.equal(b[r][f0, :j0], greedy[r][f0, :j0])
     assert any(not torch.equal(x[:, j0], y[:, j0]) for x, y in zip(a, b))
+
+
+def test_local_mask_must_be_left_padded(gpu):
+    """the backbone's RoPE offsets are the rows' pad counts, which equal GenerationMixin's
+    cumsum(mask) - 1 positions only for left padding -- an interior or right pad is refused
+    (MTTS_E_INVALID -> ValueError) by the teacher-forced forward and by generate, not decoded with
+    shifted positions; a left-padded mask still runs"""
+    cfg = L.tiny_lcfg(n_vq=4)
+    eng = make_local_engine(cfg, None, seed=3)
+    try:
+        rng = np.random.default_rng(3)
+        C = cfg.n_vq + 1
+        ids = np.full((2, 10, C), cfg.audio_pad_code, np.int64)
+        ids[..., 0] = rng.integers(200, 20000, (2, 10))
+        ids[:, -1, 0] = cfg.audio_start_token_id
+        frame = np.zeros((2, C), np.int64)
+        for bad in ([1] * 4 + [0] + [1] * 5, [1] * 9 + [0]):  # interior pad, right pad
+            mask = np.ones((2, 10), np.uint8)
+            mask[1] = bad
+            with pytest.raises(ValueError, match="left-padded"):
+                eng.local_forward(torch.from_numpy(ids), torch.from_numpy(mask), 0, torch.from_numpy(frame))
+            with pytest.raises(ValueError, match="left-padded"):
+                eng.local_generate_ids(torch.from_numpy(ids), torch.from_numpy(mask), 2)
+        mask = np.ones((2, 10), np.uint8)
+        mask[1, :3] = 0
+        eng.local_forward(torch.from_numpy(ids), torch.from_numpy(mask), 0, torch.from_numpy(frame))
+    finally:
+        eng.close()
