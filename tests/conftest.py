@@ -26,3 +26,14 @@ def pytest_sessionstart(session):
         if built != tree:
             pytest.exit(f"stale {binary}: built from sources {str(built)[:16]}, the tree's hash is {tree[:16]} "
                         "(rebuild: python -c 'import __graft_entry__ as g; g.build()')", returncode=3)
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    import numpy as np
+    d = os.path.join(ROOT, "tests", "golden")
+    g = np.load(os.path.join(d, "golden.npz"), allow_pickle=False)
+    with open(os.path.join(d, "cases.json")) as f:
+        cases = json.load(f)
+    return g, cases
