@@ -49,16 +49,7 @@ constexpr int CW = 4;                   // consumer waves
 #endif
 constexpr int LW = PSE_LW;              // loader waves
 static_assert(LW == 1, "the register-staged loader publishes one FULL counter");
-// PSE_WARM: a warmer wave reads this CU's weight slots up to PSE_WARM slots ahead of the loader's
-// issue point with default-policy loads (data discarded), so while the consumers wait out a
-// hand-off -- the loader blocked on a full ring, HBM idle -- the upcoming weights move into the
-// Infinity Cache, and the loader's own fills of them later hit there (8.6 vs 6.3 TB/s chip-wide,
-// ~0.23 us instead of an HBM miss; MI355X_MICROARCH.md "Infinity Cache").  0: no warmer wave.
-#ifndef PSE_WARM
-#define PSE_WARM 0
-#endif
-constexpr int WW = PSE_WARM > 0 ? 1 : 0;
-constexpr int THREADS = (LW + CW + WW) * 64;
+constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_POLL_SLEEP
 #define PSE_POLL_SLEEP 1  // s_sleep count between a gather's sweeps (x 64 cycles)
 #endif
@@ -1221,66 +1212,6 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
 #undef PSE_RL_LOADS
     if (dead) st32(a.err, 1u);
     __hip_atomic_store(&ctl->full[0], dead ? 0 : total, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-  } else if (wave >= LW + CW) {
-    // =================== warmer (PSE_WARM) ===================
-    // slot s is read once the loader's issue point (its published fills + the 3 register buffers)
-    // is within PSE_WARM slots, skipping ahead whenever the loader has caught up; one slot (16 loads) in flight at a time.  Loads only,
-    // every address inside the weights; it stops with the loader (end of the sequence or abort)
-    // and pauses with it while this CU's attention gathers its inputs.
-    if constexpr (WW > 0) {
-      // one asm block per slot: 16 loads into registers the block clobbers, waited for inside the
-      // block (a load left in flight past an asm statement would land in registers the compiler
-      // has since reused -- "+v" buffers get copied in and out around the block)
-      const uint32_t voff = (uint32_t)lane * 16u;
-      auto warm = [&](int s) {
-        const uint64_t p = (uint64_t)(uintptr_t)pse_slot_src(wp, c, nq, min(s, total - 1));
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)p), hi = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));
-        const void* g = (const void*)(((uint64_t)hi << 32) | lo);
-        asm volatile("s_nop 4\n\t"
-                     "global_load_dwordx4 v[192:195], %[o0], %[g] offset:0\n\t"
-                     "global_load_dwordx4 v[196:199], %[o0], %[g] offset:1024\n\t"
-                     "global_load_dwordx4 v[200:203], %[o0], %[g] offset:2048\n\t"
-                     "global_load_dwordx4 v[204:207], %[o0], %[g] offset:3072\n\t"
-                     "global_load_dwordx4 v[208:211], %[o1], %[g] offset:0\n\t"
-                     "global_load_dwordx4 v[212:215], %[o1], %[g] offset:1024\n\t"
-                     "global_load_dwordx4 v[216:219], %[o1], %[g] offset:2048\n\t"
-                     "global_load_dwordx4 v[220:223], %[o1], %[g] offset:3072\n\t"
-                     "global_load_dwordx4 v[224:227], %[o2], %[g] offset:0\n\t"
-                     "global_load_dwordx4 v[228:231], %[o2], %[g] offset:1024\n\t"
-                     "global_load_dwordx4 v[232:235], %[o2], %[g] offset:2048\n\t"
-                     "global_load_dwordx4 v[236:239], %[o2], %[g] offset:3072\n\t"
-                     "global_load_dwordx4 v[240:243], %[o3], %[g] offset:0\n\t"
-                     "global_load_dwordx4 v[244:247], %[o3], %[g] offset:1024\n\t"
-                     "global_load_dwordx4 v[248:251], %[o3], %[g] offset:2048\n\t"
-                     "global_load_dwordx4 v[252:255], %[o3], %[g] offset:3072\n\t"
-                     "s_waitcnt vmcnt(0)"
-                     :
-                     : [g] "s"(g), [o0] "v"(voff), [o1] "v"(voff + 4096u), [o2] "v"(voff + 8192u), [o3] "v"(voff + 12288u)
-                     : "memory", "v192", "v193", "v194", "v195", "v196", "v197", "v198", "v199", "v200", "v201", "v202",
-                       "v203", "v204", "v205", "v206", "v207", "v208", "v209", "v210", "v211", "v212", "v213", "v214",
-                       "v215", "v216", "v217", "v218", "v219", "v220", "v221", "v222", "v223", "v224", "v225", "v226",
-                       "v227", "v228", "v229", "v230", "v231", "v232", "v233", "v234", "v235", "v236", "v237", "v238",
-                       "v239", "v240", "v241", "v242", "v243", "v244", "v245", "v246", "v247", "v248", "v249", "v250",
-                       "v251", "v252", "v253", "v254", "v255");
-      };
-      bool stop = false;
-      for (int s = 6; !stop; ++s) {
-        for (uint32_t spins = 0;; ++spins) {
-          const int f = __hip_atomic_load(&ctl->full[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          const bool paused = PSE_APAUSE && __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          // never behind the loader: slots up to f + 2 are its in-flight register fills, and a slot it
-          // has issued already would only be read twice
-          s = max(s, f + 6);
-          if (s >= total || spins > SPIN_LDS || __hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-            stop = true;  // (past the last slot: pse_slot_src would index past the pointer table)
-            break;
-          }
-          if (!paused && s < f + 6 + PSE_WARM) break;
-          __builtin_amdgcn_s_sleep(2);
-        }
-        if (!stop) warm(s);
-      }
-    }
   } else {
     // =================== consumers ===================
     Ctx x{a.err, a.eps, a.probe, c, lane, wave, (wave - LW) * 64 + lane, epoch, 0};
