@@ -147,3 +147,39 @@ def test_weight_fill_plan_equals_make_weights(n_vq, seed, boost):
         for r, v in patch.items():
             w[r] = B16.rnd(v)
         assert np.array_equal(w, W[name]), name
+
+
+def test_golden_8b_fixture_consistent():
+    """tests/golden/golden_8b.npz (the reference at the 8B layer shape, make_golden_8b.py) is
+    self-consistent: the recorded text-row selection is the one the GPU test rebuilds, every
+    sampled (row, channel)'s recorded top-1 is the id the reference emitted at that step, channels
+    it did not sample hold the fill ids, and the per-step logits cover every forward call"""
+    import json
+    import os
+    from tests.golden import ref8b_inputs as R
+    d = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    g = np.load(os.path.join(d, "golden_8b.npz"), allow_pickle=False)
+    cases = json.load(open(os.path.join(d, "cases_8b.json")))
+    assert set(cases) == {"r8_clone_b1", "r8_ragged_b4", "r8_long_nvq16"}
+    for name, c in cases.items():
+        cfg = O.Cfg(layers=c["layers"], n_vq=c["n_vq"])
+        assert np.array_equal(g[name + "/text_sel"], R.text_sel(cfg))
+        ids = g[name + "/input_ids"]
+        T = ids.shape[1]
+        top = g[name + "/sampled_top2"]
+        assert top.shape == (c["n_forward"], c["B"], cfg.n_vq + 1, 4)
+        assert g[name + "/raw_audio_bits"].shape == (c["n_forward"], c["B"], cfg.n_vq, cfg.audio_vocab + 1)
+        n_checked = 0
+        for b in range(c["B"]):
+            out = g[f"{name}/out{b}"]
+            gen = out[c["start_len"][b]:]  # the generated rows
+            assert np.array_equal(out[:c["start_len"][b]], ids[b, T - c["start_len"][b]:])
+            for s in range(min(len(gen), c["n_forward"])):
+                for ch in range(cfg.n_vq + 1):
+                    if np.isfinite(top[s, b, ch, 1]):
+                        assert int(top[s, b, ch, 0]) == int(gen[s, ch]), (name, b, s, ch)
+                        assert top[s, b, ch, 1] >= top[s, b, ch, 2]
+                        n_checked += 1
+                    elif ch > 0:
+                        assert gen[s, ch] == cfg.audio_pad_code, (name, b, s, ch)
+        assert n_checked > 0
