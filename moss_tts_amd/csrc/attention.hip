@@ -652,14 +652,19 @@ hipError_t attention(const AttnArgs& a0, hipStream_t st) {
 #include "attn_body.h"
 namespace mtts {
 
+// Grid (KV head, row, split): the split is the slowest dimension, so the blocks that hold keys
+// (splits below pos / keys-per-block + 1; the rest return at once) are the grid's first Hkv x B x
+// nact blocks, dealt round-robin over all 8 XCDs.  With the split fastest, a short context in a
+// long cache (split 0 of each head active out of ns) put every working block on the XCDs of block
+// ids 0, ns, 2 ns, ...: at B = 32 and the default 2,048-position cache (ns = 4) on 2 of the 8.
 template <int G, int D, int NWV>
 __global__ __launch_bounds__(NWV * 64) void attn_decode_kernel(DecAttnArgs a) {
-  attn_decode_body<G, D, NWV>(a, (int)blockIdx.x, (int)blockIdx.y, (int)blockIdx.z);
+  attn_decode_body<G, D, NWV>(a, (int)blockIdx.z, (int)blockIdx.x, (int)blockIdx.y);
 }
 
 template <int D, int NWV>
 static hipError_t attn_decode_dn(const DecAttnArgs& a, int G, int B, hipStream_t s) {
-  dim3 grid(a.ns, a.Hkv, B);
+  dim3 grid(a.Hkv, B, a.ns);
   const dim3 blk(NWV * 64);
   switch (G) {
     case 1: hipLaunchKernelGGL((attn_decode_kernel<1, D, NWV>), grid, blk, 0, s, a); break;

@@ -3,7 +3,7 @@
 
 // ===========================================================================
 // Fused decode attention (one new token per row), MFMA form.
-// Grid (split, KV head, row b); a 1024-thread block (16 waves) owns 512 consecutive keys,
+// Block (split, KV head, row b) -- launched as grid (KV head, row, split), attention.hip; a 1024-thread block (16 waves) owns 512 consecutive keys,
 // 32 per wave, so a context of <= 512 tokens is ONE block per (row, KV head) and needs no
 // cross-block combine.
 //   prologue  q_norm (TF/.../modeling_qwen3.py:252-254) + RoPE (:148-170) of the G query
