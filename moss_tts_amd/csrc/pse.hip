@@ -207,6 +207,23 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 #ifndef PSE_AU
 #define PSE_AU 2
 #endif
+// PSE_KSPLIT (round 6): the two units of a KV head split its cached keys (unit k the chunks of half
+// k, all G q heads) instead of its q heads (every key, G / 2 heads each).  A unit is bound by the
+// K / V bytes one CU pulls in (~50 GB/s: ~200 KB at 390 keys), which the key split halves.  Each
+// unit publishes its heads' outputs normalised by its own sum (bf16 pairs) and its (max, sum) per
+// head; every o_proj consumer merges the two partials of its columns (the gather grows from 2,048
+// to 4,352 granules).  Unit 0 adds the new key.
+#ifndef PSE_KSPLIT
+#define PSE_KSPLIT 0
+#endif
+static_assert(!PSE_KSPLIT || PSE_AU == 2, "the key split pairs the two units of a KV head");
+// attention output granules: the merged rows (2,048), or with PSE_KSPLIT the two units' rows
+// [unit][head][64 pairs] and their (max, sum) per head, 256 granules (ml_gran)
+constexpr int NG_ATT = PSE_KSPLIT ? 2 * (HQ_ * D_ / 2) + 256 : HQ_ * D_ / 2;
+// (PSE_KSPLIT) the (max | sum) granule of q head hq of unit ku: o_proj consumer wave hq % 4 holds
+// the o pairs of head hq, so its lanes gather exactly the (max, sum) values they merge with; each
+// value is published twice (d = 0, 1) so that every lane of the 256 takes one
+__host__ __device__ inline int ml_gran(int hq, int ku, int f, int d) { return 64 * (hq % 4) + 32 * d + 16 * ku + 2 * (hq / 4) + f; }
 __host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
   return (d >= 0 && d % 7 == 0 && d / 7 < HKV_ * PSE_AU) ? d / 7 : -1;
@@ -291,11 +308,13 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
   if (PSE_GPRIO) __builtin_amdgcn_s_setprio(3);  // sweeps issue ahead of the loader's fills
   bool ok = true;
   uint32_t lo[MAXP], hi[MAXP];
+  // one lane offset (tid * 8) for every granule i: i's 2 KiB stride rides in the SGPR offset, so a
+  // gather site keeps no per-granule offset registers live across its poll loop (pse4.hip's form)
+  const uint32_t vo = (uint32_t)x.tid * 8u;
   auto issue = [&]() {
 #pragma unroll
     for (int i = 0; i < MAXP; ++i) {
-      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (pend >> i & 1u) ? (uint32_t)(x.tid + i * CW * 64) * 8u : OOB,
-                                                          0, 16 /* sc1 */);
+      const auto v = __builtin_amdgcn_raw_buffer_load_b64(rs, (pend >> i & 1u) ? vo : OOB, i * CW * 64 * 8, 16 /* sc1 */);
       lo[i] = v[0];
       hi[i] = v[1];
     }
@@ -304,8 +323,10 @@ __device__ __forceinline__ bool gather(Ctx& x, const uint64_t* g, int n, uint32_
 #pragma unroll
     for (int i = 0; i < MAXP; ++i)
       if ((pend >> i & 1u) && hi[i] == t) {
+        // (every caller's n0 is a multiple of 256: granule i of every thread goes to the same
+        // destination, a wave-uniform branch instead of a per-lane pointer select)
         const int j = x.tid + i * CW * 64;
-        if (j < n0) dst0[j] = lo[i];
+        if (i * CW * 64 < n0) dst0[j] = lo[i];
         else dst1[j - n0] = lo[i];
         pend &= ~(1u << i);
       }
@@ -601,10 +622,10 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   struct {
     uint64_t* trace;
   } a{trace};  // (PSE_STAMP)
-  constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = G_ / PSE_AU;
+  constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = PSE_KSPLIT ? G_ : G_ / PSE_AU;
   static_assert(HU * D / 2 <= CW * 64 && D / 2 == 64, "merge: one wave per head, 2 dims per lane");
   static_assert(HU <= 4, "the unit's q rows sit in MFMA D rows 0 .. 3 (lanes 0-15)");
-  const int g = unit / PSE_AU, ku = unit % PSE_AU, h0 = ku * HU;
+  const int g = unit / PSE_AU, ku = unit % PSE_AU, h0 = PSE_KSPLIT ? 0 : ku * HU;
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
   uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
   const PseLayer& Lw = *Lp;
@@ -623,6 +644,9 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(vcache, 0, Cmax * D * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mask), 0, Cmax, 0x00020000);
   const int nchunk = pos / KW + 1;
+  // this unit's chunks [cb, ce): every chunk, or (PSE_KSPLIT) half of them
+  const int nc0 = (nchunk + 1) / 2;
+  const int cb = PSE_KSPLIT && ku ? nc0 : 0, ce = PSE_KSPLIT ? (ku ? nchunk : nc0) : nchunk;
   // a wave's 32-key chunk: K tiles (A operands), V^T fragments (B operands), mask words; keys
   // >= pos read zero (branch-free buffer loads; the new key joins in the merge)
   auto load_chunk = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
@@ -648,7 +672,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   uint32_t mkA[2];
   // this wave's chunks: w, then every CW; its q job (wave w < HU: q row w) norm weight, wave 0's
   // k norm weight, the RoPE row at pos (2 dims per lane) and the new token's mask byte
-  const int ch0 = w;
+  const int ch0 = cb + w;
   constexpr int CSTEP = CW;
   uint32_t qnw = 0, knw = 0, pcs = 0, psn = 0, mnew = 0;
   auto prefetch = [&]() {
@@ -715,7 +739,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   };
   auto chunks = [&]() {
     if (w == 0) PSE_STAMP(l, 16);
-    for (int ch = ch0; ch < nchunk; ch += CSTEP) {
+    for (int ch = ch0; ch < ce; ch += CSTEP) {
       if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
       compute(ch, ktA, vtA, mkA);
     }
@@ -755,7 +779,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
     // the new key: its score q . k (this wave's head), one more partial with p = bf16(1) = 1
     const float sn = wave_sum(bf2f(q_s[h * D + d]) * k_s[d] + bf2f(q_s[h * D + d + 1]) * k_s[d + 1]) * scale;
-    const bool nv = mnew != 0u;
+    const bool nv = mnew != 0u && (!PSE_KSPLIT || ku == 0);
     if (nv) M = fmaxf(M, sn);
     float L = 0.f, o0 = 0.f, o1 = 0.f;
 #pragma unroll
@@ -772,7 +796,17 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
       o0 += f * v_s[d];
       o1 += f * v_s[d + 1];
     }
-    st64(g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+    const uint32_t ta = tagof(x.epoch, l, OP_ATT);
+    st64(g_att + (PSE_KSPLIT ? ku * (HQ_ * D_ / 2) : 0) + (g * G * D + h0 * D + e) / 2,
+         gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, ta));
+    if (PSE_KSPLIT && d == 0) {  // this unit's (max, sum) of head g G + h
+      uint64_t* gm = g_att + 2 * (HQ_ * D_ / 2);
+#pragma unroll
+      for (int dd = 0; dd < 2; ++dd) {
+        st64(gm + ml_gran(g * G + h, ku, 0, dd), gran(__float_as_uint(M), ta));
+        st64(gm + ml_gran(g * G + h, ku, 1, dd), gran(__float_as_uint(L), ta));
+      }
+    }
   }
   cbar(x);
   return x.bar_gen;
@@ -1363,9 +1397,37 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         // ---------------- o_proj (+ residual) ----------------
         // (plain CUs: the o_proj slots drain into registers while the attention runs elsewhere)
         SlotCache<RC> co;
-        if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr, NoHook(),
-                              [&]() { co.drain(x, seq); }))
+        if constexpr (PSE_KSPLIT && !LONG) {
+          // the two units' rows -> xs32 + 2,048 / + 4,096 (behind the o_proj input's place), their
+          // (max, sum) -> the sums-of-squares scratch; then each thread merges its own 8 pairs
+          // (o = (w0 o0 + w1 o1) / (w0 + w1), w_k = sum_k exp(max_k - max)) into xs32 -- wave-local
+          // data throughout, as the plain gather's (no consumer barrier)
+          uint32_t* raw = xs32 + HQ_ * D_ / 2;
+          const float* ml = ssl;
+          if (!gather<17, false>(x, a.g_att, NG_ATT, tagof(epoch, l, OP_ATT), raw, 2 * (HQ_ * D_ / 2),
+                                 reinterpret_cast<uint32_t*>(ssl), NoHook(), [&]() { co.drain(x, seq); }))
+            break;
+          const int wv = wave - LW;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const int j = x.tid + CW * 64 * i;  // pair j of q head 4 i + wv
+            const float m0 = ml[64 * wv + 2 * i], l0 = ml[64 * wv + 2 * i + 1];
+            const float m1 = ml[64 * wv + 16 + 2 * i], l1 = ml[64 * wv + 16 + 2 * i + 1];
+            const float M = fmaxf(m0, m1);
+            const float w0 = m0 == -INFINITY ? 0.f : l0 * expf(m0 - M), w1 = m1 == -INFINITY ? 0.f : l1 * expf(m1 - M);
+            const float r = w0 + w1 > 0.f ? 1.0f / (w0 + w1) : 0.f;
+            const uint32_t p0 = raw[j], p1 = raw[HQ_ * D_ / 2 + j];
+            const float a0 = __uint_as_float(p0 << 16), a1 = __uint_as_float(p0 & 0xffff0000u);
+            const float b0 = __uint_as_float(p1 << 16), b1 = __uint_as_float(p1 & 0xffff0000u);
+            xs32[j] = pack2((w0 * a0 + w1 * b0) * r, (w0 * a1 + w1 * b1) * r);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr,
+                                     NoHook(), [&]() { co.drain(x, seq); })) {
           break;
+        }
         if (wave == LW) PSE_STAMP(l, 4);
         {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -1503,7 +1565,7 @@ int pse_grid(int device) {
 size_t pse_ws_bytes() {
   // granules: q|k|v partials (768 units x 16), attention (2048), h x 2 (2048), ss x 2 (256),
   // act (6144); words: error, epoch, exit count
-  return (size_t)(768 * 16 + HQ_ * D_ / 2 + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + HCNT_GC_OFF * 4 +
+  return (size_t)(768 * 16 + NG_ATT + 2 * (H_ / 2) + 2 * (H_ / 16) + I_ / 2 + NG_PART) * 8 + HCNT_GC_OFF * 4 +
          (PSE_HCNT && PSE_HTREE ? (size_t)2 * PSE_MAXL * HGRP * GCNT_STRIDE * 4 : 0) + 64;
 }
 
@@ -1512,7 +1574,7 @@ hipError_t pse_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop, boo
   PseArgs a = a0;
   uint64_t* g = reinterpret_cast<uint64_t*>(ws);
   a.g_qkv = g; g += 768 * 16;
-  a.g_att = g; g += HQ_ * D_ / 2;
+  a.g_att = g; g += NG_ATT;
   // h granules of an op immediately followed by its sums of squares: one gather range
   a.g_h[0] = g; g += H_ / 2;
   a.g_ss[0] = g; g += H_ / 16;
