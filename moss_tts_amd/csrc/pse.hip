@@ -26,8 +26,9 @@
 // neighbour: pse_nq); o_proj and down = row tile c (CU c owns residual columns 16c..16c+15 for
 // the whole step); gate|up = pairs c, c + 256, c + 512 (pse_gu_pair).  92 slots (1.47 MB) per CU
 // per layer (88 on the attention CUs, 96 on their helpers).  The attention of KV head g runs on the
-// consumers of PSE_AU CUs (pse_att_unit: unit k takes q heads k G / PSE_AU .. over every key),
-// whose loaders pause while it runs (PSE_APAUSE).  The loader stages slots through registers
+// consumers of PSE_AU = 2 CUs (pse_att_unit: unit k takes the cached keys of half k for every q head
+// of the group, and unit 0 merges unit 1's part, PSE_KSPLIT; before round 6 unit k took q heads
+// k G / 2 .. over every key), whose loaders pause while it runs (PSE_APAUSE).  The loader stages slots through registers
 // (PSE_RLOAD).  The engine takes this launch only for contexts up to its PSE range
 // (engine.cpp pse_choose).
 //
@@ -207,23 +208,19 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 #ifndef PSE_AU
 #define PSE_AU 2
 #endif
-// PSE_KSPLIT (round 6): the two units of a KV head split its cached keys (unit k the chunks of half
-// k, all G q heads) instead of its q heads (every key, G / 2 heads each).  A unit is bound by the
-// K / V bytes one CU pulls in (~50 GB/s: ~200 KB at 390 keys), which the key split halves.  Each
-// unit publishes its heads' outputs normalised by its own sum (bf16 pairs) and its (max, sum) per
-// head; every o_proj consumer merges the two partials of its columns (the gather grows from 2,048
-// to 4,352 granules).  Unit 0 adds the new key.
+// PSE_KSPLIT (round 6, default): the two units of a KV head split its cached keys -- unit k takes the
+// 32-key chunks of half k for all G q heads -- instead of its q heads (every key, G / 2 heads each).  A
+// unit is bound by the K / V bytes its CU pulls in (~200 KB at 390 keys, ~50 GB/s per CU), which the
+// key split halves.  The pair merges itself: unit 1 (no k / v gather, no new key) publishes its
+// unnormalised rows (fp32) and its (max, sum) per head (KS_N granules per KV head, in the long form's
+// partial buffer, which the short form does not use), and unit 0 folds them into its own merge with
+// the new key, so the o_proj gather keeps its 2,048 granules.  0: the head split.
 #ifndef PSE_KSPLIT
-#define PSE_KSPLIT 0
+#define PSE_KSPLIT 1
 #endif
 static_assert(!PSE_KSPLIT || PSE_AU == 2, "the key split pairs the two units of a KV head");
-// attention output granules: the merged rows (2,048), or with PSE_KSPLIT the two units' rows
-// [unit][head][64 pairs] and their (max, sum) per head, 256 granules (ml_gran)
-constexpr int NG_ATT = PSE_KSPLIT ? 2 * (HQ_ * D_ / 2) + 256 : HQ_ * D_ / 2;
-// (PSE_KSPLIT) the (max | sum) granule of q head hq of unit ku: o_proj consumer wave hq % 4 holds
-// the o pairs of head hq, so its lanes gather exactly the (max, sum) values they merge with; each
-// value is published twice (d = 0, 1) so that every lane of the 256 takes one
-__host__ __device__ inline int ml_gran(int hq, int ku, int f, int d) { return 64 * (hq % 4) + 32 * d + 16 * ku + 2 * (hq / 4) + f; }
+constexpr int KS_N = G_ * D_ + 2 * G_;
+constexpr int NG_ATT = HQ_ * D_ / 2;  // attention output granules
 __host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
   return (d >= 0 && d % 7 == 0 && d / 7 < HKV_ * PSE_AU) ? d / 7 : -1;
@@ -289,6 +286,10 @@ __device__ __forceinline__ void cbar(Ctx& x) {
 template <bool B>
 struct BoolC {
   static constexpr bool value = B;
+};
+template <int V>
+struct IntC {
+  static constexpr int value = V;
 };
 struct NoHook {
   __device__ void operator()() const {}
@@ -613,8 +614,11 @@ __device__ __forceinline__ float red_get(Ctx& x, int r, int row) {
 #else
 #define PSE_ATT_INL __forceinline__
 #endif
+// (KU: the unit's role under PSE_KSPLIT as a template argument, one callee per role: a runtime role
+// joined both roles' register peaks into one callee-saved set; -1 without the key split)
+template <int KU>
 __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask, const bf16_t* cos_t,
-                                     const bf16_t* sin_t, uint64_t* g_qkv, uint64_t* g_att, uint32_t* err,
+                                     const bf16_t* sin_t, uint64_t* g_qkv, uint64_t* g_att, uint64_t* g_pp, uint32_t* err,
                                      uint64_t* trace, float eps, float scale, int Cmax, uint32_t epoch, int bar_gen,
                                      int l, int unit, uint32_t tq) {
   const int c = blockIdx.x;
@@ -625,7 +629,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = PSE_KSPLIT ? G_ : G_ / PSE_AU;
   static_assert(HU * D / 2 <= CW * 64 && D / 2 == 64, "merge: one wave per head, 2 dims per lane");
   static_assert(HU <= 4, "the unit's q rows sit in MFMA D rows 0 .. 3 (lanes 0-15)");
-  const int g = unit / PSE_AU, ku = unit % PSE_AU, h0 = PSE_KSPLIT ? 0 : ku * HU;
+  const int g = unit / PSE_AU, ku = KU >= 0 ? KU : unit % PSE_AU, h0 = PSE_KSPLIT ? 0 : ku * HU;
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
   uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
   const PseLayer& Lw = *Lp;
@@ -745,12 +749,17 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     }
     if (w == 0) PSE_STAMP(l, 17);
   };
-  if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + G * (D_ / 16) * 32, NKV, tq,
-                                               graw32 + G * (D_ / 16) * 32, NKV, nullptr, chunks))
+  if (PSE_KSPLIT && ku == 1) {  // (only unit 0 takes the new token's k / v)
+    chunks();
+    if (failed(x)) return -1;
+  } else if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, g_qkv + (size_t)g * NG + G * (D_ / 16) * 32, NKV, tq,
+                                                      graw32 + G * (D_ / 16) * 32, NKV, nullptr, chunks)) {
     return -1;
+  }
   if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 18);
   // ---- 3. k (wave 0) and v (wave 1); unit 0 appends them ----
-  if (w == 0) {
+  if (PSE_KSPLIT && ku == 1) {
+  } else if (w == 0) {
     float o0, o1;
     norm_rope(val(G * (D / 16), 2 * lane), val(G * (D / 16), 2 * lane + 1), knw, o0, o1);
     k_s[2 * lane] = o0;
@@ -771,6 +780,13 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   }
   cbar(x);
   if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 19);
+  // (PSE_KSPLIT) unit 0: the partner's rows and (max, sum) per head -> graw (the q|k|v partials are
+  // consumed: q in q_s, k / v in k_s / v_s)
+  const float* pp = reinterpret_cast<const float*>(graw);
+  if (PSE_KSPLIT && ku == 0 &&
+      !gather<(KS_N + CW * 64 - 1) / (CW * 64)>(x, g_pp + (size_t)g * KS_N, KS_N, tagof(x.epoch, l, OP_ATT), graw32,
+                                                 KS_N))
+    return -1;
   // ---- 4. merge (thread e / 2: 2 output dims of local head h = wave w) and publish ----
   const int e = 2 * x.tid, h = e / D, d = e % D;
   if (e < HU * D) {
@@ -797,16 +813,25 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
       o1 += f * v_s[d + 1];
     }
     const uint32_t ta = tagof(x.epoch, l, OP_ATT);
-    st64(g_att + (PSE_KSPLIT ? ku * (HQ_ * D_ / 2) : 0) + (g * G * D + h0 * D + e) / 2,
-         gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, ta));
-    if (PSE_KSPLIT && d == 0) {  // this unit's (max, sum) of head g G + h
-      uint64_t* gm = g_att + 2 * (HQ_ * D_ / 2);
-#pragma unroll
-      for (int dd = 0; dd < 2; ++dd) {
-        st64(gm + ml_gran(g * G + h, ku, 0, dd), gran(__float_as_uint(M), ta));
-        st64(gm + ml_gran(g * G + h, ku, 1, dd), gran(__float_as_uint(L), ta));
+    if (PSE_KSPLIT && ku == 1) {  // this unit's part, unnormalised, against its own max
+      uint64_t* q = g_pp + (size_t)g * KS_N;
+      st64(q + h * D + d, gran(__float_as_uint(o0), ta));
+      st64(q + h * D + d + 1, gran(__float_as_uint(o1), ta));
+      if (d == 0) {
+        st64(q + G * D + 2 * h, gran(__float_as_uint(M), ta));
+        st64(q + G * D + 2 * h + 1, gran(__float_as_uint(L), ta));
       }
     }
+    if (PSE_KSPLIT && ku == 0) {  // the partner's part: rescaled to the joint max
+      const float m1 = pp[G * D + 2 * h], l1 = pp[G * D + 2 * h + 1];
+      const float Mj = fmaxf(M, m1);
+      const float f0 = (M == -INFINITY) ? 0.f : expf(M - Mj), f1 = (m1 == -INFINITY) ? 0.f : expf(m1 - Mj);
+      L = f0 * L + f1 * l1;
+      o0 = f0 * o0 + f1 * pp[h * D + d];
+      o1 = f0 * o1 + f1 * pp[h * D + d + 1];
+    }
+    if (!(PSE_KSPLIT && ku == 1))
+      st64(g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, ta));
   }
   cbar(x);
   return x.bar_gen;
@@ -1369,8 +1394,11 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         // ---------------- attention (one CU per KV head) ----------------
         if constexpr (ATT) {
           // the head's q|k|v partials (grouped by KV head, qkv_gran): [tile][half][16]
-          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.err, a.trace,
-                                   a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
+          auto att = [&](auto ku_c) {
+            return attention<decltype(ku_c)::value>(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.g_part,
+                                                    a.err, a.trace, a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
+          };
+          const int bg = !PSE_KSPLIT ? att(IntC<-1>{}) : (att_u % PSE_AU == 0 ? att(IntC<0>{}) : att(IntC<1>{}));
           const bool att_ok = bg >= 0;
           if (att_ok) x.bar_gen = bg;
           if (PSE_APAUSE == 2 && x.tid == 0)  // (PSE_APAUSE 2: the loader waits out the whole attention)
@@ -1397,37 +1425,9 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         // ---------------- o_proj (+ residual) ----------------
         // (plain CUs: the o_proj slots drain into registers while the attention runs elsewhere)
         SlotCache<RC> co;
-        if constexpr (PSE_KSPLIT && !LONG) {
-          // the two units' rows -> xs32 + 2,048 / + 4,096 (behind the o_proj input's place), their
-          // (max, sum) -> the sums-of-squares scratch; then each thread merges its own 8 pairs
-          // (o = (w0 o0 + w1 o1) / (w0 + w1), w_k = sum_k exp(max_k - max)) into xs32 -- wave-local
-          // data throughout, as the plain gather's (no consumer barrier)
-          uint32_t* raw = xs32 + HQ_ * D_ / 2;
-          const float* ml = ssl;
-          if (!gather<17, false>(x, a.g_att, NG_ATT, tagof(epoch, l, OP_ATT), raw, 2 * (HQ_ * D_ / 2),
-                                 reinterpret_cast<uint32_t*>(ssl), NoHook(), [&]() { co.drain(x, seq); }))
-            break;
-          const int wv = wave - LW;
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const int j = x.tid + CW * 64 * i;  // pair j of q head 4 i + wv
-            const float m0 = ml[64 * wv + 2 * i], l0 = ml[64 * wv + 2 * i + 1];
-            const float m1 = ml[64 * wv + 16 + 2 * i], l1 = ml[64 * wv + 16 + 2 * i + 1];
-            const float M = fmaxf(m0, m1);
-            const float w0 = m0 == -INFINITY ? 0.f : l0 * expf(m0 - M), w1 = m1 == -INFINITY ? 0.f : l1 * expf(m1 - M);
-            const float r = w0 + w1 > 0.f ? 1.0f / (w0 + w1) : 0.f;
-            const uint32_t p0 = raw[j], p1 = raw[HQ_ * D_ / 2 + j];
-            const float a0 = __uint_as_float(p0 << 16), a1 = __uint_as_float(p0 & 0xffff0000u);
-            const float b0 = __uint_as_float(p1 << 16), b1 = __uint_as_float(p1 & 0xffff0000u);
-            xs32[j] = pack2((w0 * a0 + w1 * b0) * r, (w0 * a1 + w1 * b1) * r);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        } else if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr,
-                                     NoHook(), [&]() { co.drain(x, seq); })) {
+        if (!gather<8, false>(x, a.g_att, HQ_ * D_ / 2, tagof(epoch, l, OP_ATT), xs32, HQ_ * D_ / 2, nullptr, NoHook(),
+                              [&]() { co.drain(x, seq); }))
           break;
-        }
         if (wave == LW) PSE_STAMP(l, 4);
         {
           f32x4 acc = (f32x4){0.f, 0.f, 0.f, 0.f};
