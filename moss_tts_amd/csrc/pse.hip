@@ -206,7 +206,7 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 // (attention() below).  Unit index u = g * PSE_AU + k runs on CU P - 1 - 7 u (spread over the
 // XCDs under round-robin placement); -1: no attention unit.
 #ifndef PSE_AU
-#define PSE_AU 2
+#define PSE_AU 4
 #endif
 // PSE_KSPLIT (round 6, default): the two units of a KV head split its cached keys -- unit k takes the
 // 32-key chunks of half k for all G q heads -- instead of its q heads (every key, G / 2 heads each).  A
@@ -218,8 +218,12 @@ size_t pse_lds_bytes() { return (size_t)L_END; }
 #ifndef PSE_KSPLIT
 #define PSE_KSPLIT 1
 #endif
-static_assert(!PSE_KSPLIT || PSE_AU == 2, "the key split pairs the two units of a KV head");
-constexpr int KS_N = G_ * D_ + 2 * G_;
+static_assert(!PSE_KSPLIT || PSE_AU == 2 || PSE_AU == 4, "key split: 2 or 4 units per KV head");
+// a KV head's partials in the long form's buffer: the rows of units 1 .. AU-1 ([AU-1][G][D] fp32), then their
+// (max, sum) per head ([AU-1][G][2]); unit 0 gathers them as one range (rows -> graw, the rest -> L_MISC)
+constexpr int KS_ROWS = G_ * D_, KS_N = (PSE_AU - 1) * (G_ * D_ + 2 * G_);
+static_assert(!PSE_KSPLIT || ((PSE_AU - 1) * KS_ROWS % 256 == 0 && (PSE_AU - 1) * KS_ROWS <= 1536),
+              "the partners' rows fill whole gather rounds and fit graw");
 constexpr int NG_ATT = HQ_ * D_ / 2;  // attention output granules
 __host__ __device__ inline int pse_att_unit(int c, int P) {
   const int d = P - 1 - c;
@@ -629,7 +633,7 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = PSE_KSPLIT ? G_ : G_ / PSE_AU;
   static_assert(HU * D / 2 <= CW * 64 && D / 2 == 64, "merge: one wave per head, 2 dims per lane");
   static_assert(HU <= 4, "the unit's q rows sit in MFMA D rows 0 .. 3 (lanes 0-15)");
-  const int g = unit / PSE_AU, ku = KU >= 0 ? KU : unit % PSE_AU, h0 = PSE_KSPLIT ? 0 : ku * HU;
+  const int g = unit / PSE_AU, ku = KU >= 0 ? KU : unit % PSE_AU, h0 = PSE_KSPLIT ? 0 : ku * HU;  // (ku: the role)
   const float* graw = reinterpret_cast<const float*>(pse_lds + L_GRAW);
   uint32_t* graw32 = reinterpret_cast<uint32_t*>(pse_lds + L_GRAW);
   const PseLayer& Lw = *Lp;
@@ -648,9 +652,10 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(vcache, 0, Cmax * D * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mask), 0, Cmax, 0x00020000);
   const int nchunk = pos / KW + 1;
-  // this unit's chunks [cb, ce): every chunk, or (PSE_KSPLIT) half of them
-  const int nc0 = (nchunk + 1) / 2;
-  const int cb = PSE_KSPLIT && ku ? nc0 : 0, ce = PSE_KSPLIT ? (ku ? nchunk : nc0) : nchunk;
+  // this unit's chunks [cb, ce): every chunk, or (PSE_KSPLIT) its 1 / PSE_AU share (unit 0, which also
+  // takes the new key and the partners' parts, gets the smaller share of an uneven split)
+  const int kk = unit % PSE_AU;
+  const int cb = PSE_KSPLIT ? kk * nchunk / PSE_AU : 0, ce = PSE_KSPLIT ? (kk + 1) * nchunk / PSE_AU : nchunk;
   // a wave's 32-key chunk: K tiles (A operands), V^T fragments (B operands), mask words; keys
   // >= pos read zero (branch-free buffer loads; the new key joins in the merge)
   auto load_chunk = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
@@ -780,12 +785,13 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
   }
   cbar(x);
   if (PSE_TRACE2 && w == 0) PSE_STAMP(l, 19);
-  // (PSE_KSPLIT) unit 0: the partner's rows and (max, sum) per head -> graw (the q|k|v partials are
-  // consumed: q in q_s, k / v in k_s / v_s)
+  // (PSE_KSPLIT) unit 0: the partners' rows -> graw (the q|k|v partials are consumed: q in q_s, k / v in
+  // k_s / v_s), their (max, sum) per head -> the sums-of-squares scratch (free through the attention)
   const float* pp = reinterpret_cast<const float*>(graw);
+  const float* pml = reinterpret_cast<const float*>(pse_lds + L_MISC);
   if (PSE_KSPLIT && ku == 0 &&
       !gather<(KS_N + CW * 64 - 1) / (CW * 64)>(x, g_pp + (size_t)g * KS_N, KS_N, tagof(x.epoch, l, OP_ATT), graw32,
-                                                 KS_N))
+                                                 (PSE_AU - 1) * KS_ROWS, reinterpret_cast<uint32_t*>(pse_lds + L_MISC)))
     return -1;
   // ---- 4. merge (thread e / 2: 2 output dims of local head h = wave w) and publish ----
   const int e = 2 * x.tid, h = e / D, d = e % D;
@@ -815,20 +821,30 @@ __device__ PSE_ATT_INL int attention(const PseLayer* Lp, const int* pos_p, const
     const uint32_t ta = tagof(x.epoch, l, OP_ATT);
     if (PSE_KSPLIT && ku == 1) {  // this unit's part, unnormalised, against its own max
       uint64_t* q = g_pp + (size_t)g * KS_N;
-      st64(q + h * D + d, gran(__float_as_uint(o0), ta));
-      st64(q + h * D + d + 1, gran(__float_as_uint(o1), ta));
+      const int pi = kk - 1;
+      st64(q + pi * KS_ROWS + h * D + d, gran(__float_as_uint(o0), ta));
+      st64(q + pi * KS_ROWS + h * D + d + 1, gran(__float_as_uint(o1), ta));
       if (d == 0) {
-        st64(q + G * D + 2 * h, gran(__float_as_uint(M), ta));
-        st64(q + G * D + 2 * h + 1, gran(__float_as_uint(L), ta));
+        st64(q + (PSE_AU - 1) * KS_ROWS + pi * 2 * G + 2 * h, gran(__float_as_uint(M), ta));
+        st64(q + (PSE_AU - 1) * KS_ROWS + pi * 2 * G + 2 * h + 1, gran(__float_as_uint(L), ta));
       }
     }
-    if (PSE_KSPLIT && ku == 0) {  // the partner's part: rescaled to the joint max
-      const float m1 = pp[G * D + 2 * h], l1 = pp[G * D + 2 * h + 1];
-      const float Mj = fmaxf(M, m1);
-      const float f0 = (M == -INFINITY) ? 0.f : expf(M - Mj), f1 = (m1 == -INFINITY) ? 0.f : expf(m1 - Mj);
-      L = f0 * L + f1 * l1;
-      o0 = f0 * o0 + f1 * pp[h * D + d];
-      o1 = f0 * o1 + f1 * pp[h * D + d + 1];
+    if (PSE_KSPLIT && ku == 0) {  // the partners' parts, in unit order: everything rescaled to the joint max
+      float Mj = M;
+#pragma unroll
+      for (int pi = 0; pi < PSE_AU - 1; ++pi) Mj = fmaxf(Mj, pml[pi * 2 * G + 2 * h]);
+      const float f0 = (M == -INFINITY) ? 0.f : expf(M - Mj);
+      L *= f0;
+      o0 *= f0;
+      o1 *= f0;
+#pragma unroll
+      for (int pi = 0; pi < PSE_AU - 1; ++pi) {
+        const float mp = pml[pi * 2 * G + 2 * h];
+        const float fp = (mp == -INFINITY) ? 0.f : expf(mp - Mj);
+        L += fp * pml[pi * 2 * G + 2 * h + 1];
+        o0 += fp * pp[pi * KS_ROWS + h * D + d];
+        o1 += fp * pp[pi * KS_ROWS + h * D + d + 1];
+      }
     }
     if (!(PSE_KSPLIT && ku == 1))
       st64(g_att + (g * G * D + h0 * D + e) / 2, gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, ta));
@@ -1398,6 +1414,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
             return attention<decltype(ku_c)::value>(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.g_part,
                                                     a.err, a.trace, a.eps, a.scale, a.Cmax, epoch, x.bar_gen, l, att_u, tq);
           };
+          // (key split: role 0 = unit 0 of its KV head, 1 = the others)
           const int bg = !PSE_KSPLIT ? att(IntC<-1>{}) : (att_u % PSE_AU == 0 ? att(IntC<0>{}) : att(IntC<1>{}));
           const bool att_ok = bg >= 0;
           if (att_ok) x.bar_gen = bg;
