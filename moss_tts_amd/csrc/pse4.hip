@@ -115,10 +115,20 @@ __device__ __forceinline__ int gu_pair(int c, int j) { return c + 256 * j; }
 
 }  // namespace
 
-// attention units: one per (row, KV head) -- unit u = row * 8 + head on CU P - 1 - 7 u
+// PSE4_KS (round 6): attention units per (row, KV head), splitting its cached keys (pse.hip PSE_KSPLIT):
+// unit k takes the 32-key chunks of share k for the head's 4 q heads; units 1 .. KS-1 publish their
+// unnormalised rows and (max, sum) per head, unit 0 folds them in with the new key.  1: one unit.
+#ifndef PSE4_KS
+#define PSE4_KS 1
+#endif
+static_assert(PSE4_KS == 1 || PSE4_KS == 2, "1 or 2 units per (row, KV head)");
+constexpr int AUS = PSE4_KS == 1 ? 7 : 3;  // CU spacing of the units (every XCD under round-robin placement)
+// (PSE4_KS 2) a (row, KV head)'s partner part: rows [G][D] fp32, then (max, sum) per head
+constexpr int KS_ROWS = G_ * D_, KS_N = (PSE4_KS - 1) * (G_ * D_ + 2 * G_);
+// attention units: unit u = (row * 8 + head) * KS + k on CU P - 1 - AUS u
 __host__ __device__ inline int pse4_att_unit(int c, int P) {
   const int d = P - 1 - c;
-  return (d >= 0 && d % 7 == 0 && d / 7 < HKV_ * NB) ? d / 7 : -1;
+  return (d >= 0 && d % AUS == 0 && d / AUS < HKV_ * NB * PSE4_KS) ? d / AUS : -1;
 }
 __host__ __device__ inline int pse4_nq(int c, int P) {
   return pse4_att_unit(c, P) >= 0 ? 2 : (pse4_att_unit(c + 1, P) >= 0 ? 4 : 3);
@@ -212,6 +222,10 @@ struct NoHook {
 template <bool B>
 struct BoolC4 {
   static constexpr bool value = B;
+};
+template <int V>
+struct IntC4 {
+  static constexpr int value = V;
 };
 // Gather granules g[0..n) carrying tag t into LDS words (the first n0 to dst0, the rest to dst1):
 // every consumer thread takes granules tid + 256 k in ONE sweep loop (pse.hip `gather`), then a
@@ -521,15 +535,19 @@ __device__ __forceinline__ float red_get(int r, int col, int row) {
 // merged in a fixed order, the 4 x D outputs published as granules.  Not inlined (its chunk
 // state would push the layer loop's allocation past the budget).  Returns the barrier count, -1
 // on a failed wait.
+// (KU: the unit's role with PSE4_KS 2, one callee per role; 0 without the key split)
+template <int KU>
 __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int* pos_p, const uint8_t* mask_all,
                                                    const bf16_t* cos_t, const bf16_t* sin_t, uint64_t* g_qkv,
-                                                   uint64_t* g_att, int* hcnt, uint32_t* go, uint32_t* err, uint64_t* trace,
+                                                   uint64_t* g_att, uint64_t* g_pp, int* hcnt, uint32_t* go, uint32_t* err,
+                                                   uint64_t* trace,
                                                    float eps, float scale, int Cmax,
                                                    uint32_t epoch, int bar_gen, int l, int unit, uint32_t tq) {
   Ctx x{err, eps, (int)blockIdx.x, (int)(threadIdx.x & 63), (int)(threadIdx.x >> 6), (int)threadIdx.x - LW * 64,
         epoch, bar_gen};
   constexpr int D = D_, G = G_, KW = 32, QS = D / 32, DT = D / 16, HU = G_;
-  const int b = unit / HKV_, g = unit % HKV_;
+  const int pair = unit / PSE4_KS, kk = unit % PSE4_KS;
+  const int b = pair / HKV_, g = pair % HKV_;
   const float* graw = reinterpret_cast<const float*>(p4_lds + L_GRAW);
   uint32_t* graw32 = reinterpret_cast<uint32_t*>(p4_lds + L_GRAW);
   const PseLayer& Lw = *Lp;
@@ -549,6 +567,7 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
   const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc(vcache, 0, Cmax * D * 2, 0x00020000);
   const __amdgpu_buffer_rsrc_t mrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(mask), 0, Cmax, 0x00020000);
   const int nchunk = pos / KW + 1;
+  const int cb = kk * nchunk / PSE4_KS, ce = (kk + 1) * nchunk / PSE4_KS;  // this unit's chunks
   auto load_chunk = [&](int ch, u32x4 (&kt)[2][QS], u32x4 (&vt)[DT], uint32_t (&mk)[2]) {
     const int k0 = ch * KW;
 #pragma unroll
@@ -570,7 +589,7 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
   };
   u32x4 ktA[2][QS], vtA[DT];
   uint32_t mkA[2];
-  const int ch0 = w;
+  const int ch0 = cb + w;
   uint32_t qnw = 0, knw = 0, pcs = 0, psn = 0, mnew = 0;
   auto prefetch = [&]() {
     load_chunk(ch0, ktA, vtA, mkA);
@@ -645,18 +664,23 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
       if (ch + CW < nchunk) load_chunk(ch + CW, ktB, vtB, mkB);
     }
 #else
-    for (int ch = ch0; ch < nchunk; ch += CW) {
+    for (int ch = ch0; ch < ce; ch += CW) {
       if (ch != ch0) load_chunk(ch, ktA, vtA, mkA);
       compute(ch, ktA, vtA, mkA);
     }
 #endif
   };
-  if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, gq + G * (D_ / 16) * 32, NKV, tq, graw32 + G * (D_ / 16) * 32, NKV,
-                                               nullptr, chunks))
+  if (KU == 1) {  // (only unit 0 takes the new token's k / v)
+    chunks();
+    if (failed(x)) return -1;
+  } else if (!gather<(NKV + CW * 64 - 1) / (CW * 64)>(x, gq + G * (D_ / 16) * 32, NKV, tq, graw32 + G * (D_ / 16) * 32,
+                                                      NKV, nullptr, chunks)) {
     return -1;
+  }
   P4_ASTAMP(17);
   // ---- 3. k (wave 0) and v (wave 1), appended at pos ----
-  if (w == 0) {
+  if (KU == 1) {
+  } else if (w == 0) {
     float o0, o1;
     norm_rope(val(G * (D / 16), 2 * lane), val(G * (D / 16), 2 * lane + 1), knw, o0, o1);
     k_s[2 * lane] = o0;
@@ -674,6 +698,15 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
     ml_s[(w * HU + lane) * 2 + 1] = l_run;
   }
   cbar(x);
+  // (PSE4_KS 2) unit 0: the partner's rows -> graw (q / k / v are in q_s / k_s / v_s), its (max, sum)
+  // per head -> the sums-of-squares scratch (free through the attention)
+  const float* pp = graw;
+  const float* pml = reinterpret_cast<const float*>(p4_lds + L_MISC);
+  if constexpr (PSE4_KS > 1 && KU == 0) {
+    if (!gather<(KS_N + CW * 64 - 1) / (CW * 64)>(x, g_pp + (size_t)pair * KS_N, KS_N, tagof(x.epoch, l, OP_ATT), graw32,
+                                                  (PSE4_KS - 1) * KS_ROWS, reinterpret_cast<uint32_t*>(p4_lds + L_MISC)))
+      return -1;
+  }
   // ---- 4. merge (thread e / 2: 2 dims of local head e / D) and publish ----
   const int e = 2 * x.tid, h = e / D, d = e % D;
   {
@@ -681,7 +714,7 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
 #pragma unroll
     for (int ww = 0; ww < CW; ++ww) M = fmaxf(M, ml_s[(ww * HU + h) * 2]);
     const float sn = wave_sum(bf2f(q_s[h * D + d]) * k_s[d] + bf2f(q_s[h * D + d + 1]) * k_s[d + 1]) * scale;
-    const bool nv = mnew != 0u;
+    const bool nv = mnew != 0u && KU == 0;
     if (nv) M = fmaxf(M, sn);
     float L = 0.f, o0 = 0.f, o1 = 0.f;
 #pragma unroll
@@ -698,15 +731,44 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
       o0 += f * v_s[d];
       o1 += f * v_s[d + 1];
     }
-    if (P4_AFLAG)  // rows bf16 [4][4096] over the granule region; one arrival below
-      st32(reinterpret_cast<bf16_t*>(g_att) + (size_t)b * HQ_ * D_ + (g * G + h) * D + d, L > 0.f ? pack2(o0 / L, o1 / L) : 0u);
-    else
-      st64(g_att + xword(b, (g * G + h) * D + d), gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+    if (KU == 1) {  // this unit's part, unnormalised, against its own max
+      const uint32_t ta = tagof(x.epoch, l, OP_ATT);
+      uint64_t* q = g_pp + (size_t)pair * KS_N;
+      const int pi = kk - 1;
+      st64(q + pi * KS_ROWS + h * D + d, gran(__float_as_uint(o0), ta));
+      st64(q + pi * KS_ROWS + h * D + d + 1, gran(__float_as_uint(o1), ta));
+      if (d == 0) {
+        st64(q + (PSE4_KS - 1) * KS_ROWS + pi * 2 * G + 2 * h, gran(__float_as_uint(M), ta));
+        st64(q + (PSE4_KS - 1) * KS_ROWS + pi * 2 * G + 2 * h + 1, gran(__float_as_uint(L), ta));
+      }
+    } else {
+      if (PSE4_KS > 1) {  // the partners' parts, in unit order, rescaled to the joint max
+        float Mj = M;
+#pragma unroll
+        for (int pi = 0; pi < PSE4_KS - 1; ++pi) Mj = fmaxf(Mj, pml[pi * 2 * G + 2 * h]);
+        const float f0 = (M == -INFINITY) ? 0.f : expf(M - Mj);
+        L *= f0;
+        o0 *= f0;
+        o1 *= f0;
+#pragma unroll
+        for (int pi = 0; pi < PSE4_KS - 1; ++pi) {
+          const float mp = pml[pi * 2 * G + 2 * h];
+          const float fp = (mp == -INFINITY) ? 0.f : expf(mp - Mj);
+          L += fp * pml[pi * 2 * G + 2 * h + 1];
+          o0 += fp * pp[pi * KS_ROWS + h * D + d];
+          o1 += fp * pp[pi * KS_ROWS + h * D + d + 1];
+        }
+      }
+      if (P4_AFLAG)  // rows bf16 [4][4096] over the granule region; one arrival below
+        st32(reinterpret_cast<bf16_t*>(g_att) + (size_t)b * HQ_ * D_ + (g * G + h) * D + d, L > 0.f ? pack2(o0 / L, o1 / L) : 0u);
+      else
+        st64(g_att + xword(b, (g * G + h) * D + d), gran(L > 0.f ? pack2(o0 / L, o1 / L) : 0u, tagof(x.epoch, l, OP_ATT)));
+    }
   }
   if (P4_AFLAG) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   cbar(x);
   P4_ASTAMP(18);
-  if (P4_AFLAG && w == 0) harrive(x, hcnt, go, 2 * PSE_MAXL + l, HKV_ * NB);
+  if (P4_AFLAG && w == 0 && KU == 0) harrive(x, hcnt, go, 2 * PSE_MAXL + l, HKV_ * NB);
   return x.bar_gen;
 }
 
@@ -935,9 +997,13 @@ __global__ __launch_bounds__(THREADS) void pse4_kernel(PseArgs a) {
         if (wave == LW) P4_STAMP(l, 2);
         // ---------------- attention (32 units: one per row and KV head) ----------------
         if constexpr (ATT) {
-          const int bg = attention(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.hcnt, a.go, a.err, a.trace,
-                                   a.eps, a.scale,
-                                   a.Cmax, epoch, x.bar_gen, l, att_u, tq);
+          auto att = [&](auto ku_c) {
+            return attention<decltype(ku_c)::value>(a.L + l, a.pos, a.mask, a.cos_t, a.sin_t, a.g_qkv, a.g_att, a.g_part,
+                                                    a.hcnt, a.go, a.err, a.trace, a.eps, a.scale, a.Cmax, epoch, x.bar_gen,
+                                                    l, att_u, tq);
+          };
+          // (key split: role 0 = unit 0 of its (row, KV head), 1 = its partner; PSE4_KS 1: role 0 only)
+          const int bg = att_u % PSE4_KS == 0 ? att(IntC4<0>{}) : att(IntC4<1>{});
           const bool att_ok = bg >= 0;
           if (att_ok) x.bar_gen = bg;
           if (x.tid == 0) __hip_atomic_store(&P4_CTL->apause, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1088,7 +1154,7 @@ bool pse4_supported(int device, int layers, int H, int Hq, int Hkv, int D, int I
 // [2 PSE_MAXL][HGRP] one 128-byte line each (PSE4_HTREE), then the release flags
 constexpr size_t HCNT_BYTES = ((size_t)3 * PSE_MAXL + (size_t)2 * PSE_MAXL * HGRP * GCNT_STRIDE) * 4;
 size_t pse4_ws_bytes() {
-  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT) * 8 + HCNT_BYTES +
+  return (size_t)(NB * NG_QKV_ROW + NG_ATT + 2 * (NG_H + NG_SS) + NG_ACT + NB * HKV_ * KS_N) * 8 + HCNT_BYTES +
          (PSE4_HCNT == 2 ? (size_t)3 * PSE_MAXL * 256 * 128 : 0) + 64;
 }
 
@@ -1103,6 +1169,7 @@ hipError_t pse4_decode(const PseArgs& a0, void* ws, hipStream_t s, bool coop) {
   a.g_h[1] = g; g += NG_H + NG_SS;
   a.g_ss[1] = a.g_h[1] + NG_H;
   a.g_act = g; g += NG_ACT;
+  a.g_part = g; g += NB * HKV_ * KS_N;  // (PSE4_KS 2) the partner parts
   a.hcnt = reinterpret_cast<int*>(g);
   a.go = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(g) + HCNT_BYTES);
   uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(ws) + pse4_ws_bytes() - 64);
