@@ -72,7 +72,7 @@ constexpr int THREADS = (LW + CW) * 64;
 #define PSE_APAUSE 2
 #endif
 #ifndef PSE_RC
-#define PSE_RC 6  // ring slots a plain CU's consumer waves drain into registers during the attention wait
+#define PSE_RC 7  // ring slots a plain CU's consumer waves drain into registers during the attention wait
 #endif
 #ifndef PSE_TRACE2
 #define PSE_TRACE2 0  // (diagnostic: the input-norm h gather's own stamps replace the loader's)
