@@ -130,8 +130,8 @@ for name, v in rows:
     print(f"| {name} | {v:.2f} |")
 print(f"| layer period | {float(np.median(lay)):.2f} |")
 # stragglers: per CU, how far behind the median each op's completion runs (steady-state layers),
-# attention CUs (pse_att_unit: 255 - c = 7 u, u < 16) marked
-att = set(255 - 7 * u for u in range(16))
+# attention CUs (pse_att_unit: 255 - c = 7 u, u < 8 PSE_AU) marked
+att = set(255 - 7 * u for u in range(int(os.environ.get("PSE_AU", "4")) * 8))  # pse_att_unit
 for name, ev in (("o done", 5), ("gu done", 7), ("down done", 9)):
     lag = np.stack([tr[l, ev] - np.median(tr[l, ev]) for l in range(1, layers)]) / 100  # [layer, CU] us
     mean_lag = lag.mean(0)
