@@ -26,10 +26,10 @@
 // neighbour: pse_nq); o_proj and down = row tile c (CU c owns residual columns 16c..16c+15 for
 // the whole step); gate|up = pairs c, c + 256, c + 512 (pse_gu_pair).  92 slots (1.47 MB) per CU
 // per layer (88 on the attention CUs, 96 on their helpers).  The attention of KV head g runs on the
-// consumers of PSE_AU = 2 CUs (pse_att_unit: unit k takes the cached keys of half k for every q head
-// of the group, and unit 0 merges unit 1's part, PSE_KSPLIT; before round 6 unit k took q heads
-// k G / 2 .. over every key), whose loaders pause while it runs (PSE_APAUSE).  The loader stages slots through registers
-// (PSE_RLOAD).  The engine takes this launch only for contexts up to its PSE range
+// consumers of PSE_AU = 4 CUs (pse_att_unit: unit k takes the cached keys of quarter k for every q
+// head of the group, and unit 0 merges its partners' parts, PSE_KSPLIT; before round 6 each of 2 units
+// took 2 q heads over every key), whose loaders keep streaming through it (PSE_APAUSE; paused until
+// round 6).  The loader stages slots through registers (PSE_RLOAD).  The engine takes this launch only for contexts up to its PSE range
 // (engine.cpp pse_choose).
 //
 // Hand-offs: data-tagged granules (MI355X_MICROARCH.md "handoff-1to1" / "allgather"): 8 bytes
@@ -68,8 +68,12 @@ constexpr int THREADS = (LW + CW) * 64;
 #ifndef PSE_CSLEEP
 #define PSE_CSLEEP 0  // s_sleep of a consumer waiting for a ring slot
 #endif
+// PSE_APAUSE: the short form's attention CUs pause their loader -- 2 through the whole attention, 1 until the q
+// rows are in, 0 never (round 6 default: with the key-split units' quarter of the K / V reads, the stream
+// running on through the attention measured faster, 2.588-2.592 -> 2.564-2.570 ms/step).  The long form's
+// slices always pause it.
 #ifndef PSE_APAUSE
-#define PSE_APAUSE 2
+#define PSE_APAUSE 0
 #endif
 #ifndef PSE_RC
 #define PSE_RC 7  // ring slots a plain CU's consumer waves drain into registers during the attention wait
@@ -1177,7 +1181,7 @@ __global__ __launch_bounds__(THREADS) void pse_kernel_t(PseArgs a) {
         const int ev = r == 0 ? 0 : (r == rq ? 1 : (r == rq + 8 ? 2 : (r == rq + 56 ? 3 : (r == spl - 1 ? 4 : -1))));
         if (ev >= 0) ctl->lstamp[l & 1][ev] = __builtin_amdgcn_s_memrealtime();
       }
-      if (PSE_APAUSE && s0 < total)  // this CU's attention is gathering its inputs: no new loads
+      if ((PSE_APAUSE || LONG) && s0 < total)  // this CU's attention is gathering its inputs: no new loads
         for (uint32_t spins = 0; __hip_atomic_load(&ctl->apause, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
                                  !__hip_atomic_load(&ctl->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) &&
                                  spins < SPIN_LDS;
