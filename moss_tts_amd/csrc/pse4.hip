@@ -52,6 +52,11 @@ static_assert(PSE4_LC >= 0 && PSE4_LC <= 2, "region B holds two slots");
 #endif
 // PSE4_ATTF: the attention output hand-off (8,192 granules per consumer CU) in the same release-flag
 // form (with PSE4_HCNT 2)
+// PSE4_APAUSE: the attention CUs pause their loader through the attention (1, until round 6) or keep it streaming
+// (0: 3.036-3.041 -> 3.023-3.029 ms/step same box; pse.hip PSE_APAUSE)
+#ifndef PSE4_APAUSE
+#define PSE4_APAUSE 0
+#endif
 #ifndef PSE4_ADB
 #define PSE4_ADB 0  // attention: double-buffered chunk loads (A/B)
 #endif
@@ -617,7 +622,7 @@ __device__ __attribute__((noinline)) int attention(const PseLayer* Lp, const int
     o0 = rbf(rbf(n0 * c0) + rbf(sg * p0 * s0));
     o1 = rbf(rbf(n1 * c1) + rbf(sg * p1 * s1));
   };
-  if (x.tid == 0) __hip_atomic_store(&P4_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (PSE4_APAUSE && x.tid == 0) __hip_atomic_store(&P4_CTL->apause, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   // ---- 1. q (this row's q tiles of the head's 4 q heads, complete two thirds into q|k|v) ----
   constexpr int NG = (G_ + 2) * (D_ / 16) * 32;
   constexpr int NQ = HU * (D_ / 16) * 32, NKV = 2 * (D_ / 16) * 32;
